@@ -1,0 +1,201 @@
+/*
+ * gpumatch.h -- C-ABI of libgpumatch.so, the MI355X (gfx950) batched request-matching engine.
+ *
+ * Drop-in boundary (SURVEY.md §8 b).  The reference's own plugin seam is the Go interface
+ * nginx.Manager (internal/nginx/manager.go:34-50): the Configurator renders nginx config text
+ * and hands it to CreateMainConfig / CreateConfig / DeleteConfig, then calls Reload().  The
+ * classifier itself runs inside nginx worker processes (ngx_http_core_module location/server
+ * lookup, ngx_http_map_module, ngx_http_split_clients_module, the Wallarm module).
+ *
+ * A Go wrapper `gpumatch.Manager{inner nginx.Manager}` binds these entry
+ * points through cgo:
+ *   - CreateMainConfig/CreateConfig/DeleteConfig (manager.go:108-134) -> cached in the wrapper,
+ *     serialised into a generation blob (GMB1 format below) at Reload time;
+ *   - Reload (manager.go:201-225)        -> gm_load_generation(ctx, blob, len, configVersion);
+ *   - the nginx worker's per-request classification (external binary; templates
+ *     version1/nginx.ingress.tmpl, version2/nginx.virtualserver.tmpl) -> gm_match_batch;
+ *   - Prometheus-style counters (internal/metrics/collectors/manager.go:27-59) -> gm_counters,
+ *     reduced across GPUs with gm_counters_allreduce (RCCL over xGMI).
+ *
+ * Conventions: plain C types only; 0 = OK, negative = error (GM_E_*); no C++ exception crosses
+ * this boundary; gm_last_error() returns a thread-local message for the last failing call.
+ */
+#ifndef GPUMATCH_H
+#define GPUMATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GM_ABI_VERSION 1u
+
+/* ---------------------------------------------------------------- status codes */
+#define GM_OK            0
+#define GM_E_INVAL      -1   /* bad argument / malformed blob                          */
+#define GM_E_HIP        -2   /* HIP runtime error                                      */
+#define GM_E_NOGEN      -3   /* no generation loaded                                   */
+#define GM_E_OVERFLOW   -4   /* candidate / hit buffer capacity exceeded (batch void)  */
+#define GM_E_PARSE      -5   /* generation rejected: config text unparseable           */
+#define GM_E_NOMEM      -6
+#define GM_E_COMM       -7   /* RCCL error                                             */
+#define GM_E_NODEVICE   -8   /* compute call on a compile-only context                 */
+
+/* ---------------------------------------------------------------- gm_create flags */
+#define GM_CREATE_COMPILE_ONLY  0x1u  /* no HIP device: compile + stats only (host tests) */
+#define GM_CREATE_PROFILE       0x2u  /* record HIP events per stage (gm_stats_t.last_ms_*) */
+
+/* ---------------------------------------------------------------- packed request record
+ * One 64-byte header per request; payload bytes live in one byte arena.  The payload of a
+ * record is contiguous at arena[base ...] in this fixed field order (so only lengths are
+ * stored):
+ *     uri | args | hdrs | body | host | method | ruri | raddr
+ * The first four are the WAF-scanned zones.  `hdrs` is the header block exactly as parsed:
+ * lines "Name: value\r\n" (single space after ':' not required; OWS trimmed by the producer).
+ * `uri` is nginx's normalised $uri; `args` is $args without '?'; `host` is the raw Host header
+ * value (host_len == 0: header absent); `ruri` is the raw $request_uri (ruri_len == 0: derived
+ * as uri ["?" args]); `raddr` is $remote_addr text.  $request_id is the 16 raw random bytes in
+ * `rid` (nginx prints them as 32 lowercase hex digits).
+ * Records must be stored with non-decreasing `base`, 16-byte aligned (coalesced dwordx4 scans).
+ */
+typedef struct gm_req {
+    uint64_t base;          /* byte offset of the payload in the arena (16-B aligned)      */
+    uint32_t uri_len;
+    uint32_t args_len;
+    uint32_t hdr_len;
+    uint32_t body_len;
+    uint16_t host_len;
+    uint16_t method_len;
+    uint16_t ruri_len;
+    uint16_t raddr_len;
+    uint16_t port;          /* local listen port ($server_port)                             */
+    uint16_t remote_port;
+    uint8_t  flags;         /* GM_REQ_*                                                    */
+    uint8_t  pad0[3];
+    uint8_t  rid[16];       /* $request_id raw bytes                                        */
+    uint8_t  pad1[8];
+} gm_req;
+
+#define GM_REQ_HTTPS   0x01u  /* connection is TLS: $scheme = https, $https = on          */
+#define GM_REQ_HTTP2   0x02u  /* $http2 = "h2"                                            */
+#define GM_REQ_HTTP10  0x04u  /* request line protocol HTTP/1.0 (else HTTP/1.1 / HTTP/2.0) */
+
+typedef struct gm_batch {
+    const gm_req  *reqs;      /* n headers (device pointer unless GM_BATCH_HOST)          */
+    const uint8_t *arena;     /* payload arena (device pointer unless GM_BATCH_HOST)      */
+    uint64_t       arena_len;
+    uint32_t       n;
+    uint32_t       flags;     /* GM_BATCH_*                                               */
+} gm_batch;
+
+#define GM_BATCH_HOST  0x1u   /* reqs/arena/out/hit_ids are host memory: staged through HBM */
+
+/* ---------------------------------------------------------------- verdict (32 B) */
+typedef struct gm_verdict {
+    uint32_t gen;               /* generation (= nginx configVersion) that produced it     */
+    uint32_t server_id;         /* index of the selected server block (config order)       */
+    uint32_t location_id;       /* index of the URI-selected location, GM_NONE if none     */
+    uint32_t upstream_id;       /* index in the sorted upstream-name table, GM_NONE if none */
+    uint8_t  action;            /* GM_ACT_*                                                */
+    uint8_t  route_kind;        /* GM_ROUTE_*                                              */
+    uint8_t  split_bucket;      /* split_clients part, 0xFF none                          */
+    uint8_t  match_idx;         /* rules match index, 0xFF default / none                 */
+    uint16_t waf_mode;          /* GM_WAF_* of the location that reached the access phase */
+    uint16_t n_hits;            /* signature ids at hit_ids[first_hit_off ...]            */
+    uint32_t first_hit_off;
+    uint32_t status;            /* HTTP status the verdict implies (200 = proxied)         */
+} gm_verdict;
+
+#define GM_NONE 0xFFFFFFFFu
+
+enum {
+    GM_ACT_PROXY        = 0,  /* proxy_pass to upstream_id                                 */
+    GM_ACT_REDIRECT     = 1,  /* server-level `return 301` (ssl-redirect / x-forwarded-proto) */
+    GM_ACT_RETURN       = 2,  /* location `return <status>` (default server 404, health 200) */
+    GM_ACT_AUTO_301     = 3,  /* prefix location auto_redirect ($uri + "/")               */
+    GM_ACT_NOT_FOUND    = 4,  /* no location matched                                       */
+    GM_ACT_BAD_REQUEST  = 5,  /* invalid Host                                              */
+    GM_ACT_BLOCK        = 6,  /* WAF block mode with >= 1 signature hit                    */
+    GM_ACT_ERRPAGE      = 7,  /* error_page target empty (no split bucket) -> 302          */
+    GM_ACT_UNSUPPORTED  = 8,  /* location uses a construct the compiler rejected           */
+    GM_ACT_NO_LISTENER  = 9   /* no server listens on the port / TLS on a plain port      */
+};
+
+enum { GM_ROUTE_NONE = 0, GM_ROUTE_PLAIN = 1, GM_ROUTE_SPLIT = 2, GM_ROUTE_RULES = 3 };
+enum { GM_WAF_OFF = 0, GM_WAF_MONITORING = 1, GM_WAF_SAFE_BLOCKING = 2, GM_WAF_BLOCK = 3 };
+
+/* ---------------------------------------------------------------- generation blob (GMB1)
+ *   u32 magic 'GMB1' (0x31424D47) | u32 n_entries | n x { u32 kind, u32 name_len, u32 data_len,
+ *   name bytes, data bytes }     (all little-endian, no padding)
+ * kinds: main nginx.conf (CreateMainConfig), conf.d file (CreateConfig; include order = sorted
+ * file name, nginx.tmpl:128-129), signature set (text).
+ */
+#define GM_BLOB_MAGIC     0x31424D47u
+#define GM_ENTRY_MAIN     1u
+#define GM_ENTRY_CONFD    2u
+#define GM_ENTRY_SIGS     3u
+
+typedef struct gm_stats_t {
+    uint32_t gen;
+    uint32_t n_servers;
+    uint32_t n_locations;
+    uint32_t n_upstreams;
+    uint32_t n_routes_rules;
+    uint32_t n_routes_split;
+    uint32_t n_sigs;              /* signature rules accepted                           */
+    uint32_t n_sig_literals;
+    uint32_t n_sig_regex;
+    uint32_t n_sig_regex_always;  /* regexes with no >=4-byte required factor           */
+    uint32_t n_rejected_pcre;     /* regexes using PCRE-only constructs (rejected)      */
+    uint32_t n_rejected_other;    /* other constructs rejected (snippets, nested loc...) */
+    uint32_t n_dfa_states;
+    uint32_t n_counters;          /* n_locations + n_sigs                               */
+    uint64_t table_bytes;         /* device table bytes of the generation               */
+    uint64_t lds_bytes_scan;      /* LDS bytes the WAF scan stage stages per workgroup  */
+    uint64_t last_candidates;     /* WAF prefilter candidates in the last batch         */
+    uint64_t last_pairs;          /* (request, rule) hits before dedupe, last batch     */
+    uint64_t last_hits;           /* hit ids written, last batch                        */
+    /* GM_CREATE_PROFILE contexts: HIP-event times (ms) of the last batch's stages, on the
+     * caller's stream: route kernel, WAF scan kernel, verify kernel, and everything after it
+     * (regex confirm, sorts, hit emission, incl. the mid-batch host reads of counts). */
+    float    last_ms_route, last_ms_scan, last_ms_verify, last_ms_tail;
+} gm_stats_t;
+
+typedef struct gm_ctx gm_ctx;
+
+/* Create a context bound to one HIP device (one ctx per device, one process per GPU). */
+gm_ctx     *gm_create(int hip_device, uint32_t flags);
+void        gm_destroy(gm_ctx *ctx);
+uint32_t    gm_abi_version(void);
+
+/* Copy-in a new table generation.  Atomic: on any error the previous generation stays
+ * live; rejected rules are counted (gm_stats), never returned as an error. */
+int         gm_load_generation(gm_ctx *ctx, const void *blob, size_t len, uint32_t gen);
+
+/* Classify a batch.  Asynchronous on `stream` (hipStream_t; NULL = legacy default stream);
+ * out[i] receives the verdict of reqs[i]; the hit ids of request i are
+ * hit_ids[out[i].first_hit_off .. + n_hits), ascending.  gm_sync() completes the batch and
+ * reports capacity overflow. */
+int         gm_match_batch(gm_ctx *ctx, const gm_batch *in, gm_verdict *out,
+                           uint32_t *hit_ids, size_t hit_cap, void *stream);
+int         gm_sync(gm_ctx *ctx, void *stream);
+
+/* Per-location and per-signature hit counters, u64: [0, n_locations) locations,
+ * [n_locations, n_locations + n_sigs) signatures (gm_stats_t.n_counters entries). */
+int         gm_counters(gm_ctx *ctx, uint64_t *out, size_t n);
+int         gm_counters_reset(gm_ctx *ctx);
+
+/* Multi-GPU: ncclUniqueId (128 bytes) produced by rank 0 and shared by the caller. */
+int         gm_comm_unique_id(void *out_128_bytes);
+int         gm_comm_init(gm_ctx *ctx, const void *nccl_unique_id, int nranks, int rank);
+int         gm_counters_allreduce(gm_ctx *ctx, void *stream);
+
+int         gm_stats(gm_ctx *ctx, gm_stats_t *out);
+const char *gm_last_error(gm_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPUMATCH_H */

@@ -1,0 +1,21 @@
+/*
+ * gpumatch_debug.h -- host-only introspection exports of libgpumatch.so, used by the CPU test
+ * suite to check the generation compiler without a GPU (no request classification here).
+ */
+#ifndef GPUMATCH_DEBUG_H
+#define GPUMATCH_DEBUG_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* Compile `pat` with the engine's regex compiler and run the DFA on the host:
+ * 1 match, 0 no match, < 0 rejected (-1 PCRE-only, -2 unsupported, -3 syntax, -4 too big). */
+int gm_debug_regex(const char *pat, int caseless, const uint8_t *subject, size_t n);
+/* Required-literal factors ('\n'-separated, case-folded) the WAF prefilter uses for `pat`;
+ * returns the shortest factor length (0 = none), < 0 if rejected. */
+int gm_debug_regex_factors(const char *pat, int caseless, char *out, size_t cap);
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,992 @@
+// gm_compile.cpp -- generation compiler (host C++, part of libgpumatch.so).
+//
+// Input: the GMB1 blob the Manager wrapper builds from what the Configurator handed to
+// nginx.Manager (internal/nginx/manager.go:34-50): the main nginx.conf (version1/nginx.tmpl),
+// the conf.d files (version1/nginx.ingress.tmpl, version2/nginx.virtualserver.tmpl) in include
+// order, and the build-defined WAF signature set.  Output: one flat table image (gm_tables.hpp).
+//
+// The text is parsed with nginx's token rules (ngx_conf_read_token) and the directives that
+// decide a request's verdict are compiled; everything else (timeouts, headers, buffers) is
+// ignored.  Constructs the device path cannot express are counted in gm_stats_t and the
+// affected location answers GM_ACT_UNSUPPORTED; they never fail the load (SURVEY §8 b).
+#include "gm_compile.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <set>
+#include <unordered_map>
+
+#include "gm_regex.hpp"
+
+namespace gm {
+namespace {
+
+// ============================================================================ tokens
+struct Dir {
+    std::vector<std::string> a;
+    std::vector<Dir> body;
+    bool block = false;
+};
+
+class Tokenizer {
+  public:
+    Tokenizer(const char *s, size_t n) : s_(s), n_(n) {}
+    enum Ev { WORD, SEMI, OPEN, CLOSE, END, BAD };
+    Ev next(std::string &w) {
+        for (;;) {
+            while (i_ < n_ && is_ws(s_[i_])) i_++;
+            if (i_ >= n_) return END;
+            char c = s_[i_];
+            if (c == '#') { while (i_ < n_ && s_[i_] != '\n') i_++; continue; }
+            if (c == ';') { i_++; return SEMI; }
+            if (c == '{') { i_++; return OPEN; }
+            if (c == '}') { i_++; return CLOSE; }
+            w.clear();
+            if (c == '"' || c == '\'') {
+                size_t j = i_ + 1;
+                while (j < n_ && s_[j] != c) j += (s_[j] == '\\') ? 2 : 1;
+                if (j >= n_) return BAD;
+                unescape(i_ + 1, j, w);
+                i_ = j + 1;
+                if (i_ < n_ && s_[i_] == ')') pending_paren_ = true;   // "...") -> extra ")" token
+                else if (i_ < n_ && !is_ws(s_[i_]) && s_[i_] != ';' && s_[i_] != '{') return BAD;
+                return WORD;
+            }
+            size_t j = i_;
+            bool dollar = false;
+            while (j < n_) {
+                char ch = s_[j];
+                if (ch == '{' && dollar) { j++; continue; }
+                dollar = false;
+                if (ch == '\\' && j + 1 < n_) { j += 2; continue; }
+                if (ch == '$') { dollar = true; j++; continue; }
+                if (is_ws(ch) || ch == ';' || ch == '{') break;
+                j++;
+            }
+            unescape(i_, j, w);
+            i_ = j;
+            return WORD;
+        }
+    }
+    bool take_paren() { if (pending_paren_) { pending_paren_ = false; i_++; return true; } return false; }
+
+  private:
+    static bool is_ws(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n'; }
+    void unescape(size_t a, size_t b, std::string &w) {
+        for (size_t k = a; k < b; k++) {
+            if (s_[k] == '\\' && k + 1 < b) {
+                char e = s_[k + 1];
+                const char *m = strchr("\"'\\", e);
+                if (m) { w.push_back(e); k++; continue; }
+                if (e == 't') { w.push_back('\t'); k++; continue; }
+                if (e == 'r') { w.push_back('\r'); k++; continue; }
+                if (e == 'n') { w.push_back('\n'); k++; continue; }
+            }
+            w.push_back(s_[k]);
+        }
+    }
+    const char *s_;
+    size_t n_, i_ = 0;
+    bool pending_paren_ = false;
+};
+
+bool parse_body(Tokenizer &T, std::vector<Dir> &out, bool nested) {
+    Dir cur;
+    std::string w;
+    for (;;) {
+        auto ev = T.next(w);
+        switch (ev) {
+        case Tokenizer::WORD:
+            cur.a.push_back(w);
+            if (T.take_paren()) cur.a.push_back(")");
+            break;
+        case Tokenizer::SEMI:
+            if (cur.a.empty()) return false;
+            out.push_back(std::move(cur)); cur = Dir();
+            break;
+        case Tokenizer::OPEN:
+            cur.block = true;
+            if (!parse_body(T, cur.body, true)) return false;
+            out.push_back(std::move(cur)); cur = Dir();
+            break;
+        case Tokenizer::CLOSE:
+            return nested && cur.a.empty();
+        case Tokenizer::END:
+            return !nested && cur.a.empty();
+        case Tokenizer::BAD:
+            return false;
+        }
+    }
+}
+
+// ============================================================================ IR
+enum LocKind { PFX, EXACT, NOREGEX, RX, RXI, NAMED };
+struct Loc {
+    int id = 0, server = 0;
+    LocKind kind = PFX;
+    std::string path;
+    bool has_proxy = false, has_return = false, nested = false;
+    std::string ups, err418;
+    int code = 0;
+    int waf = -1;
+};
+struct SIf { std::string var; int op = 0; std::string val; int code = 0; bool ret_only = false; };
+struct Server {
+    int id = 0, waf = GM_WAF_OFF;
+    std::vector<std::pair<int, int>> listens;   // port, flags (1 ssl, 2 default)
+    std::vector<std::string> names;
+    std::vector<SIf> ifs;
+    std::vector<int> locs;
+};
+struct MapIR {
+    std::string src, var;
+    struct P { std::string key; bool rx = false, rxi = false; std::string val; };
+    std::vector<P> params;
+    bool has_default = false;
+    std::string def;
+};
+struct SplitIR { std::string src, var; std::vector<std::pair<std::string, std::string>> parts; };
+
+struct Model {
+    std::vector<Server> servers;
+    std::vector<Loc> locs;
+    std::map<std::string, MapIR> maps;
+    std::map<std::string, SplitIR> splits;
+    std::vector<std::string> upstreams;
+    int http_waf = GM_WAF_OFF;
+    uint32_t rejected_other = 0, rejected_pcre = 0;
+};
+
+int waf_mode(const std::string &s) {
+    if (s == "monitoring") return GM_WAF_MONITORING;
+    if (s == "safe_blocking") return GM_WAF_SAFE_BLOCKING;
+    if (s == "block") return GM_WAF_BLOCK;
+    return GM_WAF_OFF;
+}
+
+std::string lower(std::string s) { for (auto &c : s) if (c >= 'A' && c <= 'Z') c |= 0x20; return s; }
+
+struct Builder {
+    Model &M;
+    const std::vector<std::vector<Dir>> &confd;
+    explicit Builder(Model &m, const std::vector<std::vector<Dir>> &c) : M(m), confd(c) {}
+
+    void location(Server &S, const Dir &d) {
+        Loc L;
+        L.id = (int)M.locs.size(); L.server = S.id;
+        if (d.a.size() == 3) {
+            const std::string &m = d.a[1];
+            L.kind = m == "=" ? EXACT : m == "^~" ? NOREGEX : m == "~" ? RX : m == "~*" ? RXI : PFX;
+            if (L.kind == PFX) M.rejected_other++;
+            L.path = d.a[2];
+        } else if (d.a.size() == 2) {
+            L.path = d.a[1];
+            L.kind = (!L.path.empty() && L.path[0] == '@') ? NAMED : PFX;
+        }
+        for (const Dir &k : d.body) {
+            if (k.a.empty()) continue;
+            const std::string &n = k.a[0];
+            if (n == "proxy_pass" && k.a.size() == 2) {
+                std::string u = k.a[1];
+                size_t p = u.find("://");
+                u = p == std::string::npos ? u : u.substr(p + 3);
+                size_t e = u.find_first_of("/$");
+                L.ups = u.substr(0, e); L.has_proxy = true;
+            } else if (n == "return" && k.a.size() >= 2) {
+                L.has_return = true;
+                L.code = isdigit((unsigned char)k.a[1][0]) ? atoi(k.a[1].c_str()) : 302;
+            } else if (n == "error_page" && k.a.size() == 4 && k.a[1] == "418" && k.a[2] == "=") {
+                L.err418 = k.a[3];
+            } else if (n == "wallarm_mode" && k.a.size() == 2) {
+                L.waf = waf_mode(k.a[1]);
+            } else if (n == "location" || n == "if" || n == "rewrite") {
+                L.nested = true;
+            }
+        }
+        if (L.nested) M.rejected_other++;
+        M.locs.push_back(L);
+        S.locs.push_back(L.id);
+    }
+
+    void server(const Dir &d) {
+        Server S;
+        S.id = (int)M.servers.size();
+        S.waf = M.http_waf;
+        for (const Dir &k : d.body)
+            if (k.a.size() == 2 && k.a[0] == "wallarm_mode") S.waf = waf_mode(k.a[1]);
+        for (const Dir &k : d.body) {
+            if (k.a.empty()) continue;
+            const std::string &n = k.a[0];
+            if (n == "listen" && k.a.size() >= 2) {
+                const std::string &a = k.a[1];
+                if (a.rfind("unix:", 0) == 0) continue;
+                size_t c = a.rfind(':');
+                int port = atoi((c == std::string::npos ? a : a.substr(c + 1)).c_str());
+                int fl = 0;
+                for (size_t q = 2; q < k.a.size(); q++) {
+                    if (k.a[q] == "ssl") fl |= 1;
+                    if (k.a[q] == "default_server" || k.a[q] == "default") fl |= 2;
+                }
+                S.listens.push_back({port, fl});
+            } else if (n == "server_name") {
+                for (size_t q = 1; q < k.a.size(); q++) S.names.push_back(k.a[q][0] == '~' ? k.a[q] : lower(k.a[q]));
+            } else if (n == "if" && k.block) {
+                std::vector<std::string> a(k.a.begin() + 1, k.a.end());
+                if (!a.empty() && !a[0].empty() && a[0][0] == '(') {
+                    if (a[0].size() == 1) a.erase(a.begin()); else a[0] = a[0].substr(1);
+                }
+                if (!a.empty() && !a.back().empty() && a.back().back() == ')') {
+                    if (a.back().size() == 1) a.pop_back(); else a.back().pop_back();
+                }
+                SIf f;
+                bool has_ret = false;
+                for (const Dir &r : k.body)
+                    if (r.a.size() >= 2 && r.a[0] == "return") {
+                        has_ret = true;
+                        f.code = isdigit((unsigned char)r.a[1][0]) ? atoi(r.a[1].c_str()) : 302;
+                    }
+                if (!has_ret) continue;
+                if (a.size() == 1) { f.var = a[0]; f.op = 0; }
+                else if (a.size() == 3) {
+                    f.var = a[0]; f.val = a[2];
+                    const std::string &op = a[1];
+                    f.op = op == "=" ? 1 : op == "!=" ? 2 : op == "~" ? 3 : op == "~*" ? 4 : op == "!~" ? 5 : op == "!~*" ? 6 : -1;
+                } else f.op = -1;
+                S.ifs.push_back(f);
+            } else if (n == "return" && k.a.size() >= 2) {
+                SIf f; f.ret_only = true;
+                f.code = isdigit((unsigned char)k.a[1][0]) ? atoi(k.a[1].c_str()) : 302;
+                S.ifs.push_back(f);
+            } else if (n == "location" && k.block) {
+                location(S, k);
+            }
+        }
+        M.servers.push_back(std::move(S));
+    }
+
+    void http(const std::vector<Dir> &body) {
+        for (const Dir &d : body) {
+            if (d.a.empty()) continue;
+            const std::string &n = d.a[0];
+            if (n == "include" && d.a.size() == 2 && d.a[1].find("conf.d/") != std::string::npos) {
+                for (auto &f : confd) http(f);
+            } else if (n == "wallarm_mode" && d.a.size() == 2) {
+                M.http_waf = waf_mode(d.a[1]);
+            } else if (n == "upstream" && d.block && d.a.size() == 2) {
+                M.upstreams.push_back(d.a[1]);
+            } else if (n == "map" && d.block && d.a.size() == 3) {
+                MapIR m;
+                m.src = d.a[1]; m.var = lower(d.a[2].substr(1));
+                for (const Dir &p : d.body) {
+                    if (p.a.size() == 1 && (p.a[0] == "hostnames" || p.a[0] == "volatile")) continue;
+                    if (p.a.size() != 2) continue;
+                    if (p.a[0] == "default") { m.has_default = true; m.def = p.a[1]; continue; }
+                    if (p.a[0] == "include") continue;
+                    MapIR::P q;
+                    q.val = p.a[1];
+                    std::string k = p.a[0];
+                    if (!k.empty() && k[0] == '~') {
+                        q.rx = true;
+                        if (k.size() > 1 && k[1] == '*') { q.rxi = true; q.key = k.substr(2); }
+                        else q.key = k.substr(1);
+                    } else {
+                        if (!k.empty() && k[0] == '\\') k = k.substr(1);
+                        q.key = lower(k);
+                    }
+                    m.params.push_back(q);
+                }
+                M.maps[m.var] = m;
+            } else if (n == "split_clients" && d.block && d.a.size() == 3) {
+                SplitIR s;
+                s.src = d.a[1]; s.var = lower(d.a[2].substr(1));
+                for (const Dir &p : d.body) if (p.a.size() == 2) s.parts.push_back({p.a[0], p.a[1]});
+                M.splits[s.var] = s;
+            } else if (n == "server" && d.block) {
+                server(d);
+            }
+        }
+    }
+};
+
+// ============================================================================ image writer
+struct Image {
+    std::vector<uint8_t> buf;
+    template <class T> uint64_t put(const std::vector<T> &v) {
+        size_t off = (buf.size() + 15) & ~size_t(15);
+        buf.resize(off + v.size() * sizeof(T) + 16, 0);
+        if (!v.empty()) memcpy(buf.data() + off, v.data(), v.size() * sizeof(T));
+        buf.resize(off + v.size() * sizeof(T));
+        return off;
+    }
+};
+
+uint32_t pow2_at_least(size_t n) { uint32_t c = 16; while (c < n) c <<= 1; return c; }
+
+struct Compiler {
+    Model &M;
+    gm_stats_t &st;
+    std::vector<uint8_t> bytes;                  // shared byte pool
+    std::vector<DSrc> srcs;
+    std::map<std::string, uint32_t> src_ids;
+    std::vector<DCond> conds;
+    std::vector<uint32_t> chain_heads;
+    std::vector<DRules> rules;
+    std::vector<uint8_t> rtab;
+    std::vector<uint32_t> rtargets;
+    std::vector<DSplit> splits;
+    std::vector<DPart> parts;
+    std::vector<DDfa> dfas;
+    std::vector<uint16_t> dfa_trans;
+    std::vector<uint8_t> dfa_acc, dfa_cls;
+
+    Compiler(Model &m, gm_stats_t &s) : M(m), st(s) {}
+
+    uint32_t put_bytes(const std::string &s) {
+        uint32_t o = (uint32_t)bytes.size();
+        bytes.insert(bytes.end(), s.begin(), s.end());
+        return o;
+    }
+
+    int add_dfa(const Dfa &d) {
+        DDfa x{};
+        x.trans_off = (uint32_t)dfa_trans.size();
+        x.acc_off = (uint32_t)dfa_acc.size();
+        x.cls_off = (uint32_t)dfa_cls.size();
+        x.n_states = (uint16_t)d.n_states; x.n_classes = (uint16_t)d.n_classes;
+        x.flags = d.anchored_start ? DFA_ANCHOR_START : 0;
+        dfa_trans.insert(dfa_trans.end(), d.trans.begin(), d.trans.end());
+        dfa_acc.insert(dfa_acc.end(), d.acc.begin(), d.acc.end());
+        dfa_cls.insert(dfa_cls.end(), d.cls, d.cls + 256);
+        dfas.push_back(x);
+        st.n_dfa_states += d.n_states;
+        return (int)dfas.size() - 1;
+    }
+
+    // regex -> dfa id, or -1 (counted)
+    int regex(const std::string &pat, bool ci, Dfa *keep = nullptr) {
+        RegexInfo ri = compile_regex(pat, ci);
+        if (ri.status != RX_OK) {
+            if (ri.status == RX_PCRE_ONLY) st.n_rejected_pcre++; else st.n_rejected_other++;
+            return -1;
+        }
+        if (keep) *keep = ri.dfa;
+        return add_dfa(ri.dfa);
+    }
+
+    // request variable "$name" -> DSrc id, or -1
+    int src(const std::string &var) {
+        if (var.size() < 2 || var[0] != '$') return -1;
+        std::string n = lower(var.substr(1));
+        if (n.size() > 2 && n[0] == '{' && n.back() == '}') n = n.substr(1, n.size() - 2);
+        auto it = src_ids.find(n);
+        if (it != src_ids.end()) return (int)it->second;
+        DSrc s{};
+        static const std::map<std::string, uint8_t> vars = {
+            {"scheme", V_SCHEME}, {"https", V_HTTPS}, {"http2", V_HTTP2}, {"request_method", V_METHOD},
+            {"args", V_ARGS}, {"query_string", V_ARGS}, {"uri", V_URI}, {"document_uri", V_URI},
+            {"request_uri", V_REQUEST_URI}, {"request", V_REQUEST}, {"request_body", V_REQUEST_BODY},
+            {"remote_addr", V_REMOTE_ADDR}, {"remote_port", V_REMOTE_PORT}, {"server_port", V_SERVER_PORT},
+            {"request_id", V_REQUEST_ID}, {"host", V_HOST}};
+        auto v = vars.find(n);
+        if (v != vars.end()) { s.kind = SRC_VAR; s.var = v->second; }
+        else if (n.rfind("http_", 0) == 0 && n.size() > 5) {
+            s.kind = SRC_HTTP;
+            std::string h = n.substr(5);
+            s.join = h == "cookie" ? ';' : h == "x_forwarded_for" ? ',' : 0;
+            s.name_off = put_bytes(h); s.name_len = (uint32_t)h.size();
+        } else if (n.rfind("cookie_", 0) == 0 && n.size() > 7) {
+            s.kind = SRC_COOKIE; std::string h = n.substr(7);
+            s.name_off = put_bytes(h); s.name_len = (uint32_t)h.size();
+        } else if (n.rfind("arg_", 0) == 0 && n.size() > 4) {
+            s.kind = SRC_ARG; std::string h = n.substr(4);
+            s.name_off = put_bytes(h); s.name_len = (uint32_t)h.size();
+        } else return -1;
+        srcs.push_back(s);
+        src_ids[n] = (uint32_t)srcs.size() - 1;
+        return (int)srcs.size() - 1;
+    }
+
+    // split a complex value into $var parts; returns false if literal text is mixed in
+    static bool var_list(const std::string &v, std::vector<std::string> &out) {
+        size_t i = 0;
+        while (i < v.size()) {
+            if (v[i] != '$') return false;
+            size_t j = i + 1;
+            if (j < v.size() && v[j] == '{') {
+                size_t e = v.find('}', j);
+                if (e == std::string::npos) return false;
+                out.push_back(lower(v.substr(j + 1, e - j - 1))); i = e + 1; continue;
+            }
+            while (j < v.size() && (isalnum((unsigned char)v[j]) || v[j] == '_')) j++;
+            if (j == i + 1) return false;
+            out.push_back(lower(v.substr(i + 1, j - i - 1)));
+            i = j;
+        }
+        return !out.empty();
+    }
+
+    // chain map var -> node id (NEXT_0 / NEXT_1 for constants); INT32_MIN = unsupported
+    std::map<std::string, int32_t> chain_memo;
+    int32_t chain(const std::string &var, int depth) {
+        if (depth > 64) return INT32_MIN;
+        auto it = chain_memo.find(var);
+        if (it != chain_memo.end()) return it->second;
+        auto mit = M.maps.find(var);
+        if (mit == M.maps.end()) return INT32_MIN;
+        const MapIR &m = mit->second;
+        std::vector<std::string> sv;
+        if (!var_list(m.src, sv) || sv.size() != 1) return INT32_MIN;
+        int s = src("$" + sv[0]);
+        if (s < 0 || m.params.size() > 1) return INT32_MIN;
+        auto res = [&](const std::string &r) -> int32_t {
+            if (r == "0") return NEXT_0;
+            if (r == "1") return NEXT_1;
+            std::vector<std::string> rv;
+            if (var_list(r, rv) && rv.size() == 1) return chain(rv[0], depth + 1);
+            return INT32_MIN;
+        };
+        int32_t f = res(m.has_default ? m.def : std::string(""));
+        if (m.params.empty()) { chain_memo[var] = f; return f; }
+        const MapIR::P &p = m.params[0];
+        int32_t t = res(p.val);
+        if (t == INT32_MIN || f == INT32_MIN) return INT32_MIN;
+        DCond c{};
+        c.src = (uint32_t)s;
+        if (p.rx) {
+            int d = regex(p.key, p.rxi);
+            if (d < 0) return INT32_MIN;
+            c.is_regex = 1; c.dfa = (uint32_t)d;
+        } else {
+            c.key_off = put_bytes(p.key); c.key_len = (uint32_t)p.key.size();
+        }
+        c.next_true = t; c.next_false = f;
+        conds.push_back(c);
+        int32_t id = (int32_t)conds.size() - 1;
+        chain_memo[var] = id;
+        return id;
+    }
+
+    // IRL target "@name" -> named location id in server S; GM_NONE for empty; -2 unsupported
+    int64_t target(const Server &S, const std::string &v) {
+        if (v.empty()) return GM_NONE;
+        if (v.find('$') != std::string::npos || v[0] != '@') return -2;
+        for (int l : S.locs) if (M.locs[l].kind == NAMED && M.locs[l].path == v) return l;
+        return -2;
+    }
+
+    // rules route for IRL in server S referencing map `var`; returns DRules index or -1
+    int rules_route(const Server &S, const std::string &var) {
+        const MapIR &m = M.maps.at(var);
+        std::vector<std::string> chains;
+        if (!var_list(m.src, chains) || chains.size() > 8) return -1;
+        DRules r{};
+        r.first_chain = (uint32_t)chain_heads.size();
+        r.n_chains = (uint32_t)chains.size();
+        std::vector<uint32_t> heads;
+        for (auto &c : chains) {
+            int32_t h = chain(c, 0);
+            if (h == INT32_MIN) return -1;
+            heads.push_back((uint32_t)h);
+        }
+        // result of each param: literal "@name"
+        std::vector<uint32_t> tg;
+        std::vector<Dfa> rx(m.params.size());
+        for (size_t k = 0; k < m.params.size(); k++) {
+            int64_t t = target(S, m.params[k].val);
+            if (t == -2) return -1;
+            tg.push_back((uint32_t)t);
+            if (m.params[k].rx) {
+                RegexInfo ri = compile_regex(m.params[k].key, m.params[k].rxi);
+                if (ri.status != RX_OK) {
+                    if (ri.status == RX_PCRE_ONLY) st.n_rejected_pcre++; else st.n_rejected_other++;
+                    return -1;
+                }
+                rx[k] = ri.dfa;
+            }
+        }
+        int64_t dt = m.has_default ? target(S, m.def) : (int64_t)GM_NONE;
+        if (dt == -2) return -1;
+        // truth table over the chains' 0/1 outcomes (ngx_http_map_find: hash, then regexes)
+        r.table_off = (uint32_t)rtab.size();
+        for (uint32_t b = 0; b < (1u << chains.size()); b++) {
+            std::string s;
+            for (size_t c = 0; c < chains.size(); c++) s.push_back((b >> c) & 1 ? '1' : '0');
+            int res = -1;
+            for (size_t k = 0; k < m.params.size() && res < 0; k++)
+                if (!m.params[k].rx && m.params[k].key == s) res = (int)k;
+            for (size_t k = 0; k < m.params.size() && res < 0; k++)
+                if (m.params[k].rx && !s.empty() && dfa_search(rx[k], (const uint8_t *)s.data(), s.size())) res = (int)k;
+            rtab.push_back(res < 0 ? 0xFF : (uint8_t)res);
+        }
+        for (auto h : heads) chain_heads.push_back(h);
+        r.first_target = (uint32_t)rtargets.size();
+        r.n_targets = (uint32_t)tg.size();
+        for (auto t : tg) rtargets.push_back(t);
+        r.default_target = (uint32_t)dt;
+        rules.push_back(r);
+        return (int)rules.size() - 1;
+    }
+
+    int split_route(const Server &S, const std::string &var) {
+        const SplitIR &sp = M.splits.at(var);
+        std::vector<std::string> sv;
+        if (!var_list(sp.src, sv) || sv.size() != 1) return -1;
+        int s = src("$" + sv[0]);
+        if (s < 0) return -1;
+        DSplit d{};
+        d.first_part = (uint32_t)parts.size(); d.src = (uint32_t)s;
+        uint64_t last = 0;
+        std::vector<DPart> ps;
+        for (auto &p : sp.parts) {
+            DPart q{};
+            int64_t t = target(S, p.second);
+            if (t == -2) return -1;
+            q.target = (uint32_t)t;
+            if (p.first == "*") { q.star = 1; }
+            else {
+                // ngx_atofp(value, len - 1, 2)
+                const std::string &w = p.first;
+                if (w.empty() || w.back() != '%') return -1;
+                uint32_t pc = 0; int dec = -1;
+                for (size_t k = 0; k + 1 < w.size(); k++) {
+                    char c = w[k];
+                    if (c == '.') { if (dec >= 0) return -1; dec = 0; continue; }
+                    if (!isdigit((unsigned char)c)) return -1;
+                    if (dec >= 0) { if (dec < 2) { pc = pc * 10 + (c - '0'); dec++; } }
+                    else pc = pc * 10 + (c - '0');
+                }
+                for (int k = dec < 0 ? 0 : dec; k < 2; k++) pc *= 10;
+                last += (uint64_t)pc * 0xffffffffull / 10000;
+                q.bound = (uint32_t)last;
+            }
+            ps.push_back(q);
+        }
+        d.n_parts = (uint32_t)ps.size();
+        for (auto &q : ps) parts.push_back(q);
+        splits.push_back(d);
+        return (int)splits.size() - 1;
+    }
+};
+
+// ============================================================================ signatures
+struct SigRule { bool lit; bool nocase; int zones; std::string pat; };
+
+bool parse_sigs(const char *t, size_t n, std::vector<SigRule> &out) {
+    size_t i = 0;
+    while (i < n) {
+        size_t e = i;
+        while (e < n && t[e] != '\n') e++;
+        std::string line(t + i, e - i);
+        i = e + 1;
+        while (!line.empty() && (line.back() == '\r' || line.back() == ' ' || line.back() == '\t')) line.pop_back();
+        size_t s = line.find_first_not_of(" \t");
+        if (s == std::string::npos || line[s] == '#') continue;
+        line = line.substr(s);
+        std::string f[3];
+        size_t p = 0;
+        for (int k = 0; k < 3; k++) {
+            size_t q = line.find(' ', p);
+            if (q == std::string::npos) return false;
+            f[k] = line.substr(p, q - p);
+            p = line.find_first_not_of(' ', q);
+            if (p == std::string::npos) return false;
+        }
+        SigRule r;
+        r.lit = f[0] == "lit";
+        if (!r.lit && f[0] != "re") return false;
+        r.nocase = f[1] == "i";
+        r.zones = 0;
+        for (char z : f[2]) r.zones |= z == 'u' ? 1 : z == 'a' ? 2 : z == 'h' ? 4 : z == 'b' ? 8 : 0;
+        std::string pat = line.substr(p);
+        if (r.lit) {
+            if (pat.size() % 2) return false;
+            for (size_t k = 0; k < pat.size(); k += 2) r.pat.push_back((char)std::stoi(pat.substr(k, 2), nullptr, 16));
+        } else r.pat = pat;
+        out.push_back(r);
+    }
+    return true;
+}
+
+uint32_t load4(const std::string &s) {
+    return (uint32_t)(uint8_t)s[0] | (uint32_t)(uint8_t)s[1] << 8 | (uint32_t)(uint8_t)s[2] << 16 |
+           (uint32_t)(uint8_t)s[3] << 24;
+}
+
+}  // namespace
+
+// ============================================================================ entry
+CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) {
+    CompileResult R;
+    gm_stats_t &st = R.stats;
+    memset(&st, 0, sizeof st);
+    st.gen = gen;
+    if (!blob || len < 8) { R.code = GM_E_INVAL; R.err = "short blob"; return R; }
+    uint32_t magic, n;
+    memcpy(&magic, blob, 4); memcpy(&n, blob + 4, 4);
+    if (magic != GM_BLOB_MAGIC) { R.code = GM_E_INVAL; R.err = "bad blob magic"; return R; }
+    size_t off = 8;
+    std::vector<Dir> main_body;
+    bool have_main = false;
+    std::vector<std::vector<Dir>> confd;
+    const char *sig_text = nullptr; size_t sig_len = 0;
+    for (uint32_t e = 0; e < n; e++) {
+        if (off + 12 > len) { R.code = GM_E_INVAL; R.err = "truncated blob"; return R; }
+        uint32_t kind, nl, dl;
+        memcpy(&kind, blob + off, 4); memcpy(&nl, blob + off + 4, 4); memcpy(&dl, blob + off + 8, 4);
+        off += 12;
+        if (off + (uint64_t)nl + dl > len) { R.code = GM_E_INVAL; R.err = "truncated blob entry"; return R; }
+        const char *data = (const char *)blob + off + nl;
+        off += nl + dl;
+        if (kind == GM_ENTRY_SIGS) { sig_text = data; sig_len = dl; continue; }
+        Tokenizer T(data, dl);
+        std::vector<Dir> body;
+        if (!parse_body(T, body, false)) {
+            R.code = GM_E_PARSE;
+            R.err = "nginx config parse error in " + std::string((const char *)blob + off - dl - nl, nl);
+            return R;
+        }
+        if (kind == GM_ENTRY_MAIN) { main_body = std::move(body); have_main = true; }
+        else confd.push_back(std::move(body));
+    }
+
+    Model M;
+    Builder B(M, confd);
+    if (have_main) {
+        for (const Dir &d : main_body)
+            if (!d.a.empty() && d.a[0] == "http" && d.block) B.http(d.body);
+    } else {
+        for (auto &f : confd) B.http(f);
+    }
+
+    Compiler C(M, st);
+    st.n_rejected_other += M.rejected_other;
+
+    // ---- upstreams: sorted unique name table
+    std::vector<std::string> ups = M.upstreams;
+    std::sort(ups.begin(), ups.end());
+    ups.erase(std::unique(ups.begin(), ups.end()), ups.end());
+    st.n_upstreams = (uint32_t)ups.size();
+
+    // ---- ports
+    std::vector<DPort> ports;
+    std::map<int, int> port_idx;
+    for (auto &S : M.servers)
+        for (auto &l : S.listens) {
+            auto it = port_idx.find(l.first);
+            if (it == port_idx.end()) {
+                port_idx[l.first] = (int)ports.size();
+                ports.push_back(DPort{(uint32_t)l.first, 0, (uint32_t)S.id, 0xFFFFFFFFu});
+                it = port_idx.find(l.first);
+            }
+            DPort &P = ports[it->second];
+            if (l.second & 1) P.ssl = 1;
+            if ((l.second & 2) && P.pad == 0xFFFFFFFFu) { P.default_server = (uint32_t)S.id; P.pad = 0; }
+        }
+    for (auto &P : ports) P.pad = 0;
+
+    // ---- server names: exact / wildcard-head / wildcard-tail hash tables, first wins
+    struct NameKey { std::string name; int port; uint32_t server; };
+    std::vector<NameKey> exact, head, tail;
+    for (auto &S : M.servers) {
+        std::set<int> sp;
+        for (auto &l : S.listens) sp.insert(port_idx[l.first]);
+        for (auto &nm : S.names) {
+            if (nm.empty()) continue;
+            if (nm[0] == '~') { st.n_rejected_other++; continue; }
+            for (int p : sp) {
+                if (nm.size() > 2 && nm[0] == '*' && nm[1] == '.') head.push_back({nm.substr(2), p, (uint32_t)S.id});
+                else if (nm.size() > 1 && nm[0] == '.') head.push_back({nm.substr(1), p, (uint32_t)S.id | 0x80000000u});
+                else if (nm.size() > 2 && nm.back() == '*' && nm[nm.size() - 2] == '.')
+                    tail.push_back({nm.substr(0, nm.size() - 2), p, (uint32_t)S.id});
+                else if (nm.find('*') == std::string::npos) exact.push_back({nm, p, (uint32_t)S.id});
+                else st.n_rejected_other++;
+            }
+        }
+    }
+    auto build_names = [&](std::vector<NameKey> &keys, uint32_t &mask) {
+        uint32_t cap = pow2_at_least(keys.size() * 2 + 1);
+        std::vector<DName> tab(cap);
+        for (auto &k : keys) {
+            uint32_t h = 2166136261u;
+            for (char c : k.name) h = fnv1a_step(h, (uint8_t)c);
+            h = name_hash_fin(h, (uint32_t)k.port);
+            uint32_t i = h & (cap - 1);
+            bool dup = false;
+            while (tab[i].hash) {
+                const DName &e = tab[i];
+                if (e.hash == h && e.port_idx == k.port && e.name_len == k.name.size() &&
+                    !memcmp(C.bytes.data() + e.name_off, k.name.data(), k.name.size())) { dup = true; break; }
+                i = (i + 1) & (cap - 1);
+            }
+            if (dup) continue;   // duplicate name on this port: first definition wins
+            tab[i].hash = h; tab[i].name_off = C.put_bytes(k.name); tab[i].name_len = (uint16_t)k.name.size();
+            tab[i].port_idx = (uint16_t)k.port; tab[i].server = k.server;
+        }
+        mask = cap - 1;
+        return tab;
+    };
+    uint32_t names_mask, head_mask, tail_mask;
+    auto tab_exact = build_names(exact, names_mask);
+    auto tab_head = build_names(head, head_mask);
+    auto tab_tail = build_names(tail, tail_mask);
+
+    // ---- locations, tries, regex locations, server ifs
+    std::vector<DLoc> dlocs(M.locs.size());
+    std::vector<DNode> nodes;
+    std::vector<std::pair<uint32_t, uint32_t>> edge_list;   // key, child
+    std::map<std::pair<uint32_t, uint8_t>, uint32_t> edge_map;
+    std::vector<DServer> dservers(M.servers.size());
+    std::vector<DServerIf> sifs;
+    std::vector<DRegexLoc> rlocs;
+    auto new_node = [&]() { nodes.push_back(DNode{-1, -1, -1, 0}); return (uint32_t)nodes.size() - 1; };
+    auto walk = [&](uint32_t root, const std::string &p) {
+        uint32_t cur = root;
+        for (unsigned char c : p) {
+            auto key = std::make_pair(cur, c);
+            auto it = edge_map.find(key);
+            if (it == edge_map.end()) {
+                uint32_t nn = new_node();
+                edge_map[key] = nn;
+                edge_list.push_back({cur * 256u + c + 1u, nn});
+                cur = nn;
+            } else cur = it->second;
+        }
+        return cur;
+    };
+    auto is_redirect = [](int code) { return code == 301 || code == 302 || code == 303 || code == 307 || code == 308; };
+    (void)is_redirect;
+    for (auto &S : M.servers) {
+        DServer &D = dservers[S.id];
+        D.trie_root = new_node();
+        D.waf_mode = (uint32_t)S.waf;
+        D.first_if = (uint32_t)sifs.size();
+        for (auto &f : S.ifs) {
+            DServerIf x{};
+            x.code = (uint32_t)f.code;
+            if (f.ret_only) x.op = SIF_RETURN;
+            else {
+                int s = C.src(f.var);
+                if (s < 0 || f.op < 0) { x.op = 0xFF; st.n_rejected_other++; }
+                else {
+                    x.src = (uint32_t)s;
+                    if (f.op == 0) x.op = 4;   // truthy: non-empty and not "0"
+                    else if (f.op == 1 || f.op == 2) { x.op = f.op == 1 ? SIF_EQ : SIF_NE; x.val_off = C.put_bytes(f.val); x.val_len = (uint32_t)f.val.size(); }
+                    else {
+                        int d = C.regex(f.val, f.op == 4 || f.op == 6);
+                        if (d < 0) x.op = 0xFF;
+                        else { x.op = (f.op == 3 || f.op == 4) ? 5 : 6; x.val_off = (uint32_t)d; }
+                    }
+                }
+            }
+            sifs.push_back(x);
+        }
+        D.n_if = (uint32_t)sifs.size() - D.first_if;
+        D.first_rloc = (uint32_t)rlocs.size();
+        for (int lid : S.locs) {
+            Loc &L = M.locs[lid];
+            DLoc &dl = dlocs[lid];
+            dl.waf_mode = (uint8_t)(L.waf >= 0 ? L.waf : S.waf);
+            dl.upstream = GM_NONE;
+            dl.noregex = L.kind == NOREGEX;
+            dl.is_named = L.kind == NAMED;
+            if (L.nested) dl.kind = LK_UNSUPPORTED;
+            else if (L.has_return && L.code == 418 && !L.err418.empty()) {
+                std::vector<std::string> vv;
+                int route = -1;
+                uint8_t kind = LK_UNSUPPORTED;
+                if (Compiler::var_list(L.err418, vv) && vv.size() == 1) {
+                    if (M.splits.count(vv[0])) { route = C.split_route(S, vv[0]); kind = LK_IRL_SPLIT; }
+                    else if (M.maps.count(vv[0])) { route = C.rules_route(S, vv[0]); kind = LK_IRL_RULES; }
+                }
+                if (route < 0) { dl.kind = LK_UNSUPPORTED; st.n_rejected_other++; }
+                else { dl.kind = kind; dl.route = (uint32_t)route; }
+                if (kind == LK_IRL_SPLIT && route >= 0) st.n_routes_split++;
+                if (kind == LK_IRL_RULES && route >= 0) st.n_routes_rules++;
+            } else if (L.has_return) { dl.kind = LK_RETURN; dl.ret_code = (uint32_t)L.code; }
+            else if (L.has_proxy) {
+                dl.kind = LK_PROXY;
+                auto it = std::lower_bound(ups.begin(), ups.end(), L.ups);
+                if (it != ups.end() && *it == L.ups) dl.upstream = (uint32_t)(it - ups.begin());
+            } else dl.kind = LK_NONE;
+
+            if (L.kind == PFX || L.kind == NOREGEX || L.kind == EXACT) {
+                uint32_t nd = walk(D.trie_root, L.path);
+                int32_t &slot = (L.kind == EXACT) ? nodes[nd].exact_loc : nodes[nd].prefix_loc;
+                if (slot >= 0) st.n_rejected_other++;   // duplicate location: nginx refuses; keep first
+                else slot = lid;
+            } else if (L.kind == RX || L.kind == RXI) {
+                int d = C.regex(L.path, L.kind == RXI);
+                if (d >= 0) rlocs.push_back(DRegexLoc{(uint32_t)d, (uint32_t)lid});
+                else dl.kind = LK_UNSUPPORTED;
+            }
+        }
+        D.n_rloc = (uint32_t)rlocs.size() - D.first_rloc;
+        // auto_redirect: location "<p>/" with proxy_pass -> node for "<p>" if nothing ends there
+        for (int lid : S.locs) {
+            Loc &L = M.locs[lid];
+            if (!(L.kind == PFX || L.kind == NOREGEX || L.kind == EXACT)) continue;
+            if (!L.has_proxy || L.path.empty() || L.path.back() != '/') continue;
+            uint32_t nd = walk(D.trie_root, L.path.substr(0, L.path.size() - 1));
+            if (nodes[nd].prefix_loc < 0 && nodes[nd].exact_loc < 0 && nodes[nd].ar_loc < 0) nodes[nd].ar_loc = lid;
+        }
+    }
+    // second pass: an ar_loc whose node later got a location is void
+    for (auto &nd : nodes) if (nd.prefix_loc >= 0 || nd.exact_loc >= 0) nd.ar_loc = -1;
+
+    uint32_t ecap = pow2_at_least(edge_list.size() * 2 + 1);
+    std::vector<DEdge> edges(ecap, DEdge{0, 0});
+    for (auto &e : edge_list) {
+        uint32_t i = edge_hash(e.first) & (ecap - 1);
+        while (edges[i].key) i = (i + 1) & (ecap - 1);
+        edges[i] = DEdge{e.first, e.second};
+    }
+
+    // ---- signatures
+    std::vector<SigRule> sig;
+    if (sig_text && !parse_sigs(sig_text, sig_len, sig)) { R.code = GM_E_PARSE; R.err = "signature set parse error"; return R; }
+    struct LitE { uint32_t key; DLit lit; std::string bytes; };
+    std::vector<LitE> lits;
+    std::vector<DSigRegex> sregex;
+    std::vector<uint32_t> always;
+    for (size_t r = 0; r < sig.size(); r++) {
+        const SigRule &g = sig[r];
+        if (g.lit) {
+            if (g.pat.size() < 4 || g.pat.size() > 0xFFFF) { st.n_rejected_other++; continue; }
+            std::string b = g.nocase ? lower(g.pat) : g.pat;
+            LitE e{fold4(load4(g.pat)), DLit{(uint32_t)r, 0, (uint16_t)b.size(),
+                                             (uint8_t)(g.nocase ? LIT_NOCASE : 0), (uint8_t)g.zones, 0}, b};
+            lits.push_back(e);
+            st.n_sig_literals++;
+        } else {
+            RegexInfo ri = compile_regex(g.pat, g.nocase);
+            if (ri.status != RX_OK) {
+                if (ri.status == RX_PCRE_ONLY) st.n_rejected_pcre++; else st.n_rejected_other++;
+                continue;
+            }
+            int d = C.add_dfa(ri.dfa);
+            uint32_t ridx = (uint32_t)sregex.size();
+            bool alw = ri.min_factor < 4;
+            sregex.push_back(DSigRegex{(uint32_t)d, (uint32_t)r, (uint32_t)g.zones, alw ? 1u : 0u});
+            st.n_sig_regex++;
+            if (alw) { always.push_back(ridx); st.n_sig_regex_always++; }
+            else
+                for (auto &f : ri.factors) {
+                    LitE e{fold4(load4(f)), DLit{ridx, 0, (uint16_t)f.size(), (uint8_t)(LIT_NOCASE | LIT_TRIGGER),
+                                                 (uint8_t)g.zones, 0}, f};
+                    lits.push_back(e);
+                }
+        }
+    }
+    st.n_sigs = (uint32_t)sig.size();
+    std::sort(lits.begin(), lits.end(), [](const LitE &a, const LitE &b) {
+        return a.key != b.key ? a.key < b.key : a.lit.id < b.lit.id;
+    });
+    std::vector<DLit> dlits;
+    std::vector<uint32_t> waf_a((1u << WAF_A_BITS) / 32, 0), waf_b((1u << WAF_B_BITS) / 32, 0);
+    std::vector<std::pair<uint32_t, std::pair<uint32_t, uint32_t>>> buckets;
+    for (size_t i = 0; i < lits.size(); i++) {
+        LitE &e = lits[i];
+        e.lit.bytes_off = C.put_bytes(e.bytes);
+        dlits.push_back(e.lit);
+        if (i == 0 || lits[i - 1].key != e.key) {
+            buckets.push_back({e.key, {(uint32_t)i, 0}});
+            uint32_t ha = waf_hash_a(e.key), hb = waf_hash_b(e.key);
+            waf_a[ha >> 5] |= 1u << (ha & 31);
+            waf_b[hb >> 5] |= 1u << (hb & 31);
+        }
+        buckets.back().second.second++;
+    }
+    uint32_t lcap = pow2_at_least(buckets.size() * 2 + 1);
+    std::vector<DLitBucket> ltab(lcap, DLitBucket{0, 0, 0, 0});
+    for (auto &b : buckets) {
+        uint32_t i = lit_bucket_hash(b.first) & (lcap - 1);
+        while (ltab[i].count) i = (i + 1) & (lcap - 1);
+        ltab[i] = DLitBucket{b.first, b.second.first, b.second.second, 0};
+    }
+
+    // ---- stats
+    st.n_servers = (uint32_t)M.servers.size();
+    st.n_locations = (uint32_t)M.locs.size();
+    st.n_counters = st.n_locations + st.n_sigs;
+    st.lds_bytes_scan = ((1u << WAF_A_BITS) + (1u << WAF_B_BITS)) / 8;
+
+    // ---- image
+    Image I;
+    TabHeader &h = R.hdr;
+    memset(&h, 0, sizeof h);
+    I.buf.resize(sizeof(TabHeader));
+    h.magic = 0x47544142u; h.version = 1;
+    h.n_ports = (uint32_t)ports.size();
+    h.n_names_cap = names_mask + 1; h.n_wild_head_cap = head_mask + 1; h.n_wild_tail_cap = tail_mask + 1;
+    h.n_servers = (uint32_t)dservers.size(); h.n_server_ifs = (uint32_t)sifs.size(); h.n_rlocs = (uint32_t)rlocs.size();
+    h.n_nodes = (uint32_t)nodes.size(); h.n_edges_cap = ecap; h.n_locs = (uint32_t)dlocs.size();
+    h.n_srcs = (uint32_t)C.srcs.size(); h.n_conds = (uint32_t)C.conds.size(); h.n_chain_heads = (uint32_t)C.chain_heads.size();
+    h.n_rules = (uint32_t)C.rules.size(); h.n_splits = (uint32_t)C.splits.size(); h.n_parts = (uint32_t)C.parts.size();
+    h.n_dfas = (uint32_t)C.dfas.size();
+    h.n_lit_buckets_cap = lcap; h.n_lits = (uint32_t)dlits.size(); h.n_sig_regex = (uint32_t)sregex.size();
+    h.n_always = (uint32_t)always.size(); h.n_sigs = st.n_sigs;
+    h.off_ports = I.put(ports);
+    h.off_names = I.put(tab_exact); h.off_wild_head = I.put(tab_head); h.off_wild_tail = I.put(tab_tail);
+    h.off_servers = I.put(dservers); h.off_server_ifs = I.put(sifs); h.off_rlocs = I.put(rlocs);
+    h.off_nodes = I.put(nodes); h.off_edges = I.put(edges); h.off_locs = I.put(dlocs);
+    h.off_srcs = I.put(C.srcs); h.off_conds = I.put(C.conds); h.off_chain_heads = I.put(C.chain_heads);
+    h.off_rules = I.put(C.rules); h.off_rtab = I.put(C.rtab); h.off_rtargets = I.put(C.rtargets);
+    h.off_splits = I.put(C.splits); h.off_parts = I.put(C.parts);
+    h.off_dfas = I.put(C.dfas); h.off_dfa_trans = I.put(C.dfa_trans); h.off_dfa_acc = I.put(C.dfa_acc);
+    h.off_dfa_cls = I.put(C.dfa_cls);
+    h.off_waf_a = I.put(waf_a); h.off_waf_b = I.put(waf_b);
+    h.off_lit_buckets = I.put(ltab); h.off_lits = I.put(dlits); h.off_sig_regex = I.put(sregex);
+    h.off_always = I.put(always);
+    C.bytes.resize(C.bytes.size() + 64, 0);   // slack: vector compares may over-read
+    h.off_bytes = I.put(C.bytes);
+    I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
+    h.total = I.buf.size();
+    memcpy(I.buf.data(), &h, sizeof h);
+    st.table_bytes = h.total;
+    R.image = std::move(I.buf);
+    R.ok = true;
+    return R;
+}
+
+GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
+    GTab t{};
+    t.ports = (const DPort *)(b + h.off_ports);
+    t.names = (const DName *)(b + h.off_names);
+    t.wild_head = (const DName *)(b + h.off_wild_head);
+    t.wild_tail = (const DName *)(b + h.off_wild_tail);
+    t.servers = (const DServer *)(b + h.off_servers);
+    t.server_ifs = (const DServerIf *)(b + h.off_server_ifs);
+    t.rlocs = (const DRegexLoc *)(b + h.off_rlocs);
+    t.nodes = (const DNode *)(b + h.off_nodes);
+    t.edges = (const DEdge *)(b + h.off_edges);
+    t.locs = (const DLoc *)(b + h.off_locs);
+    t.srcs = (const DSrc *)(b + h.off_srcs);
+    t.conds = (const DCond *)(b + h.off_conds);
+    t.chain_heads = (const uint32_t *)(b + h.off_chain_heads);
+    t.rules = (const DRules *)(b + h.off_rules);
+    t.rtab = b + h.off_rtab;
+    t.rtargets = (const uint32_t *)(b + h.off_rtargets);
+    t.splits = (const DSplit *)(b + h.off_splits);
+    t.parts = (const DPart *)(b + h.off_parts);
+    t.dfas = (const DDfa *)(b + h.off_dfas);
+    t.dfa_trans = (const uint16_t *)(b + h.off_dfa_trans);
+    t.dfa_acc = b + h.off_dfa_acc;
+    t.dfa_cls = b + h.off_dfa_cls;
+    t.bytes = b + h.off_bytes;
+    t.waf_a = (const uint32_t *)(b + h.off_waf_a);
+    t.waf_b = (const uint32_t *)(b + h.off_waf_b);
+    t.lit_buckets = (const DLitBucket *)(b + h.off_lit_buckets);
+    t.lits = (const DLit *)(b + h.off_lits);
+    t.sig_regex = (const DSigRegex *)(b + h.off_sig_regex);
+    t.always = (const uint32_t *)(b + h.off_always);
+    t.n_ports = h.n_ports;
+    t.names_mask = h.n_names_cap - 1; t.wild_head_mask = h.n_wild_head_cap - 1; t.wild_tail_mask = h.n_wild_tail_cap - 1;
+    t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;
+    t.n_locs = h.n_locs; t.n_sigs = h.n_sigs; t.n_sig_regex = h.n_sig_regex; t.n_always = h.n_always;
+    t.n_lits = h.n_lits;
+    t.gen = gen;
+    return t;
+}
+
+}  // namespace gm

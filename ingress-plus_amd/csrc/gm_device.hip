@@ -1,0 +1,1089 @@
+// gm_device.hip -- gfx950 kernels + host runtime + C-ABI of libgpumatch.so.
+//
+// Pipeline of one gm_match_batch (all on the caller's HIP stream):
+//   1. route   (lane per request)  host -> server, server rewrite `if`s, location trie / regex
+//                                   locations, IRL -> rules truth table / split_clients, verdict;
+//                                   per-location counters; arena block -> first record index.
+//   2. scan    (wave per 1 KiB)    WAF prefilter over the flat arena: every byte position's
+//                                   case-folded 4-gram probes an LDS bitmap (A) and, on a hit, a
+//                                   second LDS bitmap (B); survivors are appended (ballot-free
+//                                   wave prefix) to a candidate list.  HBM-bound by design.
+//   3. verify  (lane per candidate) exact literal compare inside the record's zone -> (req, rule)
+//                                   pairs; regex factor hits -> (req, zone, regex) jobs.
+//   4. regex   (lane per job)      byte-class DFA over the zone -> pairs.  (+ always-run regexes)
+//   5. finalize sort pairs, drop duplicates and requests whose location has WAF off, write the
+//                                   hit-id list in request order, n_hits / first_hit_off / block.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/gpumatch.h"
+#include "gm_compile.hpp"
+#include "gm_tables.hpp"
+
+using namespace gm;
+
+// ============================================================================ device helpers
+namespace {
+
+struct Rec {
+    uint64_t base;
+    uint32_t uri_len, args_len, hdr_len, body_len;
+    uint32_t host_len, method_len, ruri_len, raddr_len;
+    uint32_t port, rport, flags;
+    uint32_t rid[4];
+};
+
+__device__ __forceinline__ Rec load_rec(const gm_req *r) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(r);
+    uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+    Rec x;
+    x.base = (uint64_t)a.x | ((uint64_t)a.y << 32);
+    x.uri_len = a.z; x.args_len = a.w; x.hdr_len = b.x; x.body_len = b.y;
+    x.host_len = b.z & 0xFFFF; x.method_len = b.z >> 16; x.ruri_len = b.w & 0xFFFF; x.raddr_len = b.w >> 16;
+    x.port = c.x & 0xFFFF; x.rport = c.x >> 16; x.flags = c.y & 0xFF;
+    x.rid[0] = c.z; x.rid[1] = c.w; x.rid[2] = d.x; x.rid[3] = d.y;
+    return x;
+}
+
+__device__ __forceinline__ uint32_t lc(uint32_t c) { return (c - 'A' < 26u) ? (c | 0x20) : c; }
+
+// value = up to MAXSEG byte segments (generic pointers: arena, table bytes or lane-private)
+constexpr int MAXSEG = 12;
+struct Val {
+    const uint8_t *p[MAXSEG];
+    uint32_t n[MAXSEG];
+    int cnt;
+    uint32_t total;
+    bool overflow;
+    __device__ void clear() { cnt = 0; total = 0; overflow = false; }
+    __device__ void add(const uint8_t *q, uint32_t len) {
+        if (len == 0) return;
+        if (cnt == MAXSEG) { overflow = true; return; }
+        p[cnt] = q; n[cnt] = len; cnt++; total += len;
+    }
+};
+
+__constant__ uint8_t c_const[64] = "httpsonh2; , ?HTTP/2.0HTTP/1.0HTTP/1.1 0123456789abcdef";
+// offsets into c_const: "http" 0, "https" 0(5), "on" 5, "h2" 7, "; " 9, ", " 11, "?" 13,
+// "HTTP/2.0" 14, "HTTP/1.0" 22, "HTTP/1.1" 30, " " 38, hex digits 39
+
+struct Ctx {
+    const uint8_t *A;
+    Rec r;
+    uint64_t uri, args, hdrs, body, host, method, ruri, raddr;
+    uint8_t scratch[48];   // $request_id hex / $remote_port digits
+};
+
+__device__ void ctx_init(Ctx &c, const uint8_t *A, const Rec &r) {
+    c.A = A; c.r = r;
+    uint64_t o = r.base;
+    c.uri = o; o += r.uri_len; c.args = o; o += r.args_len; c.hdrs = o; o += r.hdr_len;
+    c.body = o; o += r.body_len; c.host = o; o += r.host_len; c.method = o; o += r.method_len;
+    c.ruri = o; o += r.ruri_len; c.raddr = o;
+}
+
+// iterate "Name: value\r\n" lines; returns false at end
+struct HdrIt { uint64_t pos, end; };
+__device__ bool hdr_next(const uint8_t *A, HdrIt &it, uint64_t &ns, uint32_t &nl, uint64_t &vs, uint32_t &vl) {
+    while (it.pos < it.end) {
+        uint64_t st = it.pos, e = st;
+        while (e < it.end && A[e] != '\n') e++;
+        it.pos = e + 1;
+        uint64_t le = e;
+        if (le > st && A[le - 1] == '\r') le--;
+        uint64_t c = st;
+        while (c < le && A[c] != ':') c++;
+        if (c >= le) continue;
+        ns = st; nl = (uint32_t)(c - st);
+        uint64_t v0 = c + 1;
+        while (v0 < le && (A[v0] == ' ' || A[v0] == '\t')) v0++;
+        uint64_t v1 = le;
+        while (v1 > v0 && (A[v1 - 1] == ' ' || A[v1 - 1] == '\t')) v1--;
+        vs = v0; vl = (uint32_t)(v1 - v0);
+        return true;
+    }
+    return false;
+}
+
+// header name vs variable suffix (lowercase, '-' -> '_'), ngx_http_variable_unknown_header
+__device__ bool hdr_name_is(const uint8_t *A, uint64_t ns, uint32_t nl, const uint8_t *var, uint32_t vl) {
+    if (nl != vl) return false;
+    for (uint32_t i = 0; i < nl; i++) {
+        uint32_t ch = A[ns + i];
+        ch = (ch - 'A' < 26u) ? (ch | 0x20) : (ch == '-' ? '_' : ch);
+        if (ch != var[i]) return false;
+    }
+    return true;
+}
+
+__device__ void get_var(Ctx &c, const GTab &t, uint32_t src_id, Val &v) {
+    v.clear();
+    const DSrc s = t.srcs[src_id];
+    const uint8_t *A = c.A;
+    const Rec &r = c.r;
+    if (s.kind == SRC_VAR) {
+        switch (s.var) {
+        case V_SCHEME: v.add(c_const, (r.flags & GM_REQ_HTTPS) ? 5 : 4); break;
+        case V_HTTPS: if (r.flags & GM_REQ_HTTPS) v.add(c_const + 5, 2); break;
+        case V_HTTP2: if (r.flags & GM_REQ_HTTP2) v.add(c_const + 7, 2); break;
+        case V_METHOD: v.add(A + c.method, r.method_len); break;
+        case V_ARGS: v.add(A + c.args, r.args_len); break;
+        case V_URI: v.add(A + c.uri, r.uri_len); break;
+        case V_REQUEST_BODY: break;
+        case V_REMOTE_ADDR: v.add(A + c.raddr, r.raddr_len); break;
+        case V_HOST: v.add(A + c.host, r.host_len); break;
+        case V_REQUEST_URI:
+        case V_REQUEST:
+            if (s.var == V_REQUEST) { v.add(A + c.method, r.method_len); v.add(c_const + 38, 1); }
+            if (r.ruri_len) v.add(A + c.ruri, r.ruri_len);
+            else {
+                v.add(A + c.uri, r.uri_len);
+                if (r.args_len) { v.add(c_const + 13, 1); v.add(A + c.args, r.args_len); }
+            }
+            if (s.var == V_REQUEST) {
+                v.add(c_const + 38, 1);
+                v.add(c_const + ((r.flags & GM_REQ_HTTP2) ? 14 : (r.flags & GM_REQ_HTTP10) ? 22 : 30), 8);
+            }
+            break;
+        case V_REQUEST_ID:
+            for (int i = 0; i < 16; i++) {
+                uint32_t b = (r.rid[i >> 2] >> (8 * (i & 3))) & 0xFF;
+                c.scratch[2 * i] = c_const[39 +(b >> 4)];
+                c.scratch[2 * i + 1] = c_const[39 +(b & 15)];
+            }
+            v.add(c.scratch, 32);
+            break;
+        case V_REMOTE_PORT:
+        case V_SERVER_PORT: {
+            uint32_t x = s.var == V_REMOTE_PORT ? r.rport : r.port;
+            uint8_t tmp[6]; int k = 0;
+            do { tmp[k++] = (uint8_t)('0' + x % 10); x /= 10; } while (x);
+            for (int i = 0; i < k; i++) c.scratch[i] = tmp[k - 1 - i];
+            v.add(c.scratch, (uint32_t)k);
+            break;
+        }
+        default: break;
+        }
+        return;
+    }
+    const uint8_t *nm = t.bytes + s.name_off;
+    if (s.kind == SRC_HTTP) {
+        HdrIt it{c.hdrs, c.hdrs + r.hdr_len};
+        uint64_t ns, vs; uint32_t nl, vl;
+        bool have = false;
+        while (hdr_next(A, it, ns, nl, vs, vl)) {
+            if (!hdr_name_is(A, ns, nl, nm, s.name_len)) continue;
+            if (!s.join) { v.add(A + vs, vl); return; }
+            if (have) v.add(c_const + (s.join == ';' ? 9 : 11), 2);
+            v.add(A + vs, vl);
+            have = true;
+        }
+        return;
+    }
+    if (s.kind == SRC_COOKIE) {
+        // ngx_http_parse_multi_header_lines over every Cookie line
+        HdrIt it{c.hdrs, c.hdrs + r.hdr_len};
+        uint64_t ns, vs; uint32_t nl, vl;
+        const uint8_t cookie[7] = "cookie";
+        while (hdr_next(A, it, ns, nl, vs, vl)) {
+            if (!hdr_name_is(A, ns, nl, cookie, 6)) continue;
+            if (s.name_len > vl) continue;
+            uint64_t start = vs, end = vs + vl;
+            while (start < end) {
+                bool ok = end - start >= s.name_len;
+                for (uint32_t k = 0; ok && k < s.name_len; k++) if (lc(A[start + k]) != nm[k]) ok = false;
+                if (ok) {
+                    start += s.name_len;
+                    while (start < end && A[start] == ' ') start++;
+                    if (start < end && A[start] == '=') {
+                        start++;
+                        while (start < end && A[start] == ' ') start++;
+                        uint64_t last = start;
+                        while (last < end && A[last] != ';') last++;
+                        v.add(A + start, (uint32_t)(last - start));
+                        return;
+                    }
+                }
+                while (start < end) { uint8_t ch = A[start++]; if (ch == ';' || ch == ',') break; }
+                while (start < end && A[start] == ' ') start++;
+            }
+        }
+        return;
+    }
+    if (s.kind == SRC_ARG) {
+        // ngx_http_arg
+        uint64_t a = c.args;
+        uint32_t n = r.args_len, L = s.name_len;
+        for (uint32_t p = 0; p + L < n; p++) {
+            bool ok = true;
+            for (uint32_t k = 0; ok && k < L; k++) if (lc(A[a + p + k]) != nm[k]) ok = false;
+            if (!ok) continue;
+            if ((p == 0 || A[a + p - 1] == '&') && A[a + p + L] == '=') {
+                uint32_t b = p + L + 1, e = b;
+                while (e < n && A[a + e] != '&') e++;
+                v.add(A + a + b, e - b);
+                return;
+            }
+        }
+    }
+}
+
+__device__ bool val_eq(const Val &v, const uint8_t *key, uint32_t kl, bool nocase) {
+    if (v.total != kl) return false;
+    uint32_t k = 0;
+    for (int s = 0; s < v.cnt; s++)
+        for (uint32_t i = 0; i < v.n[s]; i++, k++) {
+            uint32_t a = v.p[s][i];
+            if (nocase) a = lc(a);
+            if (a != key[k]) return false;
+        }
+    return true;
+}
+
+// PCRE search semantics on a byte stream given as segments (see gm_regex.cpp dfa_search)
+__device__ bool dfa_run_val(const GTab &t, uint32_t dfa_id, const Val &v) {
+    const DDfa d = t.dfas[dfa_id];
+    const uint16_t *tr = t.dfa_trans + d.trans_off;
+    const uint8_t *acc = t.dfa_acc + d.acc_off, *cls = t.dfa_cls + d.cls_off;
+    uint32_t st = 1;
+    if (acc[st] & 1) return true;
+    uint32_t pos = 0;
+    for (int s = 0; s < v.cnt; s++)
+        for (uint32_t i = 0; i < v.n[s]; i++, pos++) {
+            uint8_t b = v.p[s][i];
+            if ((acc[st] & 2) && pos + 1 == v.total && b == '\n') return true;
+            st = tr[st * d.n_classes + cls[b]];
+            if (st == 0) return false;
+            if (acc[st] & 1) return true;
+        }
+    return (acc[st] & 2) != 0;
+}
+
+__device__ bool dfa_run_bytes(const GTab &t, uint32_t dfa_id, const uint8_t *p, uint32_t n) {
+    const DDfa d = t.dfas[dfa_id];
+    const uint16_t *tr = t.dfa_trans + d.trans_off;
+    const uint8_t *acc = t.dfa_acc + d.acc_off, *cls = t.dfa_cls + d.cls_off;
+    uint32_t st = 1;
+    if (acc[st] & 1) return true;
+    for (uint32_t i = 0; i < n; i++) {
+        uint8_t b = p[i];
+        if ((acc[st] & 2) && i + 1 == n && b == '\n') return true;
+        st = tr[st * d.n_classes + cls[b]];
+        if (st == 0) return false;
+        if (acc[st] & 1) return true;
+    }
+    return (acc[st] & 2) != 0;
+}
+
+__device__ uint32_t murmur2_val(const Val &v, uint8_t *buf, bool &ok) {
+    // gather to a contiguous lane-private buffer (values here are <= 64 bytes: $request_id)
+    uint32_t n = v.total;
+    if (n > 64) { ok = false; return 0; }
+    uint32_t k = 0;
+    for (int s = 0; s < v.cnt; s++) for (uint32_t i = 0; i < v.n[s]; i++) buf[k++] = v.p[s][i];
+    uint32_t h = n, len = n;
+    const uint8_t *d = buf;
+    while (len >= 4) {
+        uint32_t x = d[0] | (d[1] << 8) | (d[2] << 16) | ((uint32_t)d[3] << 24);
+        x *= 0x5bd1e995u; x ^= x >> 24; x *= 0x5bd1e995u;
+        h *= 0x5bd1e995u; h ^= x;
+        d += 4; len -= 4;
+    }
+    switch (len) {
+    case 3: h ^= d[2] << 16; [[fallthrough]];
+    case 2: h ^= d[1] << 8; [[fallthrough]];
+    case 1: h ^= d[0]; h *= 0x5bd1e995u;
+    }
+    h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15;
+    ok = true;
+    return h;
+}
+
+// ngx_http_validate_host; returns normalised length or -1
+__device__ int validate_host(const uint8_t *h, uint32_t n) {
+    int dot_pos = (int)n, host_len = (int)n, state = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        uint8_t ch = h[i];
+        if (ch == '.') { if (dot_pos == (int)i - 1) return -1; dot_pos = (int)i; }
+        else if (ch == ':') { if (state == 0) { host_len = (int)i; state = 2; } }
+        else if (ch == '[') { if (i == 0) state = 1; }
+        else if (ch == ']') { if (state == 1) { host_len = (int)i + 1; state = 2; } }
+        else if (ch == 0 || ch == '/') return -1;
+    }
+    if (dot_pos == host_len - 1) host_len--;
+    return host_len <= 0 ? -1 : host_len;
+}
+
+__device__ uint32_t name_probe(const DName *tab, uint32_t mask, const uint8_t *bytes, const uint8_t *h,
+                               uint32_t off, uint32_t len, uint32_t port_idx) {
+    uint32_t hs = 2166136261u;
+    for (uint32_t i = 0; i < len; i++) hs = fnv1a_step(hs, lc(h[off + i]));
+    hs = name_hash_fin(hs, port_idx);
+    for (uint32_t i = hs & mask;; i = (i + 1) & mask) {
+        const DName e = tab[i];
+        if (e.hash == 0) return GM_NONE;
+        if (e.hash == hs && e.port_idx == port_idx && e.name_len == len) {
+            bool ok = true;
+            for (uint32_t k = 0; ok && k < len; k++) if (lc(h[off + k]) != bytes[e.name_off + k]) ok = false;
+            if (ok) return e.server;
+        }
+    }
+}
+
+__device__ __forceinline__ bool is_redirect(uint32_t code) {
+    return code == 301 || code == 302 || code == 303 || code == 307 || code == 308;
+}
+
+struct RouteOut {
+    uint32_t server, loc, ups, status;
+    uint8_t action, kind, bucket, match;
+    uint16_t waf;
+};
+
+__device__ void route_one(const uint8_t *A, const Rec &r, const GTab &t, RouteOut &o) {
+    o.server = GM_NONE; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0;
+    o.action = GM_ACT_NO_LISTENER; o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF;
+    Ctx c;
+    ctx_init(c, A, r);
+    // ---- listen port
+    uint32_t pi = GM_NONE;
+    for (uint32_t i = 0; i < t.n_ports; i++) if (t.ports[i].port == r.port) { pi = i; break; }
+    if (pi == GM_NONE) return;
+    const DPort P = t.ports[pi];
+    const bool https = r.flags & GM_REQ_HTTPS;
+    if (https && !P.ssl) return;
+    uint32_t sid = P.default_server;
+    // ---- host -> server (exact > *.x/.x > x.*)
+    bool bad = false;
+    if (r.host_len) {
+        const uint8_t *h = A + c.host;
+        int hl = validate_host(h, r.host_len);
+        if (hl < 0) bad = true;
+        else {
+            uint32_t s = name_probe(t.names, t.names_mask, t.bytes, h, 0, (uint32_t)hl, pi);
+            if (s == GM_NONE) {
+                uint32_t w = name_probe(t.wild_head, t.wild_head_mask, t.bytes, h, 0, (uint32_t)hl, pi);
+                if (w != GM_NONE && (w & 0x80000000u)) s = w & 0x7FFFFFFFu;      // ".x" matches x itself
+                for (int d = 0; s == GM_NONE && d < hl; d++)
+                    if (h[d] == '.') {
+                        w = name_probe(t.wild_head, t.wild_head_mask, t.bytes, h, d + 1, (uint32_t)(hl - d - 1), pi);
+                        if (w != GM_NONE) s = w & 0x7FFFFFFFu;
+                    }
+                for (int d = hl - 2; s == GM_NONE && d > 0; d--)
+                    if (h[d] == '.') s = name_probe(t.wild_tail, t.wild_tail_mask, t.bytes, h, 0, (uint32_t)d, pi);
+            }
+            if (s != GM_NONE) sid = s;
+        }
+    }
+    o.server = sid;
+    if (bad || (P.ssl && !https)) { o.action = GM_ACT_BAD_REQUEST; o.status = 400; return; }
+    const DServer S = t.servers[sid];
+    // ---- server rewrite phase
+    Val v;
+    for (uint32_t i = 0; i < S.n_if; i++) {
+        const DServerIf f = t.server_ifs[S.first_if + i];
+        bool hit;
+        if (f.op == SIF_RETURN) hit = true;
+        else if (f.op == 0xFF) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; return; }
+        else {
+            get_var(c, t, f.src, v);
+            if (f.op == SIF_EQ) hit = val_eq(v, t.bytes + f.val_off, f.val_len, false);
+            else if (f.op == SIF_NE) hit = !val_eq(v, t.bytes + f.val_off, f.val_len, false);
+            else if (f.op == 4) hit = v.total && !(v.total == 1 && v.p[0][0] == '0');
+            else { bool m = dfa_run_val(t, f.val_off, v); hit = f.op == 5 ? m : !m; }
+        }
+        if (hit) { o.action = is_redirect(f.code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = f.code; return; }
+    }
+    // ---- location: trie walk (exact, longest prefix, auto_redirect), then regex locations
+    const uint8_t *u = A + c.uri;
+    uint32_t node = S.trie_root;
+    int32_t best = -1;
+    uint32_t i = 0;
+    for (;; i++) {
+        const DNode nd = t.nodes[node];
+        if (nd.prefix_loc >= 0) best = nd.prefix_loc;
+        if (i == r.uri_len) break;
+        uint32_t key = node * 256u + u[i] + 1u;
+        uint32_t slot = edge_hash(key) & t.edges_mask, child = GM_NONE;
+        for (;; slot = (slot + 1) & t.edges_mask) {
+            const DEdge e = t.edges[slot];
+            if (e.key == 0) break;
+            if (e.key == key) { child = e.child; break; }
+        }
+        if (child == GM_NONE) break;
+        node = child;
+    }
+    int32_t loc = -1;
+    if (i == r.uri_len) {
+        const DNode nd = t.nodes[node];
+        if (nd.exact_loc >= 0) loc = nd.exact_loc;
+        else if (nd.ar_loc >= 0) { o.loc = (uint32_t)nd.ar_loc; o.action = GM_ACT_AUTO_301; o.status = 301; return; }
+    }
+    if (loc < 0) {
+        if (best >= 0 && t.locs[best].noregex) loc = best;
+        else {
+            for (uint32_t k = 0; k < S.n_rloc && loc < 0; k++) {
+                const DRegexLoc rl = t.rlocs[S.first_rloc + k];
+                Val uv; uv.clear(); uv.add(u, r.uri_len);
+                if (dfa_run_bytes(t, rl.dfa, u, r.uri_len)) loc = (int32_t)rl.loc;
+            }
+            if (loc < 0) loc = best;
+        }
+    }
+    if (loc < 0) { o.action = GM_ACT_NOT_FOUND; o.status = 404; return; }
+    o.loc = (uint32_t)loc;
+    DLoc L = t.locs[loc];
+    uint32_t fin = (uint32_t)loc;
+    if (L.kind == LK_IRL_RULES) {
+        const DRules R = t.rules[L.route];
+        uint32_t bits = 0;
+        for (uint32_t ch = 0; ch < R.n_chains; ch++) {
+            int32_t nd = (int32_t)t.chain_heads[R.first_chain + ch];
+            int guard = 0;
+            while (nd >= 0 && guard++ < 64) {
+                const DCond cd = t.conds[nd];
+                get_var(c, t, cd.src, v);
+                bool m;
+                if (cd.is_regex) m = v.total > 0 && dfa_run_val(t, cd.dfa, v);
+                else m = val_eq(v, t.bytes + cd.key_off, cd.key_len, true);
+                nd = m ? cd.next_true : cd.next_false;
+            }
+            if (nd == NEXT_1) bits |= 1u << ch;
+        }
+        uint8_t idx = t.rtab[R.table_off + bits];
+        o.kind = GM_ROUTE_RULES; o.match = idx;
+        fin = idx == 0xFF ? R.default_target : t.rtargets[R.first_target + idx];
+    } else if (L.kind == LK_IRL_SPLIT) {
+        const DSplit Sp = t.splits[L.route];
+        get_var(c, t, Sp.src, v);
+        uint8_t buf[64]; bool ok;
+        uint32_t hsh = murmur2_val(v, buf, ok);
+        o.kind = GM_ROUTE_SPLIT;
+        fin = GM_NONE;
+        if (!ok) { o.action = GM_ACT_UNSUPPORTED; return; }
+        for (uint32_t k = 0; k < Sp.n_parts; k++) {
+            const DPart pt = t.parts[Sp.first_part + k];
+            if (hsh < pt.bound || pt.star) { o.bucket = (uint8_t)k; fin = pt.target; break; }
+        }
+    } else if (L.kind == LK_UNSUPPORTED) {
+        o.action = GM_ACT_UNSUPPORTED; return;
+    }
+    if (L.kind == LK_IRL_RULES || L.kind == LK_IRL_SPLIT) {
+        if (fin == GM_NONE) { o.action = GM_ACT_ERRPAGE; o.status = 302; return; }
+        L = t.locs[fin];
+        if (L.kind != LK_PROXY && L.kind != LK_RETURN && L.kind != LK_NONE) { o.action = GM_ACT_UNSUPPORTED; return; }
+    }
+    if (L.kind == LK_RETURN) { o.action = is_redirect(L.ret_code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = L.ret_code; return; }
+    if (L.kind != LK_PROXY) { o.action = GM_ACT_NOT_FOUND; o.status = 404; return; }
+    if (fin == (uint32_t)loc) o.kind = GM_ROUTE_PLAIN;
+    o.action = GM_ACT_PROXY; o.status = 0; o.ups = L.upstream; o.waf = L.waf_mode;
+}
+
+// ============================================================================ kernels
+constexpr int ROUTE_BLOCK = 256;
+constexpr uint32_t LDS_HIST_MAX = 2048;
+
+__global__ __launch_bounds__(ROUTE_BLOCK) void k_route(const gm_req *__restrict__ reqs, uint32_t n,
+                                                       const uint8_t *__restrict__ A, uint64_t arena_len,
+                                                       GTab t, gm_verdict *__restrict__ out,
+                                                       unsigned long long *__restrict__ counters,
+                                                       uint32_t *__restrict__ blk2rec, uint32_t nblk) {
+    __shared__ uint32_t hist[LDS_HIST_MAX];
+    const bool use_hist = t.n_locs <= LDS_HIST_MAX;
+    if (use_hist) for (uint32_t k = threadIdx.x; k < t.n_locs; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const Rec r = load_rec(reqs + i);
+        RouteOut o;
+        route_one(A, r, t, o);
+        uint4 w0, w1;
+        w0.x = t.gen; w0.y = o.server; w0.z = o.loc; w0.w = o.ups;
+        w1.x = (uint32_t)o.action | ((uint32_t)o.kind << 8) | ((uint32_t)o.bucket << 16) | ((uint32_t)o.match << 24);
+        w1.y = (uint32_t)o.waf;   // n_hits = 0
+        w1.z = 0;                 // first_hit_off
+        w1.w = o.status;
+        uint4 *dst = reinterpret_cast<uint4 *>(out + i);
+        dst[0] = w0; dst[1] = w1;
+        if (o.loc != GM_NONE) {
+            if (use_hist) atomicAdd(&hist[o.loc], 1u);
+            else atomicAdd(&counters[o.loc], 1ull);
+        }
+        if (blk2rec) {
+            // blocks whose start lies in [base_i, base_{i+1}) belong to record i
+            uint64_t b0 = (i == 0) ? 0 : r.base;
+            uint64_t b1 = (i + 1 < n) ? reqs[i + 1].base : arena_len;
+            uint64_t k0 = (b0 + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
+            uint64_t k1 = (b1 + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
+            if (i + 1 == n) k1 = nblk;
+            for (uint64_t k = k0; k < k1 && k < nblk; k++) blk2rec[k] = i;
+        }
+    }
+    if (use_hist) {
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < t.n_locs; k += blockDim.x)
+            if (hist[k]) atomicAdd(&counters[k], (unsigned long long)hist[k]);
+    }
+}
+
+constexpr int SCAN_BLOCK = 1024;
+constexpr int SCAN_WAVES = SCAN_BLOCK / 64;
+constexpr uint32_t WAF_A_WORDS = (1u << WAF_A_BITS) / 32, WAF_B_WORDS = (1u << WAF_B_BITS) / 32;
+
+__device__ __forceinline__ uint32_t load_u32_guard(const uint8_t *A, uint64_t off, uint64_t len) {
+    if (off + 4 <= len) return *reinterpret_cast<const uint32_t *>(A + off);
+    uint32_t w = 0;
+    for (int k = 0; k < 4; k++) if (off + k < len) w |= (uint32_t)A[off + k] << (8 * k);
+    return w;
+}
+
+__global__ __launch_bounds__(SCAN_BLOCK) void k_waf_scan(const uint8_t *__restrict__ A, uint64_t len,
+                                                         const uint32_t *__restrict__ bmA,
+                                                         const uint32_t *__restrict__ bmB,
+                                                         unsigned long long *__restrict__ cand, uint32_t cap,
+                                                         uint32_t *__restrict__ status) {
+    extern __shared__ uint32_t lds[];
+    uint32_t *la = lds, *lb = lds + WAF_A_WORDS;
+    {
+        const uint4 *ga = reinterpret_cast<const uint4 *>(bmA);
+        const uint4 *gb = reinterpret_cast<const uint4 *>(bmB);
+        uint4 *sa = reinterpret_cast<uint4 *>(la), *sb = reinterpret_cast<uint4 *>(lb);
+        for (uint32_t k = threadIdx.x; k < WAF_A_WORDS / 4; k += SCAN_BLOCK) sa[k] = ga[k];
+        for (uint32_t k = threadIdx.x; k < WAF_B_WORDS / 4; k += SCAN_BLOCK) sb[k] = gb[k];
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t nchunks = (len + 1023) >> 10;
+    const uint64_t stride = (uint64_t)gridDim.x * SCAN_WAVES;
+    for (uint64_t ch = (uint64_t)blockIdx.x * SCAN_WAVES + wave; ch < nchunks; ch += stride) {
+        const uint64_t off = (ch << 10) + lane * 16;
+        uint32_t d[5];
+        if (off + 16 <= len) {
+            uint4 q = *reinterpret_cast<const uint4 *>(A + off);
+            d[0] = q.x; d[1] = q.y; d[2] = q.z; d[3] = q.w;
+        } else {
+            for (int k = 0; k < 4; k++) d[k] = load_u32_guard(A, off + 4 * k, len);
+        }
+        uint32_t nx = __shfl_down(d[0], 1);
+        if (lane == 63) nx = load_u32_guard(A, off + 16, len);
+        d[4] = nx;
+#pragma unroll
+        for (int k = 0; k < 5; k++) d[k] = fold4(d[k]);
+        uint32_t mask = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t w = __builtin_amdgcn_alignbyte(d[(j >> 2) + 1], d[j >> 2], j & 3);
+            const uint32_t ha = waf_hash_a(w);
+            if ((la[ha >> 5] >> (ha & 31)) & 1u) {
+                const uint32_t hb = waf_hash_b(w);
+                if (((lb[hb >> 5] >> (hb & 31)) & 1u) && off + j + 4 <= len) mask |= 1u << j;
+            }
+        }
+        if (__ballot(mask != 0) == 0ull) continue;
+        // wave-wide exclusive prefix of per-lane counts
+        uint32_t cnt = __popc(mask), incl = cnt;
+#pragma unroll
+        for (int s = 1; s < 64; s <<= 1) {
+            uint32_t y = __shfl_up(incl, s);
+            if (lane >= (uint32_t)s) incl += y;
+        }
+        uint32_t total = __shfl(incl, 63);
+        uint32_t base = 0;
+        if (lane == 63) base = atomicAdd(status + 0, total);
+        base = __shfl(base, 63) + incl - cnt;
+        while (mask) {
+            int j = __ffs(mask) - 1;
+            mask &= mask - 1;
+            if (base < cap) cand[base] = off + j;
+            base++;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t find_rec(const gm_req *reqs, uint32_t n, const uint32_t *blk2rec, uint64_t pos) {
+    uint32_t r = blk2rec[pos >> BLK_SHIFT];
+    while (r + 1 < n && reqs[r + 1].base <= pos) r++;
+    return r;
+}
+
+__device__ __forceinline__ void push_u64(unsigned long long *buf, uint32_t cap, uint32_t *ctr, unsigned long long v,
+                                         uint32_t *status) {
+    uint32_t k = atomicAdd(ctr, 1u);
+    if (k < cap) buf[k] = v; else atomicOr(status + 3, 1u);
+}
+
+__global__ __launch_bounds__(256) void k_waf_verify(const uint8_t *__restrict__ A, uint64_t len,
+                                                    const gm_req *__restrict__ reqs, uint32_t n,
+                                                    const uint32_t *__restrict__ blk2rec, GTab t,
+                                                    const unsigned long long *__restrict__ cand, uint32_t ccap,
+                                                    unsigned long long *__restrict__ pairs, uint32_t pcap,
+                                                    unsigned long long *__restrict__ jobs, uint32_t jcap,
+                                                    uint32_t *__restrict__ status) {
+    const uint32_t nc = min(status[0], ccap);
+    if (status[0] > ccap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(status + 3, 4u);
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nc; i += gridDim.x * blockDim.x) {
+        const uint64_t pos = cand[i];
+        uint32_t w = 0;
+        for (int k = 0; k < 4; k++) w |= (uint32_t)A[pos + k] << (8 * k);
+        w = fold4(w);
+        uint32_t b = lit_bucket_hash(w) & t.lit_mask;
+        DLitBucket bk;
+        for (;; b = (b + 1) & t.lit_mask) {
+            bk = t.lit_buckets[b];
+            if (bk.count == 0 || bk.key == w) break;
+        }
+        if (bk.count == 0) continue;
+        const uint32_t r = find_rec(reqs, n, blk2rec, pos);
+        const Rec rc = load_rec(reqs + r);
+        if (pos < rc.base) continue;
+        const uint64_t rel = pos - rc.base;
+        uint32_t z; uint64_t zend;
+        if (rel < rc.uri_len) { z = 0; zend = rc.uri_len; }
+        else if (rel < (uint64_t)rc.uri_len + rc.args_len) { z = 1; zend = rc.uri_len + rc.args_len; }
+        else if (rel < (uint64_t)rc.uri_len + rc.args_len + rc.hdr_len) { z = 2; zend = (uint64_t)rc.uri_len + rc.args_len + rc.hdr_len; }
+        else if (rel < (uint64_t)rc.uri_len + rc.args_len + rc.hdr_len + rc.body_len) {
+            z = 3; zend = (uint64_t)rc.uri_len + rc.args_len + rc.hdr_len + rc.body_len;
+        } else continue;
+        zend += rc.base;
+        for (uint32_t k = 0; k < bk.count; k++) {
+            const DLit L = t.lits[bk.first + k];
+            if (!(L.zones & (1u << z)) || pos + L.len > zend) continue;
+            const uint8_t *pat = t.bytes + L.bytes_off;
+            bool ok = true;
+            if (L.flags & LIT_NOCASE) { for (uint32_t q = 0; ok && q < L.len; q++) if (lc(A[pos + q]) != pat[q]) ok = false; }
+            else { for (uint32_t q = 0; ok && q < L.len; q++) if (A[pos + q] != pat[q]) ok = false; }
+            if (!ok) continue;
+            if (L.flags & LIT_TRIGGER)
+                push_u64(jobs, jcap, status + 2, ((unsigned long long)r << 32) | (L.id << 2) | z, status);
+            else
+                push_u64(pairs, pcap, status + 1, ((unsigned long long)r << 32) | L.id, status);
+        }
+    }
+}
+
+__device__ __forceinline__ void zone_of(const Rec &rc, uint32_t z, uint64_t &zs, uint32_t &zl) {
+    uint64_t o = rc.base;
+    const uint32_t lens[4] = {rc.uri_len, rc.args_len, rc.hdr_len, rc.body_len};
+    for (uint32_t k = 0; k < z; k++) o += lens[k];
+    zs = o; zl = lens[z];
+}
+
+__global__ __launch_bounds__(256) void k_waf_regex(const uint8_t *__restrict__ A, const gm_req *__restrict__ reqs,
+                                                   GTab t, const unsigned long long *__restrict__ jobs, uint32_t nj,
+                                                   unsigned long long *__restrict__ pairs, uint32_t pcap,
+                                                   uint32_t *__restrict__ status) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nj; i += gridDim.x * blockDim.x) {
+        const unsigned long long j = jobs[i];
+        if (i > 0 && jobs[i - 1] == j) continue;
+        const uint32_t r = (uint32_t)(j >> 32), lo = (uint32_t)j, rx = lo >> 2, z = lo & 3;
+        const Rec rc = load_rec(reqs + r);
+        uint64_t zs; uint32_t zl;
+        zone_of(rc, z, zs, zl);
+        const DSigRegex g = t.sig_regex[rx];
+        if (dfa_run_bytes(t, g.dfa, A + zs, zl))
+            push_u64(pairs, pcap, status + 1, ((unsigned long long)r << 32) | g.rule, status);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_waf_always(const uint8_t *__restrict__ A, const gm_req *__restrict__ reqs,
+                                                    uint32_t n, GTab t, unsigned long long *__restrict__ pairs,
+                                                    uint32_t pcap, uint32_t *__restrict__ status) {
+    const uint64_t total = (uint64_t)n * t.n_always;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = (uint32_t)(i / t.n_always), a = (uint32_t)(i % t.n_always);
+        const DSigRegex g = t.sig_regex[t.always[a]];
+        const Rec rc = load_rec(reqs + r);
+        for (uint32_t z = 0; z < 4; z++) {
+            if (!(g.zones & (1u << z))) continue;
+            uint64_t zs; uint32_t zl;
+            zone_of(rc, z, zs, zl);
+            if (dfa_run_bytes(t, g.dfa, A + zs, zl)) {
+                push_u64(pairs, pcap, status + 1, ((unsigned long long)r << 32) | g.rule, status);
+                break;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ bool waf_active(const gm_verdict &v) {
+    return v.action == GM_ACT_PROXY && v.waf_mode != GM_WAF_OFF;
+}
+
+__global__ __launch_bounds__(256) void k_pairs_mark(const unsigned long long *__restrict__ p, uint32_t m,
+                                                    const gm_verdict *__restrict__ out, uint32_t *__restrict__ keep) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        const unsigned long long x = p[i];
+        bool k = (i == 0 || p[i - 1] != x) && waf_active(out[(uint32_t)(x >> 32)]);
+        keep[i] = k ? 1u : 0u;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pairs_emit(const unsigned long long *__restrict__ p, uint32_t m,
+                                                    const uint32_t *__restrict__ keep, const uint32_t *__restrict__ idx,
+                                                    gm_verdict *__restrict__ out, uint32_t *__restrict__ hit_ids,
+                                                    uint64_t hit_cap, unsigned long long *__restrict__ counters,
+                                                    uint32_t n_locs, uint32_t *__restrict__ status) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        if (i == m - 1) status[4] = idx[i] + keep[i];
+        if (!keep[i]) continue;
+        const unsigned long long x = p[i];
+        const uint32_t r = (uint32_t)(x >> 32), rule = (uint32_t)x;
+        const uint32_t o = idx[i];
+        if (o < hit_cap) hit_ids[o] = rule; else atomicOr(status + 3, 2u);
+        atomicAdd(&counters[n_locs + rule], 1ull);
+        if (i == 0 || (uint32_t)(p[i - 1] >> 32) != r) {
+            uint32_t cnt = 0;
+            for (uint32_t j = i; j < m && (uint32_t)(p[j] >> 32) == r; j++) cnt += keep[j];
+            gm_verdict &v = out[r];
+            v.first_hit_off = o;
+            v.n_hits = (uint16_t)min(cnt, 0xFFFFu);
+            if (v.waf_mode == GM_WAF_BLOCK && cnt) { v.action = GM_ACT_BLOCK; v.status = 403; }
+        }
+    }
+}
+
+}  // namespace
+
+// ============================================================================ host runtime
+struct Generation {
+    uint8_t *d_image = nullptr;
+    TabHeader hdr{};
+    GTab tab{};
+    gm_stats_t stats{};
+};
+
+struct gm_ctx {
+    int dev = 0;
+    uint32_t flags = 0;
+    Generation *gen = nullptr;
+    std::string err;
+    unsigned long long *d_counters = nullptr;
+    size_t n_counters = 0;
+    uint32_t *d_status = nullptr, *h_status = nullptr;
+    uint32_t *d_blk2rec = nullptr; size_t cap_blk = 0;
+    unsigned long long *d_cand = nullptr; size_t cap_cand = 0;
+    unsigned long long *d_pairs = nullptr, *d_pairs2 = nullptr; size_t cap_pairs = 0;
+    unsigned long long *d_jobs = nullptr, *d_jobs2 = nullptr; size_t cap_jobs = 0;
+    uint32_t *d_keep = nullptr, *d_idx = nullptr; size_t cap_keep = 0, cap_idx = 0;
+    uint8_t *d_temp = nullptr; size_t cap_temp = 0;
+    // host-staging (GM_BATCH_HOST)
+    uint8_t *d_stage = nullptr; size_t cap_stage = 0;
+    ncclComm_t comm = nullptr;
+    uint64_t last_candidates = 0, last_pairs = 0, last_hits = 0;
+    hipEvent_t ev[5] = {};
+    bool ev_pending = false;
+    int ev_used = 0;
+    float last_ms[4] = {0, 0, 0, 0};
+    int cu_count = 256;
+    std::mutex mu;
+};
+
+static thread_local std::string t_err;
+
+static int fail(gm_ctx *c, int code, const std::string &m) {
+    t_err = m;
+    if (c) c->err = m;
+    return code;
+}
+#define HIPCHK(c, x)                                                                         \
+    do {                                                                                     \
+        hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess) return fail((c), GM_E_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+template <class T>
+static int grow(gm_ctx *c, T *&p, size_t &cap, size_t need) {
+    if (need <= cap) return GM_OK;
+    if (p) HIPCHK(c, hipFree(p));
+    p = nullptr;
+    size_t nc = std::max(need, cap + cap / 2);
+    HIPCHK(c, hipMalloc((void **)&p, nc * sizeof(T)));
+    cap = nc;
+    return GM_OK;
+}
+
+extern "C" {
+
+uint32_t gm_abi_version(void) { return GM_ABI_VERSION; }
+
+gm_ctx *gm_create(int hip_device, uint32_t flags) {
+    gm_ctx *c = new gm_ctx();
+    c->dev = hip_device;
+    c->flags = flags;
+    if (!(flags & GM_CREATE_COMPILE_ONLY)) {
+        if (hipSetDevice(hip_device) != hipSuccess) { t_err = "hipSetDevice failed"; delete c; return nullptr; }
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
+            c->cu_count = cus;
+        if (hipMalloc((void **)&c->d_status, 64) != hipSuccess ||
+            hipHostMalloc((void **)&c->h_status, 64, hipHostMallocDefault) != hipSuccess) {
+            t_err = "status alloc failed"; delete c; return nullptr;
+        }
+        (void)hipFuncSetAttribute((const void *)k_waf_scan, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (WAF_A_WORDS + WAF_B_WORDS) * 4);
+        if (flags & GM_CREATE_PROFILE)
+            for (auto &e : c->ev) (void)hipEventCreate(&e);
+    }
+    return c;
+}
+
+void gm_destroy(gm_ctx *c) {
+    if (!c) return;
+    if (!(c->flags & GM_CREATE_COMPILE_ONLY)) {
+        (void)hipSetDevice(c->dev);
+        (void)hipDeviceSynchronize();
+        if (c->gen) (void)hipFree(c->gen->d_image);
+        for (void *p : {(void *)c->d_counters, (void *)c->d_status, (void *)c->d_blk2rec, (void *)c->d_cand,
+                        (void *)c->d_pairs, (void *)c->d_pairs2, (void *)c->d_jobs, (void *)c->d_jobs2,
+                        (void *)c->d_keep, (void *)c->d_idx, (void *)c->d_temp, (void *)c->d_stage})
+            if (p) (void)hipFree(p);
+        if (c->h_status) (void)hipHostFree(c->h_status);
+        if (c->comm) ncclCommDestroy(c->comm);
+        for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
+    }
+    delete c->gen;
+    delete c;
+}
+
+const char *gm_last_error(gm_ctx *c) { return c ? c->err.c_str() : t_err.c_str(); }
+
+int gm_load_generation(gm_ctx *c, const void *blob, size_t len, uint32_t gen) {
+    if (!c || !blob) return fail(c, GM_E_INVAL, "null argument");
+    std::lock_guard<std::mutex> lk(c->mu);
+    CompileResult R = compile_generation((const uint8_t *)blob, len, gen);
+    if (!R.ok) return fail(c, R.code, R.err);   // previous generation stays live
+    Generation *g = new Generation();
+    g->hdr = R.hdr;
+    g->stats = R.stats;
+    if (!(c->flags & GM_CREATE_COMPILE_ONLY)) {
+        HIPCHK(c, hipSetDevice(c->dev));
+        HIPCHK(c, hipMalloc((void **)&g->d_image, R.image.size()));
+        HIPCHK(c, hipMemcpy(g->d_image, R.image.data(), R.image.size(), hipMemcpyHostToDevice));
+        g->tab = make_gtab(g->hdr, g->d_image, gen);
+        size_t nctr = g->stats.n_counters;
+        if (nctr != c->n_counters || !c->d_counters) {
+            if (c->d_counters) HIPCHK(c, hipFree(c->d_counters));
+            HIPCHK(c, hipMalloc((void **)&c->d_counters, std::max<size_t>(nctr, 1) * 8));
+            c->n_counters = nctr;
+        }
+        HIPCHK(c, hipMemset(c->d_counters, 0, std::max<size_t>(nctr, 1) * 8));
+        // RCU-style swap: in-flight batches of the old generation complete first
+        HIPCHK(c, hipDeviceSynchronize());
+        if (c->gen) (void)hipFree(c->gen->d_image);
+    }
+    delete c->gen;
+    c->gen = g;
+    return GM_OK;
+}
+
+int gm_stats(gm_ctx *c, gm_stats_t *out) {
+    if (!c || !out) return fail(c, GM_E_INVAL, "null argument");
+    if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
+    *out = c->gen->stats;
+    out->last_candidates = c->last_candidates;
+    out->last_pairs = c->last_pairs;
+    out->last_hits = c->last_hits;
+    out->last_ms_route = c->last_ms[0]; out->last_ms_scan = c->last_ms[1];
+    out->last_ms_verify = c->last_ms[2]; out->last_ms_tail = c->last_ms[3];
+    return GM_OK;
+}
+
+static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t alen, uint32_t n, gm_verdict *out,
+                     uint32_t *hit_ids, size_t hit_cap, hipStream_t s) {
+    const Generation *g = c->gen;
+    const GTab &t = g->tab;
+    const bool waf = t.n_sigs > 0 && (t.n_lits > 0 || t.n_sig_regex > 0);
+    const uint32_t nblk = (uint32_t)((alen >> BLK_SHIFT) + 1);
+    if (waf) { int e = grow(c, c->d_blk2rec, c->cap_blk, nblk); if (e) return e; }
+    const bool prof = c->flags & GM_CREATE_PROFILE;
+    auto mark = [&](int k) -> int {
+        if (prof) { HIPCHK(c, hipEventRecord(c->ev[k], s)); c->ev_used = k + 1; c->ev_pending = true; }
+        return GM_OK;
+    };
+    c->ev_used = 0;
+    HIPCHK(c, hipMemsetAsync(c->d_status, 0, 64, s));
+    if (mark(0)) return GM_E_HIP;
+    {
+        uint32_t blocks = std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK, (uint32_t)c->cu_count * 8);
+        if (blocks == 0) blocks = 1;
+        k_route<<<blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, c->d_counters,
+                                                waf ? c->d_blk2rec : nullptr, nblk);
+        HIPCHK(c, hipGetLastError());
+    }
+    if (mark(1)) return GM_E_HIP;
+    c->last_candidates = c->last_pairs = c->last_hits = 0;
+    if (!waf || n == 0) return GM_OK;
+
+    const size_t ccap = alen / 64 + 65536, pcap = (size_t)n * 2 + 65536, jcap = (size_t)n + 65536;
+    int e;
+    if ((e = grow(c, c->d_cand, c->cap_cand, ccap))) return e;
+    { size_t cp = c->cap_pairs; if ((e = grow(c, c->d_pairs, cp, pcap))) return e;
+      size_t cp2 = c->cap_pairs; if ((e = grow(c, c->d_pairs2, cp2, pcap))) return e; c->cap_pairs = std::max(cp, cp2); }
+    { size_t cj = c->cap_jobs; if ((e = grow(c, c->d_jobs, cj, jcap))) return e;
+      size_t cj2 = c->cap_jobs; if ((e = grow(c, c->d_jobs2, cj2, jcap))) return e; c->cap_jobs = std::max(cj, cj2); }
+
+    {
+        const uint64_t nchunks = (alen + 1023) >> 10;
+        uint32_t blocks = (uint32_t)std::min<uint64_t>((nchunks + SCAN_WAVES - 1) / SCAN_WAVES, (uint64_t)c->cu_count * 2 * 8);
+        if (blocks == 0) blocks = 1;
+        k_waf_scan<<<blocks, SCAN_BLOCK, (WAF_A_WORDS + WAF_B_WORDS) * 4, s>>>(
+            A, alen, t.waf_a, t.waf_b, c->d_cand, (uint32_t)std::min<size_t>(c->cap_cand, 0xFFFFFFFFu), c->d_status);
+        HIPCHK(c, hipGetLastError());
+    }
+    if (mark(2)) return GM_E_HIP;
+    {
+        uint32_t blocks = (uint32_t)c->cu_count * 8;
+        k_waf_verify<<<blocks, 256, 0, s>>>(A, alen, reqs, n, c->d_blk2rec, t, c->d_cand,
+                                            (uint32_t)std::min<size_t>(c->cap_cand, 0xFFFFFFFFu), c->d_pairs,
+                                            (uint32_t)c->cap_pairs, c->d_jobs, (uint32_t)c->cap_jobs, c->d_status);
+        HIPCHK(c, hipGetLastError());
+    }
+    if (mark(3)) return GM_E_HIP;
+    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, 64, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->last_candidates = c->h_status[0];
+    if (c->h_status[3]) return fail(c, GM_E_OVERFLOW, "WAF candidate/pair/job capacity exceeded");
+    uint32_t nj = std::min<uint32_t>(c->h_status[2], (uint32_t)c->cap_jobs);
+    int rec_bits = 1;
+    while (rec_bits < 32 && (1ull << rec_bits) < n) rec_bits++;
+    if (nj) {
+        size_t need = 0;
+        HIPCHK(c, hipcub::DeviceRadixSort::SortKeys(nullptr, need, c->d_jobs, c->d_jobs2, (int)nj, 0, 32 + rec_bits, s));
+        if ((e = grow(c, c->d_temp, c->cap_temp, need))) return e;
+        HIPCHK(c, hipcub::DeviceRadixSort::SortKeys(c->d_temp, need, c->d_jobs, c->d_jobs2, (int)nj, 0, 32 + rec_bits, s));
+        k_waf_regex<<<std::min<uint32_t>((nj + 255) / 256, c->cu_count * 8), 256, 0, s>>>(
+            A, reqs, t, c->d_jobs2, nj, c->d_pairs, (uint32_t)c->cap_pairs, c->d_status);
+        HIPCHK(c, hipGetLastError());
+    }
+    if (t.n_always) {
+        k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(A, reqs, n, t, c->d_pairs, (uint32_t)c->cap_pairs, c->d_status);
+        HIPCHK(c, hipGetLastError());
+    }
+    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, 64, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (c->h_status[3]) return fail(c, GM_E_OVERFLOW, "WAF pair capacity exceeded");
+    uint32_t m = std::min<uint32_t>(c->h_status[1], (uint32_t)c->cap_pairs);
+    c->last_pairs = m;
+    if (m == 0) return mark(4) ? GM_E_HIP : GM_OK;
+    if ((e = grow(c, c->d_keep, c->cap_keep, m))) return e;
+    if ((e = grow(c, c->d_idx, c->cap_idx, m))) return e;
+    size_t need = 0;
+    HIPCHK(c, hipcub::DeviceRadixSort::SortKeys(nullptr, need, c->d_pairs, c->d_pairs2, (int)m, 0, 32 + rec_bits, s));
+    size_t need2 = 0;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, need2, c->d_keep, c->d_keep, (int)m, s));
+    if ((e = grow(c, c->d_temp, c->cap_temp, std::max(need, need2)))) return e;
+    HIPCHK(c, hipcub::DeviceRadixSort::SortKeys(c->d_temp, need, c->d_pairs, c->d_pairs2, (int)m, 0, 32 + rec_bits, s));
+    uint32_t blocks = std::min<uint32_t>((m + 255) / 256, c->cu_count * 8);
+    k_pairs_mark<<<blocks, 256, 0, s>>>(c->d_pairs2, m, out, c->d_keep);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->d_temp, need2, c->d_keep, c->d_idx, (int)m, s));
+    k_pairs_emit<<<blocks, 256, 0, s>>>(c->d_pairs2, m, c->d_keep, c->d_idx, out, hit_ids, hit_cap, c->d_counters,
+                                        t.n_locs, c->d_status);
+    HIPCHK(c, hipGetLastError());
+    if (mark(4)) return GM_E_HIP;
+    return GM_OK;
+}
+
+int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit_ids, size_t hit_cap, void *stream) {
+    if (!c || !in || !out) return fail(c, GM_E_INVAL, "null argument");
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
+    if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIPCHK(c, hipSetDevice(c->dev));
+    hipStream_t s = (hipStream_t)stream;
+    if (in->n == 0) return GM_OK;
+    if (((uintptr_t)in->arena & 15) || ((uintptr_t)in->reqs & 15) || ((uintptr_t)out & 15))
+        return fail(c, GM_E_INVAL, "reqs / arena / out must be 16-byte aligned");
+    if (!(in->flags & GM_BATCH_HOST))
+        return run_batch(c, in->reqs, in->arena, in->arena_len, in->n, out, hit_ids, hit_cap, s);
+    // host buffers: stage reqs + arena + verdicts + hits through HBM
+    size_t rq = (size_t)in->n * sizeof(gm_req), ar = (in->arena_len + 255) & ~255ull;
+    size_t vo = (size_t)in->n * sizeof(gm_verdict), ho = hit_cap * 4;
+    size_t tot = rq + ar + vo + ho + 1024;
+    int e = grow(c, c->d_stage, c->cap_stage, tot);
+    if (e) return e;
+    uint8_t *p = c->d_stage;
+    gm_req *dr = (gm_req *)p; p += (rq + 255) & ~255ull;
+    uint8_t *da = p; p += ar;
+    gm_verdict *dv = (gm_verdict *)p; p += (vo + 255) & ~255ull;
+    uint32_t *dh = (uint32_t *)p;
+    HIPCHK(c, hipMemcpyAsync(dr, in->reqs, rq, hipMemcpyHostToDevice, s));
+    if (in->arena_len) HIPCHK(c, hipMemcpyAsync(da, in->arena, in->arena_len, hipMemcpyHostToDevice, s));
+    e = run_batch(c, dr, da, in->arena_len, in->n, dv, dh, hit_cap, s);
+    if (e) return e;
+    HIPCHK(c, hipMemcpyAsync(out, dv, vo, hipMemcpyDeviceToHost, s));
+    if (hit_ids && hit_cap) HIPCHK(c, hipMemcpyAsync(hit_ids, dh, ho, hipMemcpyDeviceToHost, s));
+    return GM_OK;
+}
+
+int gm_sync(gm_ctx *c, void *stream) {
+    if (!c) return fail(c, GM_E_INVAL, "null ctx");
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return GM_OK;
+    HIPCHK(c, hipSetDevice(c->dev));
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, 64, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->last_hits = c->h_status[4];
+    if (c->ev_pending) {
+        for (int k = 0; k < 4; k++) {
+            c->last_ms[k] = 0;
+            if (k + 1 < c->ev_used) (void)hipEventElapsedTime(&c->last_ms[k], c->ev[k], c->ev[k + 1]);
+        }
+        c->ev_pending = false;
+    }
+    if (c->h_status[3]) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded");
+    return GM_OK;
+}
+
+int gm_counters(gm_ctx *c, uint64_t *out, size_t n) {
+    if (!c || !out) return fail(c, GM_E_INVAL, "null argument");
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
+    if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
+    HIPCHK(c, hipSetDevice(c->dev));
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(out, c->d_counters, std::min(n, c->n_counters) * 8, hipMemcpyDeviceToHost));
+    return GM_OK;
+}
+
+int gm_counters_reset(gm_ctx *c) {
+    if (!c) return fail(c, GM_E_INVAL, "null ctx");
+    if (c->flags & GM_CREATE_COMPILE_ONLY || !c->d_counters) return GM_OK;
+    HIPCHK(c, hipSetDevice(c->dev));
+    HIPCHK(c, hipMemset(c->d_counters, 0, std::max<size_t>(c->n_counters, 1) * 8));
+    return GM_OK;
+}
+
+int gm_comm_unique_id(void *out) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return fail(nullptr, GM_E_COMM, "ncclGetUniqueId failed");
+    memcpy(out, &id, sizeof id);
+    return GM_OK;
+}
+
+int gm_comm_init(gm_ctx *c, const void *uid, int nranks, int rank) {
+    if (!c || !uid) return fail(c, GM_E_INVAL, "null argument");
+    HIPCHK(c, hipSetDevice(c->dev));
+    ncclUniqueId id;
+    memcpy(&id, uid, sizeof id);
+    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+    if (r != ncclSuccess) return fail(c, GM_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    return GM_OK;
+}
+
+int gm_counters_allreduce(gm_ctx *c, void *stream) {
+    if (!c || !c->comm) return fail(c, GM_E_COMM, "gm_comm_init not called");
+    if (!c->d_counters) return fail(c, GM_E_NOGEN, "no counters");
+    ncclResult_t r = ncclAllReduce(c->d_counters, c->d_counters, c->n_counters, ncclUint64, ncclSum, c->comm,
+                                   (hipStream_t)stream);
+    if (r != ncclSuccess) return fail(c, GM_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    return GM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,642 @@
+// gm_regex.cpp -- regex (RE2-compatible subset, PCRE 8.x semantics) -> byte-class DFA + factors.
+// See gm_regex.hpp for the supported language.
+#include "gm_regex.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <bitset>
+#include <map>
+#include <unordered_map>
+
+namespace gm {
+namespace {
+
+using CSet = std::bitset<256>;
+
+struct Node {
+    enum K { EMPTY, SET, CAT, ALT, REP, BOL, EOL } k = EMPTY;
+    CSet set;
+    std::vector<int> kids;
+    int mn = 0, mx = 0;  // REP: mx < 0 = unbounded
+};
+
+struct Parser {
+    const std::string &p;
+    size_t i = 0;
+    bool icase = false, dotall = false;
+    RegexStatus st = RX_OK;
+    std::string err;
+    std::vector<Node> nodes;
+
+    explicit Parser(const std::string &s) : p(s) {}
+
+    int add(Node n) { nodes.push_back(std::move(n)); return (int)nodes.size() - 1; }
+    bool fail(RegexStatus s, const char *m) { if (st == RX_OK) { st = s; err = m; } return false; }
+    bool eof() const { return i >= p.size(); }
+
+    void fold(CSet &s) const {
+        if (!icase) return;
+        for (int c = 'a'; c <= 'z'; c++) {
+            if (s[c] || s[c - 32]) { s[c] = true; s[c - 32] = true; }
+        }
+    }
+    static CSet digit() { CSet s; for (int c = '0'; c <= '9'; c++) s[c] = true; return s; }
+    static CSet word() {
+        CSet s = digit();
+        for (int c = 'a'; c <= 'z'; c++) { s[c] = true; s[c - 32] = true; }
+        s['_'] = true; return s;
+    }
+    static CSet space() { CSet s; for (int c : {' ', '\t', '\n', '\v', '\f', '\r'}) s[c] = true; return s; }
+
+    int hexv(char c) {
+        if (c >= '0' && c <= '9') return c - '0';
+        if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+        if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+        return -1;
+    }
+
+    // escape after '\\' (i points past the backslash). Returns true and fills `out`.
+    bool escape(CSet &out, bool in_class) {
+        if (eof()) return fail(RX_SYNTAX, "trailing backslash");
+        char c = p[i++];
+        out.reset();
+        switch (c) {
+        case 'd': out = digit(); return true;
+        case 'D': out = ~digit(); return true;
+        case 'w': out = word(); return true;
+        case 'W': out = ~word(); return true;
+        case 's': out = space(); return true;
+        case 'S': out = ~space(); return true;
+        case 't': out['\t'] = true; return true;
+        case 'n': out['\n'] = true; return true;
+        case 'r': out['\r'] = true; return true;
+        case 'f': out['\f'] = true; return true;
+        case 'e': out[0x1b] = true; return true;
+        case 'a': out[0x07] = true; return true;
+        case 'x': {
+            int v = 0, n = 0;
+            if (!eof() && p[i] == '{') return fail(RX_UNSUPPORTED, "\\x{...}");
+            while (n < 2 && !eof() && hexv(p[i]) >= 0) { v = v * 16 + hexv(p[i++]); n++; }
+            out[v] = true; return true;
+        }
+        case 'b':
+            if (in_class) { out[0x08] = true; return true; }
+            return fail(RX_UNSUPPORTED, "\\b word boundary");
+        case '0': {
+            int v = 0, n = 0;
+            while (n < 2 && !eof() && p[i] >= '0' && p[i] <= '7') { v = v * 8 + (p[i++] - '0'); n++; }
+            out[v & 0xff] = true; return true;
+        }
+        default: break;
+        }
+        if (c >= '1' && c <= '9') return fail(RX_PCRE_ONLY, "backreference");
+        if (c == 'K') return fail(RX_PCRE_ONLY, "\\K");
+        if (c == 'G' || c == 'R' || c == 'X' || c == 'C' || c == 'g' || c == 'k') return fail(RX_PCRE_ONLY, "PCRE escape");
+        if (c == 'B' || c == 'A' || c == 'z' || c == 'Z') return fail(RX_UNSUPPORTED, "assertion escape");
+        if (c == 'p' || c == 'P' || c == 'h' || c == 'H' || c == 'v' || c == 'V' || c == 'N' || c == 'Q' ||
+            c == 'E' || c == 'c' || c == 'o' || c == 'u' || c == 'U' || c == 'l' || c == 'L')
+            return fail(RX_UNSUPPORTED, "escape");
+        if ((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z')) return fail(RX_UNSUPPORTED, "unknown escape");
+        out[(unsigned char)c] = true;
+        return true;
+    }
+
+    int parse_class() {   // after '['
+        CSet s;
+        bool neg = false;
+        if (!eof() && p[i] == '^') { neg = true; i++; }
+        bool first = true;
+        for (;;) {
+            if (eof()) { fail(RX_SYNTAX, "unterminated class"); return -1; }
+            char c = p[i];
+            if (c == ']' && !first) { i++; break; }
+            first = false;
+            if (c == '[' && i + 1 < p.size() && (p[i + 1] == ':' || p[i + 1] == '=' || p[i + 1] == '.')) {
+                fail(RX_UNSUPPORTED, "POSIX class"); return -1;
+            }
+            CSet lo; int lo_ch = -1;
+            i++;
+            if (c == '\\') {
+                if (!escape(lo, true)) return -1;
+                if (lo.count() == 1) for (int k = 0; k < 256; k++) if (lo[k]) lo_ch = k;
+            } else { lo[(unsigned char)c] = true; lo_ch = (unsigned char)c; }
+            if (lo_ch >= 0 && i + 1 < p.size() && p[i] == '-' && p[i + 1] != ']') {
+                i++;
+                char d = p[i++]; int hi_ch;
+                if (d == '\\') {
+                    CSet h; if (!escape(h, true)) return -1;
+                    if (h.count() != 1) { fail(RX_SYNTAX, "bad range"); return -1; }
+                    hi_ch = 0; for (int k = 0; k < 256; k++) if (h[k]) hi_ch = k;
+                } else hi_ch = (unsigned char)d;
+                if (hi_ch < lo_ch) { fail(RX_SYNTAX, "range out of order"); return -1; }
+                for (int k = lo_ch; k <= hi_ch; k++) s[k] = true;
+            } else s |= lo;
+        }
+        fold(s);
+        if (neg) s = ~s;   // PCRE: a negated class matches '\n' too
+        Node n; n.k = Node::SET; n.set = s;
+        return add(n);
+    }
+
+    int parse_atom() {
+        char c = p[i];
+        if (c == '(') {
+            i++;
+            if (!eof() && p[i] == '?') {
+                i++;
+                if (eof()) { fail(RX_SYNTAX, "bad group"); return -1; }
+                char t = p[i];
+                if (t == ':') i++;
+                else if (t == 'P' || t == '<' || t == '\'') {
+                    if (t == 'P') { i++; if (eof() || p[i] != '<') { fail(RX_PCRE_ONLY, "(?P"); return -1; } }
+                    if (p[i] == '<' && i + 1 < p.size() && (p[i + 1] == '=' || p[i + 1] == '!')) {
+                        fail(RX_PCRE_ONLY, "lookbehind"); return -1;
+                    }
+                    char close = p[i] == '\'' ? '\'' : '>';
+                    while (!eof() && p[i] != close) i++;
+                    if (eof()) { fail(RX_SYNTAX, "bad group name"); return -1; }
+                    i++;
+                } else if (t == '=' || t == '!' || t == '>' || t == '|' || t == '(' || t == 'R' ||
+                           t == '&' || t == '#' || t == 'C' || (t >= '0' && t <= '9') || t == '+') {
+                    fail(RX_PCRE_ONLY, "PCRE group construct"); return -1;
+                } else { fail(RX_UNSUPPORTED, "inline flags inside pattern"); return -1; }
+            }
+            int r = parse_alt();
+            if (r < 0) return -1;
+            if (eof() || p[i] != ')') { fail(RX_SYNTAX, "missing )"); return -1; }
+            i++;
+            return r;
+        }
+        if (c == '[') { i++; return parse_class(); }
+        if (c == '.') {
+            i++; Node n; n.k = Node::SET; n.set.set(); if (!dotall) n.set['\n'] = false; return add(n);
+        }
+        if (c == '^') { i++; Node n; n.k = Node::BOL; return add(n); }
+        if (c == '$') { i++; Node n; n.k = Node::EOL; return add(n); }
+        if (c == '*' || c == '+' || c == '?') { fail(RX_SYNTAX, "nothing to repeat"); return -1; }
+        i++;
+        Node n; n.k = Node::SET;
+        if (c == '\\') { if (!escape(n.set, false)) return -1; }
+        else n.set[(unsigned char)c] = true;
+        fold(n.set);
+        return add(n);
+    }
+
+    bool quant(int &mn, int &mx) {   // at a possible quantifier; returns false if none
+        if (eof()) return false;
+        char c = p[i];
+        if (c == '*') { i++; mn = 0; mx = -1; return true; }
+        if (c == '+') { i++; mn = 1; mx = -1; return true; }
+        if (c == '?') { i++; mn = 0; mx = 1; return true; }
+        if (c == '{') {
+            size_t j = i + 1; int a = 0, b = -1, da = 0, db = 0; bool comma = false;
+            while (j < p.size() && isdigit((unsigned char)p[j])) { a = a * 10 + (p[j] - '0'); j++; da++; }
+            if (j < p.size() && p[j] == ',') {
+                comma = true; j++; b = 0;
+                while (j < p.size() && isdigit((unsigned char)p[j])) { b = b * 10 + (p[j] - '0'); j++; db++; }
+            }
+            if (j >= p.size() || p[j] != '}' || da == 0) return false;   // literal '{'
+            i = j + 1;
+            mn = a; mx = comma ? (db ? b : -1) : a;
+            if (mx >= 0 && mx < mn) { fail(RX_SYNTAX, "bad {n,m}"); return false; }
+            if (mn > 1000 || mx > 1000) { fail(RX_TOO_BIG, "repeat count"); return false; }
+            return true;
+        }
+        return false;
+    }
+
+    int parse_rep() {
+        int a = parse_atom();
+        if (a < 0) return -1;
+        for (;;) {
+            int mn, mx;
+            if (!quant(mn, mx)) { if (st != RX_OK) return -1; return a; }
+            if (nodes[a].k == Node::BOL || nodes[a].k == Node::EOL) { fail(RX_UNSUPPORTED, "quantified anchor"); return -1; }
+            if (!eof() && p[i] == '+') { fail(RX_PCRE_ONLY, "possessive quantifier"); return -1; }
+            if (!eof() && p[i] == '?') i++;   // lazy: same language
+            Node n; n.k = Node::REP; n.kids = {a}; n.mn = mn; n.mx = mx;
+            a = add(n);
+            if (!eof() && (p[i] == '*' || p[i] == '+' || p[i] == '?')) { fail(RX_SYNTAX, "nothing to repeat"); return -1; }
+        }
+    }
+
+    int parse_cat() {
+        Node n; n.k = Node::CAT;
+        while (!eof() && p[i] != '|' && p[i] != ')') {
+            int r = parse_rep();
+            if (r < 0) return -1;
+            n.kids.push_back(r);
+        }
+        if (n.kids.empty()) { Node e; e.k = Node::EMPTY; return add(e); }
+        if (n.kids.size() == 1) return n.kids[0];
+        return add(n);
+    }
+
+    int parse_alt() {
+        int a = parse_cat();
+        if (a < 0) return -1;
+        if (eof() || p[i] != '|') return a;
+        Node n; n.k = Node::ALT; n.kids = {a};
+        while (!eof() && p[i] == '|') {
+            i++;
+            int b = parse_cat();
+            if (b < 0) return -1;
+            n.kids.push_back(b);
+        }
+        return add(n);
+    }
+
+    int parse() {
+        // leading inline flags (?i) (?s) (?is) ...
+        while (i + 2 < p.size() && p[i] == '(' && p[i + 1] == '?') {
+            size_t j = i + 2; bool ok = true, any = false; bool fi = icase, fs = dotall;
+            while (j < p.size() && p[j] != ')') {
+                if (p[j] == 'i') fi = true; else if (p[j] == 's') fs = true; else { ok = false; break; }
+                j++; any = true;
+            }
+            if (!ok || !any || j >= p.size()) break;
+            icase = fi; dotall = fs; i = j + 1;
+        }
+        int r = parse_alt();
+        if (r >= 0 && !eof()) { fail(RX_SYNTAX, "unmatched )"); return -1; }
+        return r;
+    }
+};
+
+// anchors: ^ only in head position, $ only in tail position (else unsupported)
+bool check_anchors(const std::vector<Node> &N, int n, bool head, bool tail) {
+    const Node &x = N[n];
+    switch (x.k) {
+    case Node::BOL: return head;
+    case Node::EOL: return tail;
+    case Node::SET: case Node::EMPTY: return true;
+    case Node::REP: return check_anchors(N, x.kids[0], false, false);
+    case Node::ALT:
+        for (int k : x.kids) if (!check_anchors(N, k, head, tail)) return false;
+        return true;
+    case Node::CAT: {
+        // head position persists across leading anchors/empties
+        size_t m = x.kids.size();
+        for (size_t k = 0; k < m; k++) {
+            bool h = head, t = tail;
+            for (size_t q = 0; q < k; q++) { auto kk = N[x.kids[q]].k; if (kk != Node::BOL && kk != Node::EMPTY) h = false; }
+            for (size_t q = k + 1; q < m; q++) { auto kk = N[x.kids[q]].k; if (kk != Node::EOL && kk != Node::EMPTY) t = false; }
+            if (!check_anchors(N, x.kids[k], h, t)) return false;
+        }
+        return true;
+    }
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------- Thompson NFA
+struct NS { enum T { SET, SPLIT, EPS, BOL, EOL, MATCH } t; int set; int out, out1; };
+
+struct NfaBuilder {
+    const std::vector<Node> &N;
+    std::vector<NS> st;
+    std::vector<CSet> sets;
+    bool too_big = false;
+    explicit NfaBuilder(const std::vector<Node> &n) : N(n) {}
+
+    int mk(NS s) { st.push_back(s); if (st.size() > 200000) too_big = true; return (int)st.size() - 1; }
+    struct Frag { int start; std::vector<int *> dummy; std::vector<std::pair<int, int>> outs; };  // (state, which)
+
+    void patch(const std::vector<std::pair<int, int>> &outs, int to) {
+        for (auto &o : outs) (o.second == 0 ? st[o.first].out : st[o.first].out1) = to;
+    }
+
+    Frag build(int n) {
+        if (too_big) return Frag{mk({NS::EPS, -1, -1, -1}), {}, {}};
+        const Node &x = N[n];
+        switch (x.k) {
+        case Node::EMPTY: { int s = mk({NS::EPS, -1, -1, -1}); return Frag{s, {}, {{s, 0}}}; }
+        case Node::BOL: { int s = mk({NS::BOL, -1, -1, -1}); return Frag{s, {}, {{s, 0}}}; }
+        case Node::EOL: { int s = mk({NS::EOL, -1, -1, -1}); return Frag{s, {}, {{s, 0}}}; }
+        case Node::SET: {
+            sets.push_back(x.set);
+            int s = mk({NS::SET, (int)sets.size() - 1, -1, -1});
+            return Frag{s, {}, {{s, 0}}};
+        }
+        case Node::CAT: {
+            Frag f = build(x.kids[0]);
+            for (size_t k = 1; k < x.kids.size(); k++) {
+                Frag g = build(x.kids[k]);
+                patch(f.outs, g.start);
+                f.outs = g.outs;
+            }
+            return f;
+        }
+        case Node::ALT: {
+            Frag f = build(x.kids[0]);
+            for (size_t k = 1; k < x.kids.size(); k++) {
+                Frag g = build(x.kids[k]);
+                int s = mk({NS::SPLIT, -1, f.start, g.start});
+                f.start = s;
+                f.outs.insert(f.outs.end(), g.outs.begin(), g.outs.end());
+            }
+            return f;
+        }
+        case Node::REP: {
+            int kid = x.kids[0];
+            int mn = x.mn, mx = x.mx;
+            int entry = mk({NS::EPS, -1, -1, -1});
+            std::vector<std::pair<int, int>> outs = {{entry, 0}};
+            for (int r = 0; r < mn; r++) {
+                Frag g = build(kid);
+                patch(outs, g.start); outs = g.outs;
+            }
+            if (mx < 0) {
+                Frag g = build(kid);
+                int sp = mk({NS::SPLIT, -1, g.start, -1});
+                patch(outs, sp);
+                patch(g.outs, sp);
+                outs = {{sp, 1}};
+            } else {
+                std::vector<std::pair<int, int>> skips;
+                for (int r = mn; r < mx; r++) {
+                    Frag g = build(kid);
+                    int sp = mk({NS::SPLIT, -1, g.start, -1});
+                    patch(outs, sp);
+                    skips.push_back({sp, 1});
+                    outs = g.outs;
+                }
+                outs.insert(outs.end(), skips.begin(), skips.end());
+            }
+            return Frag{entry, {}, outs};
+        }
+        }
+        return Frag{mk({NS::EPS, -1, -1, -1}), {}, {}};
+    }
+};
+
+// ---------------------------------------------------------------- factors
+struct FI {
+    bool exact_ok = false;
+    std::vector<std::string> exact;
+    std::vector<std::string> best;   // best OR-set found anywhere inside (empty = none)
+};
+
+int score_len(const std::vector<std::string> &s) {
+    if (s.empty()) return -1;
+    size_t m = SIZE_MAX;
+    for (auto &x : s) m = std::min(m, x.size());
+    return (int)m;
+}
+bool better(const std::vector<std::string> &a, const std::vector<std::string> &b) {   // a better than b
+    int la = score_len(a), lb = score_len(b);
+    if (la != lb) return la > lb;
+    return !a.empty() && (b.empty() || a.size() < b.size());
+}
+void uniq(std::vector<std::string> &v) { std::sort(v.begin(), v.end()); v.erase(std::unique(v.begin(), v.end()), v.end()); }
+void take_best(std::vector<std::string> &best, const std::vector<std::string> &cand) {
+    if (score_len(cand) > 0 && better(cand, best)) best = cand;
+}
+
+FI factors(const std::vector<Node> &N, int n) {
+    const Node &x = N[n];
+    FI r;
+    switch (x.k) {
+    case Node::EMPTY: case Node::BOL: case Node::EOL:
+        r.exact_ok = true; r.exact = {""}; return r;
+    case Node::SET: {
+        std::vector<int> chars;
+        CSet f;
+        for (int c = 0; c < 256; c++) if (x.set[c]) f[(c >= 'A' && c <= 'Z') ? c | 0x20 : c] = true;
+        if (f.count() <= 4) {
+            r.exact_ok = true;
+            for (int c = 0; c < 256; c++) if (f[c]) r.exact.push_back(std::string(1, (char)c));
+        }
+        return r;
+    }
+    case Node::CAT: {
+        std::vector<std::string> cur = {""};
+        bool cur_ok = true, all_exact = true;
+        for (int k : x.kids) {
+            FI g = factors(N, k);
+            take_best(r.best, g.best);
+            if (g.exact_ok && cur_ok && cur.size() * g.exact.size() <= 16) {
+                std::vector<std::string> nx;
+                for (auto &a : cur) for (auto &b : g.exact) nx.push_back(a + b);
+                uniq(nx);
+                bool too_long = false; for (auto &s : nx) if (s.size() > 32) too_long = true;
+                if (!too_long) { cur = nx; continue; }
+            }
+            // chain breaks here
+            all_exact = false;
+            take_best(r.best, cur);
+            if (g.exact_ok) { cur = g.exact; cur_ok = true; }
+            else { cur = {""}; cur_ok = true; }
+        }
+        take_best(r.best, cur);
+        if (all_exact) { r.exact_ok = true; r.exact = cur; }
+        return r;
+    }
+    case Node::ALT: {
+        bool all_exact = true, all_req = true;
+        std::vector<std::string> ex, un;
+        for (int k : x.kids) {
+            FI g = factors(N, k);
+            if (g.exact_ok) ex.insert(ex.end(), g.exact.begin(), g.exact.end()); else all_exact = false;
+            std::vector<std::string> b = g.best;
+            if (g.exact_ok) take_best(b, g.exact);
+            if (score_len(b) <= 0) all_req = false; else un.insert(un.end(), b.begin(), b.end());
+        }
+        uniq(ex); uniq(un);
+        if (all_exact && ex.size() <= 16) { r.exact_ok = true; r.exact = ex; }
+        if (all_req) r.best = un;
+        return r;
+    }
+    case Node::REP: {
+        FI g = factors(N, x.kids[0]);
+        if (x.mn >= 1) {
+            r.best = g.best;
+            if (g.exact_ok) take_best(r.best, g.exact);
+            if (x.mn == x.mx && g.exact_ok) {
+                std::vector<std::string> cur = {""};
+                bool ok = true;
+                for (int q = 0; q < x.mn && ok; q++) {
+                    std::vector<std::string> nx;
+                    for (auto &a : cur) for (auto &b : g.exact) nx.push_back(a + b);
+                    uniq(nx);
+                    if (nx.size() > 16) ok = false;
+                    for (auto &s : nx) if (s.size() > 32) ok = false;
+                    cur = nx;
+                }
+                if (ok) { r.exact_ok = true; r.exact = cur; }
+            }
+        }
+        return r;
+    }
+    }
+    return r;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- DFA construction
+RegexInfo compile_regex(const std::string &pattern, bool caseless, int max_states) {
+    RegexInfo out;
+    Parser P(pattern);
+    P.icase = caseless;
+    int root = P.parse();
+    if (root < 0 || P.st != RX_OK) {
+        out.status = P.st == RX_OK ? RX_SYNTAX : P.st;
+        out.error = P.err;
+        return out;
+    }
+    if (!check_anchors(P.nodes, root, true, true)) { out.status = RX_UNSUPPORTED; out.error = "anchor position"; return out; }
+
+    NfaBuilder B(P.nodes);
+    auto f = B.build(root);
+    int match = B.mk({NS::MATCH, -1, -1, -1});
+    B.patch(f.outs, match);
+    int start = f.start;
+    if (B.too_big) { out.status = RX_TOO_BIG; out.error = "nfa too big"; return out; }
+
+    // byte classes: refine by membership in every set
+    std::vector<int> cls(256, 0);
+    {
+        std::map<std::vector<bool>, int> sig;
+        for (int b = 0; b < 256; b++) {
+            std::vector<bool> v(B.sets.size());
+            for (size_t s = 0; s < B.sets.size(); s++) v[s] = B.sets[s][b];
+            auto it = sig.find(v);
+            if (it == sig.end()) { int id = (int)sig.size(); sig[v] = id; cls[b] = id; }
+            else cls[b] = it->second;
+        }
+        out.dfa.n_classes = (int)sig.size();
+    }
+    std::vector<int> rep(out.dfa.n_classes, 0);
+    for (int b = 255; b >= 0; b--) rep[cls[b]] = b;
+
+    const auto &S = B.st;
+    auto closure = [&](std::vector<int> seeds, bool bol) {
+        std::vector<char> seen(S.size(), 0);
+        std::vector<int> stack = std::move(seeds), res;
+        while (!stack.empty()) {
+            int s = stack.back(); stack.pop_back();
+            if (s < 0 || seen[s]) continue;
+            seen[s] = 1;
+            switch (S[s].t) {
+            case NS::SPLIT: stack.push_back(S[s].out); stack.push_back(S[s].out1); break;
+            case NS::EPS: stack.push_back(S[s].out); break;
+            case NS::BOL: if (bol) stack.push_back(S[s].out); break;
+            default: res.push_back(s); break;   // SET, EOL, MATCH kept
+            }
+        }
+        std::sort(res.begin(), res.end());
+        return res;
+    };
+    auto end_accept = [&](const std::vector<int> &set) {
+        // follow EOL edges (and epsilons) to MATCH
+        std::vector<int> seeds;
+        for (int s : set) { if (S[s].t == NS::MATCH) return true; if (S[s].t == NS::EOL) seeds.push_back(S[s].out); }
+        std::vector<char> seen(S.size(), 0);
+        while (!seeds.empty()) {
+            int s = seeds.back(); seeds.pop_back();
+            if (s < 0 || seen[s]) continue;
+            seen[s] = 1;
+            if (S[s].t == NS::MATCH) return true;
+            if (S[s].t == NS::SPLIT) { seeds.push_back(S[s].out); seeds.push_back(S[s].out1); }
+            else if (S[s].t == NS::EPS || S[s].t == NS::EOL) seeds.push_back(S[s].out);
+        }
+        return false;
+    };
+    auto useful = [&](const std::vector<int> &set) {
+        for (int s : set) if (S[s].t != NS::BOL) return true;
+        return false;
+    };
+
+    std::vector<int> restart = closure({start}, false);
+    bool has_restart = false;
+    for (int s : restart) if (S[s].t == NS::SET || S[s].t == NS::MATCH || S[s].t == NS::EOL) has_restart = true;
+    out.dfa.anchored_start = !has_restart;
+
+    std::map<std::vector<int>, int> ids;
+    std::vector<std::vector<int>> sets;
+    sets.push_back({});                       // 0 = dead
+    std::vector<int> s0 = closure({start}, true);
+    ids[s0] = 1; sets.push_back(s0);
+    std::vector<uint16_t> trans;
+    std::vector<uint8_t> acc;
+    const int C = out.dfa.n_classes;
+    for (size_t cur = 0; cur < sets.size(); cur++) {
+        trans.resize((cur + 1) * C, 0);
+        uint8_t a = 0;
+        if (cur != 0) {
+            for (int s : sets[cur]) if (S[s].t == NS::MATCH) a |= 1;
+            if (end_accept(sets[cur])) a |= 2;
+        }
+        acc.push_back(a);
+        if (cur == 0) continue;
+        if (a & 1) {   // absorbing: a match already exists
+            for (int c = 0; c < C; c++) trans[cur * C + c] = (uint16_t)cur;
+            continue;
+        }
+        for (int c = 0; c < C; c++) {
+            int b = rep[c];
+            std::vector<int> seeds;
+            for (int s : sets[cur]) if (S[s].t == NS::SET && B.sets[S[s].set][b]) seeds.push_back(S[s].out);
+            if (has_restart) seeds.push_back(start);
+            std::vector<int> nx = closure(seeds, false);
+            int id;
+            if (!useful(nx) || (!has_restart && nx.empty())) id = 0;
+            else {
+                auto it = ids.find(nx);
+                if (it == ids.end()) {
+                    id = (int)sets.size();
+                    if (id >= max_states) { out.status = RX_TOO_BIG; out.error = "dfa too big"; return out; }
+                    ids[nx] = id; sets.push_back(nx);
+                } else id = it->second;
+            }
+            trans[cur * C + c] = (uint16_t)id;
+        }
+    }
+    out.dfa.trans = std::move(trans);
+    out.dfa.acc = std::move(acc);
+    out.dfa.n_states = (int)sets.size();
+    for (int b = 0; b < 256; b++) out.dfa.cls[b] = (uint8_t)cls[b];
+
+    FI fi = factors(P.nodes, root);
+    std::vector<std::string> best = fi.best;
+    if (fi.exact_ok) take_best(best, fi.exact);
+    if (score_len(best) > 0) { out.factors = best; out.min_factor = score_len(best); }
+    out.status = RX_OK;
+    return out;
+}
+
+bool dfa_search(const Dfa &d, const uint8_t *s, size_t n) {
+    int st = 1;
+    if (d.acc[st] & 1) return true;
+    for (size_t i = 0; i < n; i++) {
+        if ((d.acc[st] & 2) && i + 1 == n && s[i] == '\n') return true;
+        st = d.trans[(size_t)st * d.n_classes + d.cls[s[i]]];
+        if (st == 0) return false;
+        if (d.acc[st] & 1) return true;
+    }
+    return (d.acc[st] & 2) != 0;
+}
+
+}  // namespace gm
+
+// ---------------------------------------------------------------- debug exports (gpumatch_debug.h)
+extern "C" int gm_debug_regex(const char *pat, int caseless, const uint8_t *subj, size_t n) {
+    gm::RegexInfo ri = gm::compile_regex(pat, caseless != 0);
+    if (ri.status != gm::RX_OK) return -(int)ri.status;
+    return gm::dfa_search(ri.dfa, subj, n) ? 1 : 0;
+}
+
+extern "C" int gm_debug_regex_factors(const char *pat, int caseless, char *out, size_t cap) {
+    gm::RegexInfo ri = gm::compile_regex(pat, caseless != 0);
+    if (ri.status != gm::RX_OK) return -(int)ri.status;
+    size_t o = 0;
+    for (auto &f : ri.factors) {
+        if (o + f.size() + 1 > cap) break;
+        memcpy(out + o, f.data(), f.size());
+        o += f.size();
+        out[o++] = '\n';
+    }
+    if (o < cap) out[o] = 0;
+    return ri.min_factor;
+}

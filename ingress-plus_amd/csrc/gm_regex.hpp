@@ -1,0 +1,41 @@
+// gm_regex.hpp -- RE2-compatible regex subset -> byte-class DFA, plus required-literal factors.
+//
+// Semantics follow PCRE 8.x as nginx uses it (ngx_regex_compile, no PCRE_MULTILINE /
+// PCRE_DOTALL; `~*` adds PCRE_CASELESS): `.` excludes '\n', `^` = subject start, `$` = subject
+// end or before a final '\n', \s = [\t\n\v\f\r ], \w = [0-9A-Za-z_], ASCII case folding.
+// PCRE-only constructs (backrefs, lookaround, atomic groups, possessive quantifiers, \K,
+// recursion, conditionals, callouts) are rejected with RX_PCRE_ONLY and counted by the caller
+// (SURVEY.md §8 A8).
+#pragma once
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+namespace gm {
+
+enum RegexStatus { RX_OK = 0, RX_PCRE_ONLY = 1, RX_UNSUPPORTED = 2, RX_SYNTAX = 3, RX_TOO_BIG = 4 };
+
+struct Dfa {
+    // state 0 = dead, state 1 = start.  acc bit0: accepting (match found once reached),
+    // bit1: accepting at end of subject ($ satisfied).
+    std::vector<uint16_t> trans;   // [n_states * n_classes]
+    std::vector<uint8_t> acc;
+    uint8_t cls[256];
+    int n_states = 0, n_classes = 0;
+    bool anchored_start = false;   // every start path begins with ^ (no search prefix)
+};
+
+struct RegexInfo {
+    RegexStatus status = RX_SYNTAX;
+    std::string error;
+    Dfa dfa;
+    std::vector<std::string> factors;  // case-folded literals; every match contains one of them
+    int min_factor = 0;                // shortest factor length (0 = no factor)
+};
+
+RegexInfo compile_regex(const std::string &pattern, bool caseless, int max_states = 8192);
+
+// Host evaluation with PCRE search semantics (used for compile-time map truth tables).
+bool dfa_search(const Dfa &d, const uint8_t *s, size_t n);
+
+}  // namespace gm

@@ -1,0 +1,200 @@
+// gm_tables.hpp -- device-resident table generation: layout shared by the host compiler
+// (gm_compile.cpp) and the gfx950 kernels (gm_device.hip).
+//
+// One generation = one contiguous image in HBM (copy-in at gm_load_generation).  Every section
+// is an array of plain structs at a 16-byte aligned offset; `GTab` carries the device pointers
+// by value into every kernel launch.  Sizes are small (KB..MB) and read-mostly, so after first
+// touch they live in L2 / Infinity Cache; the hot WAF bitmap is staged into LDS per workgroup.
+#pragma once
+#include <stdint.h>
+
+#ifndef __HIPCC__
+#ifndef __host__
+#define __host__
+#endif
+#ifndef __device__
+#define __device__
+#endif
+#endif
+
+namespace gm {
+
+// ---- servers / hosts -----------------------------------------------------------------
+struct DPort {               // one entry per distinct listen port
+    uint32_t port;
+    uint32_t ssl;            // any `listen <port> ssl`
+    uint32_t default_server; // `default_server` or first server listening on the port
+    uint32_t pad;
+};
+
+// open-addressing hash: exact names and wildcard keys, keyed by (port index, lowercase name)
+struct DName {
+    uint32_t hash;           // 0 = empty slot
+    uint32_t name_off;       // into bytes pool
+    uint16_t name_len;
+    uint16_t port_idx;
+    uint32_t server;
+};
+
+enum : uint32_t { SIF_EQ = 1, SIF_NE = 2, SIF_RETURN = 3 };
+struct DServer {
+    uint32_t trie_root;      // node index of this server's location trie
+    uint32_t first_if, n_if; // server rewrite-phase `if (...) { return }` list (DServerIf)
+    uint32_t first_rloc, n_rloc;  // regex locations (DRegexLoc), config order
+    uint32_t waf_mode;
+    uint32_t pad[2];
+};
+struct DServerIf {
+    uint32_t op;             // SIF_*
+    uint32_t src;            // DSrc index (variable), unused for SIF_RETURN
+    uint32_t val_off, val_len;  // literal (case-sensitive compare, ngx_http_script_equal_code)
+    uint32_t code;           // return code
+    uint32_t pad[3];
+};
+struct DRegexLoc { uint32_t dfa; uint32_t loc; };
+
+// ---- location trie ---------------------------------------------------------------------
+struct DNode {
+    int32_t prefix_loc;      // prefix / ^~ location whose name ends here, -1 none
+    int32_t exact_loc;       // `location = ...` ending here
+    int32_t ar_loc;          // auto_redirect target: location named <this>/ (only if nothing ends here)
+    uint32_t pad;
+};
+struct DEdge { uint32_t key; uint32_t child; };   // key = node*256 + byte + 1, 0 = empty
+
+// ---- locations -------------------------------------------------------------------------
+enum : uint8_t { LK_PROXY = 0, LK_RETURN = 1, LK_IRL_SPLIT = 2, LK_IRL_RULES = 3, LK_UNSUPPORTED = 4,
+                 LK_NONE = 5, LK_IRL_EMPTY = 6 };
+struct DLoc {
+    uint8_t  kind;           // LK_*
+    uint8_t  noregex;        // ^~
+    uint8_t  waf_mode;
+    uint8_t  is_named;
+    uint32_t upstream;       // GM_NONE if not a known upstream
+    uint32_t ret_code;
+    uint32_t route;          // DSplit / DRules index for IRLs
+};
+
+// ---- request variables ---------------------------------------------------------------
+enum : uint8_t { SRC_HTTP = 1, SRC_COOKIE = 2, SRC_ARG = 3, SRC_VAR = 4 };
+enum : uint8_t { V_SCHEME = 1, V_HTTPS, V_HTTP2, V_METHOD, V_ARGS, V_URI, V_REQUEST_URI, V_REQUEST,
+                 V_REQUEST_BODY, V_REMOTE_ADDR, V_REMOTE_PORT, V_SERVER_PORT, V_REQUEST_ID, V_HOST };
+struct DSrc {
+    uint8_t  kind;           // SRC_*
+    uint8_t  var;            // V_* for SRC_VAR
+    uint8_t  join;           // $http_cookie -> ';', $http_x_forwarded_for -> ','
+    uint8_t  pad;
+    uint32_t name_off, name_len;   // lowercase header name with '_' / cookie / arg name
+};
+
+// ---- rules routes (compiled map chains) ----------------------------------------------
+// A condition node evaluates one map: value(src) vs one key (lowercase literal, or a DFA on
+// the raw value that is only run for a non-empty value, ngx_http_map_find), then branches.
+// next_* >= 0: another node; NEXT_0 / NEXT_1: the chain's constant result.
+enum : int32_t { NEXT_0 = -1, NEXT_1 = -2 };
+struct DCond {
+    uint32_t src;            // DSrc index
+    uint32_t is_regex;
+    uint32_t key_off, key_len;   // literal (lowercased)
+    uint32_t dfa;
+    int32_t  next_true, next_false;
+    uint32_t pad;
+};
+struct DRules {
+    uint32_t first_chain, n_chains;  // chain head node ids in DChainHead[]
+    uint32_t table_off;              // 2^n_chains entries (uint8 result index, 0xFF = default)
+    uint32_t first_target, n_targets;// n_targets = #params (result index -> named location)
+    uint32_t default_target;         // named location id, GM_NONE -> empty (302)
+    uint32_t pad[2];
+};
+struct DSplit {
+    uint32_t first_part, n_parts;    // DPart
+    uint32_t src;                    // DSrc (normally $request_id)
+    uint32_t pad;
+};
+struct DPart { uint32_t bound; uint32_t star; uint32_t target; uint32_t pad; };  // target GM_NONE -> empty
+
+// ---- DFAs (regex) ----------------------------------------------------------------------
+enum : uint32_t { DFA_ANCHOR_START = 1, DFA_ANCHOR_END = 2 };
+struct DDfa {
+    uint32_t trans_off;      // uint16 [n_states][n_classes] into dfa_trans; state 0 = dead, 1 = start
+    uint32_t acc_off;        // uint8 [n_states] accept flags into dfa_acc
+    uint32_t cls_off;        // uint8 [256] byte -> class into dfa_cls
+    uint16_t n_states, n_classes;
+    uint32_t flags;          // DFA_ANCHOR_*
+    uint32_t pad[3];
+};
+
+// ---- WAF signatures ----------------------------------------------------------------------
+constexpr int WAF_A_BITS = 19;       // LDS bitmap A: 2^19 bits = 64 KiB
+constexpr int WAF_B_BITS = 16;       // LDS bitmap B: 2^16 bits =  8 KiB (only probed on A hits)
+constexpr int BLK_SHIFT = 10;        // arena block (1 KiB) -> first record index (blk2rec)
+
+enum : uint8_t { LIT_NOCASE = 1, LIT_TRIGGER = 2 };
+struct DLitBucket { uint32_t key; uint32_t first; uint32_t count; uint32_t pad; };  // key = folded 4-gram + 1? see kWafEmpty
+struct DLit {
+    uint32_t id;             // signature rule id (LIT) or regex index (TRIGGER)
+    uint32_t bytes_off;      // pattern bytes (folded if NOCASE)
+    uint16_t len;
+    uint8_t  flags;          // LIT_*
+    uint8_t  zones;          // bit0 uri, bit1 args, bit2 hdrs, bit3 body
+    uint32_t pad;
+};
+struct DSigRegex {
+    uint32_t dfa;
+    uint32_t rule;           // signature rule id
+    uint32_t zones;
+    uint32_t always;         // no >= 4-byte required factor: run on every request
+};
+
+struct TabHeader {
+    uint32_t magic, version;
+    uint32_t n_ports, n_names_cap, n_wild_head_cap, n_wild_tail_cap;
+    uint32_t n_servers, n_server_ifs, n_rlocs, n_nodes, n_edges_cap, n_locs;
+    uint32_t n_srcs, n_conds, n_chain_heads, n_rules, n_splits, n_parts, n_dfas;
+    uint32_t n_lit_buckets_cap, n_lits, n_sig_regex, n_always, n_sigs;
+    uint64_t off_ports, off_names, off_wild_head, off_wild_tail, off_servers, off_server_ifs, off_rlocs,
+             off_nodes, off_edges, off_locs, off_srcs, off_conds, off_chain_heads, off_rules, off_rtab,
+             off_rtargets, off_splits, off_parts, off_dfas, off_dfa_trans, off_dfa_acc, off_dfa_cls,
+             off_bytes, off_waf_a, off_waf_b, off_lit_buckets, off_lits, off_sig_regex, off_always;
+    uint64_t total;
+};
+
+struct GTab {                // device pointers, built on host from the image base
+    const DPort *ports; const DName *names; const DName *wild_head; const DName *wild_tail;
+    const DServer *servers; const DServerIf *server_ifs; const DRegexLoc *rlocs;
+    const DNode *nodes; const DEdge *edges; const DLoc *locs;
+    const DSrc *srcs; const DCond *conds; const uint32_t *chain_heads; const DRules *rules;
+    const uint8_t *rtab; const uint32_t *rtargets; const DSplit *splits; const DPart *parts;
+    const DDfa *dfas; const uint16_t *dfa_trans; const uint8_t *dfa_acc; const uint8_t *dfa_cls;
+    const uint8_t *bytes; const uint32_t *waf_a; const uint32_t *waf_b;
+    const DLitBucket *lit_buckets; const DLit *lits; const DSigRegex *sig_regex; const uint32_t *always;
+    uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
+    uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits;
+    uint32_t gen;
+};
+
+// hashing shared by compiler and kernels
+__host__ __device__ inline uint32_t fnv1a_step(uint32_t h, uint32_t b) { return (h ^ b) * 16777619u; }
+__host__ __device__ inline uint32_t name_hash_fin(uint32_t h, uint32_t port_idx) {
+    h ^= port_idx * 0x9E3779B9u; h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13;
+    return h | 1u;           // never 0 (0 marks an empty slot)
+}
+__host__ __device__ inline uint32_t edge_hash(uint32_t key) {
+    uint32_t h = key * 0x9E3779B1u; return h ^ (h >> 15);
+}
+__host__ __device__ inline uint32_t waf_hash_a(uint32_t w) { return (w * 0x9E3779B1u) >> (32 - WAF_A_BITS); }
+__host__ __device__ inline uint32_t waf_hash_b(uint32_t w) {
+    uint32_t h = (w ^ (w >> 15)) * 0x85EBCA77u; return h >> (32 - WAF_B_BITS);
+}
+__host__ __device__ inline uint32_t lit_bucket_hash(uint32_t w) { uint32_t h = w * 0xC2B2AE3Du; return h ^ (h >> 16); }
+__host__ __device__ inline uint32_t fold4(uint32_t w) {
+    // ASCII A-Z -> a-z on four packed bytes (SWAR)
+    uint32_t x = w & 0x7F7F7F7Fu;
+    uint32_t ge_a = (x + 0x3F3F3F3Fu) & 0x80808080u;   // byte >= 'A'
+    uint32_t gt_z = (x + 0x25252525u) & 0x80808080u;   // byte >  'Z'
+    uint32_t up = ge_a & ~gt_z & ~w & 0x80808080u;     // high bit clear in the original byte
+    return w | (up >> 2);
+}
+
+}  // namespace gm

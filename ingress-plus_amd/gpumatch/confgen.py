@@ -1,0 +1,689 @@
+"""Rule-set shaping: Ingress / VirtualServer -> typed config -> nginx config text.
+
+This is the fixture side of SURVEY.md §8 row A12: a Python restatement of the
+reference Configurator's config *generation*, so that the engine can be fed
+exactly the nginx text the reference would hand to ``nginx.Manager.CreateConfig``.
+It is host tooling (used by tests, bench and the sample Manager), not part of the
+device path.
+
+Restated reference code (wallarm/ingress-plus 1.5.5-wallarm-r1):
+
+* ``internal/configs/config_params.go:107-141``  NewDefaultConfigParams
+* ``internal/configs/annotations.go:57-333``     parseAnnotations (verdict-affecting keys)
+* ``internal/configs/ingress.go:47-231``         generateNginxCfg
+* ``internal/configs/ingress.go:233-252``        createLocation
+* ``internal/configs/ingress.go:329-362``        pathOrDefault / getNameForUpstream / upstreamMapToSlice
+* ``internal/configs/ingress.go:364-432``        generateNginxCfgForMergeableIngresses
+* ``internal/configs/virtualserver.go:41-82``    upstream / variable namers
+* ``internal/configs/virtualserver.go:84-196``   generateVirtualServerConfig
+* ``internal/configs/virtualserver.go:250-442``  split / rules / map-value generation
+* ``internal/configs/virtualserver.go:444-472``  generateSSLConfig
+* ``internal/configs/configurator.go:172-190,556-571`` TLS pem names, conf.d file names
+* ``internal/k8s/controller.go:1827-1886``       getMinionsForMaster (path dedupe, first wins)
+* templates ``version1/nginx.ingress.tmpl``, ``version1/nginx.tmpl:81-129``,
+  ``version2/nginx.virtualserver.tmpl`` -- rendered here by ``render_*``; only the
+  directive *sequence* matters to the engine, whitespace is free.
+
+Typed configs are plain dicts whose keys follow the Go struct field names, so the
+Go unit tests' expected structs can be transcribed 1:1 into ``tests/golden``.
+"""
+
+from __future__ import annotations
+
+import copy
+
+PEM_MISSING = "/etc/nginx/secrets/default"      # configurator.go:19
+PEM_WILDCARD = "/etc/nginx/secrets/wildcard"    # configurator.go:20
+NGINX502_SERVER = "unix:/var/run/nginx-502-server.sock"  # virtualserver.go:14
+
+
+# --------------------------------------------------------------------------- params
+
+def default_config_params() -> dict:
+    """config_params.go:107-141 (verdict-relevant subset plus template fields)."""
+    return {
+        "ServerTokens": "on",
+        "ProxyConnectTimeout": "60s",
+        "ProxyReadTimeout": "60s",
+        "ClientMaxBodySize": "1m",
+        "SSLRedirect": True,
+        "RedirectToHTTPS": False,
+        "HTTP2": False,
+        "ProxyProtocol": False,
+        "ProxyBuffering": True,
+        "ProxyBuffers": "",
+        "ProxyBufferSize": "",
+        "ProxyMaxTempFileSize": "",
+        "Ports": [80],
+        "SSLPorts": [443],
+        "MaxFails": 1,
+        "FailTimeout": "10s",
+        "LBMethod": "random two least_conn",
+        "Keepalive": 0,
+        "HealthStatus": False,
+        "MainEnableWallarm": False,
+        "Wallarm": None,
+        "ServerSnippets": [],
+        "LocationSnippets": [],
+        "HSTS": False,
+    }
+
+
+def new_wallarm() -> dict:
+    """version1/config.go:208-222 NewWallarm."""
+    return {"Mode": "off", "ModeAllowOverride": "on", "Fallback": "on", "Instance": "",
+            "BlockPage": "", "ParseResponse": "on", "ParseWebsocket": "off",
+            "UnpackResponse": "on", "ParserDisable": []}
+
+
+def _as_bool(v):
+    s = str(v).strip().lower()
+    if s in ("true", "1", "t"):
+        return True
+    if s in ("false", "0", "f"):
+        return False
+    return None  # GetMapKeyAsBool error -> ignored (annotations.go logs and keeps default)
+
+
+def parse_annotations(ing: dict, base: dict) -> dict:
+    """annotations.go:57-333, restricted to keys that change the request verdict:
+    redirect-to-https (:176-182), ssl-redirect (:184-190), listen ports (:266-273),
+    wallarm.* (:294-330).  Timeouts/buffers/etc. only feed non-verdict directives."""
+    ann = (ing.get("metadata") or {}).get("annotations") or {}
+    p = copy.deepcopy(base)
+    if "nginx.org/redirect-to-https" in ann:
+        b = _as_bool(ann["nginx.org/redirect-to-https"])
+        if b is not None:
+            p["RedirectToHTTPS"] = b
+    if "ingress.kubernetes.io/ssl-redirect" in ann:
+        b = _as_bool(ann["ingress.kubernetes.io/ssl-redirect"])
+        if b is not None:
+            p["SSLRedirect"] = b
+    if "nginx.org/client-max-body-size" in ann:
+        p["ClientMaxBodySize"] = ann["nginx.org/client-max-body-size"]
+    for key, field in (("nginx.org/listen-ports", "Ports"), ("nginx.org/listen-ports-ssl", "SSLPorts")):
+        if key in ann:
+            ports = []
+            for v in str(ann[key]).split(","):
+                try:
+                    port = int(v)
+                except ValueError:
+                    continue
+                if 1 <= port <= 65535:
+                    ports.append(port)
+            if ports:
+                p[field] = ports
+    if p["MainEnableWallarm"]:
+        w = new_wallarm()
+        for k, f in (("wallarm.com/mode", "Mode"), ("wallarm.com/mode-allow-override", "ModeAllowOverride"),
+                     ("wallarm.com/fallback", "Fallback"), ("wallarm.com/instance", "Instance"),
+                     ("wallarm.com/block-page", "BlockPage"), ("wallarm.com/parse-response", "ParseResponse"),
+                     ("wallarm.com/parse-websocket", "ParseWebsocket"),
+                     ("wallarm.com/unpack-response", "UnpackResponse")):
+            if k in ann:
+                w[f] = ann[k]
+        if "wallarm.com/parser-disable" in ann:
+            w["ParserDisable"] = [s.strip() for s in str(ann["wallarm.com/parser-disable"]).split(",")]
+        p["Wallarm"] = w
+    return p
+
+
+# --------------------------------------------------------------------------- Ingress
+
+def _meta(obj):
+    m = obj.get("metadata") or {}
+    return m.get("namespace", "default"), m["name"]
+
+
+def object_meta_to_file_name(obj) -> str:
+    """configurator.go:560-562."""
+    ns, name = _meta(obj)
+    return f"{ns}-{name}"
+
+
+def _svc_port(backend) -> str:
+    return str(backend["servicePort"])
+
+
+def get_name_for_upstream(ing, host, backend) -> str:
+    """ingress.go:336-338."""
+    ns, name = _meta(ing)
+    return f"{ns}-{name}-{host}-{backend['serviceName']}-{_svc_port(backend)}"
+
+
+def path_or_default(path) -> str:
+    """ingress.go:329-334."""
+    return path if path else "/"
+
+
+def _create_upstream(ing_ex, name, backend, p):
+    """ingress.go:266-305 (OSS branch): default server 127.0.0.1:8181 when no endpoints
+    (version1/config.go:194-206)."""
+    ups = {"Name": name, "UpstreamServers": [{"Address": "127.0.0.1", "Port": "8181",
+                                              "MaxFails": 1, "FailTimeout": "10s"}],
+           "LBMethod": p["LBMethod"]}
+    key = backend["serviceName"] + _svc_port(backend)
+    endps = (ing_ex.get("Endpoints") or {}).get(key)
+    if endps:
+        ups["UpstreamServers"] = [{"Address": e.split(":")[0], "Port": e.split(":")[1],
+                                   "MaxFails": p["MaxFails"], "FailTimeout": p["FailTimeout"]} for e in endps]
+    return ups
+
+
+def _create_location(path, upstream, p):
+    """ingress.go:233-252."""
+    return {"Path": path, "Upstream": upstream, "ProxyConnectTimeout": p["ProxyConnectTimeout"],
+            "ProxyReadTimeout": p["ProxyReadTimeout"], "ClientMaxBodySize": p["ClientMaxBodySize"],
+            "Rewrite": "", "SSL": False, "GRPC": False, "Websocket": False,
+            "ProxyBuffering": p["ProxyBuffering"], "Wallarm": None, "MinionIngress": None}
+
+
+def generate_nginx_cfg(ing_ex: dict, pems: dict, is_minion: bool, base: dict) -> dict:
+    """ingress.go:47-231 generateNginxCfg (OSS, no JWT/health-check/grpc paths)."""
+    ing = ing_ex["Ingress"]
+    p = parse_annotations(ing, base)
+    spec = ing.get("spec") or {}
+    upstreams = {}
+    default_backend = spec.get("backend")
+    if default_backend is not None:
+        name = get_name_for_upstream(ing, "", default_backend)
+        upstreams[name] = _create_upstream(ing_ex, name, default_backend, p)
+    servers = []
+    for rule in spec.get("rules") or []:
+        if not rule.get("http"):
+            continue
+        host = rule.get("host", "")
+        server = {"Name": host, "ServerTokens": p["ServerTokens"], "HTTP2": p["HTTP2"],
+                  "RedirectToHTTPS": p["RedirectToHTTPS"], "SSLRedirect": p["SSLRedirect"],
+                  "ProxyProtocol": p["ProxyProtocol"], "HSTS": p["HSTS"], "StatusZone": host,
+                  "Ports": list(p["Ports"]), "SSLPorts": list(p["SSLPorts"]), "Wallarm": p["Wallarm"],
+                  "SSL": False, "SSLCertificate": "", "SSLCertificateKey": "", "SSLCiphers": "",
+                  "GRPCOnly": False, "ServerSnippets": list(p["ServerSnippets"])}
+        if host in pems:
+            pem = pems[host]
+            server.update(SSL=True, SSLCertificate=pem, SSLCertificateKey=pem)
+            if pem == PEM_MISSING:
+                server["SSLCiphers"] = "NULL"
+        locations = []
+        root = False
+        for path in rule["http"].get("paths") or []:
+            be = path["backend"]
+            ups_name = get_name_for_upstream(ing, host, be)
+            if ups_name not in upstreams:
+                upstreams[ups_name] = _create_upstream(ing_ex, ups_name, be, p)
+            loc = _create_location(path_or_default(path.get("path", "")), upstreams[ups_name], p)
+            locations.append(loc)
+            if loc["Path"] == "/":
+                root = True
+        if not root and default_backend is not None:
+            ups_name = get_name_for_upstream(ing, "", default_backend)
+            locations.append(_create_location("/", upstreams[ups_name], p))
+        server["Locations"] = locations
+        servers.append(server)
+    ns, name = _meta(ing)
+    return {"Upstreams": [upstreams[k] for k in sorted(upstreams)], "Servers": servers,
+            "Keepalive": str(p["Keepalive"]) if p["Keepalive"] > 0 else "",
+            "Ingress": {"Name": name, "Namespace": ns,
+                        "Annotations": (ing.get("metadata") or {}).get("annotations") or {}}}
+
+
+# annotations.go:17-55
+MASTER_DENY = ("nginx.org/rewrites", "nginx.org/ssl-services", "nginx.org/grpc-services",
+               "nginx.org/websocket-services", "nginx.com/sticky-cookie-services",
+               "nginx.com/health-checks", "nginx.com/health-checks-mandatory",
+               "nginx.com/health-checks-mandatory-queue")
+MINION_DENY = ("nginx.org/proxy-hide-headers", "nginx.org/proxy-pass-headers", "nginx.org/redirect-to-https",
+               "ingress.kubernetes.io/ssl-redirect", "nginx.org/hsts", "nginx.org/hsts-max-age",
+               "nginx.org/hsts-include-subdomains", "nginx.org/server-tokens", "nginx.org/listen-ports",
+               "nginx.org/listen-ports-ssl", "nginx.org/server-snippets")
+MINION_INHERIT = ("nginx.org/proxy-connect-timeout", "nginx.org/proxy-read-timeout",
+                  "nginx.org/client-max-body-size", "nginx.org/proxy-buffering", "nginx.org/proxy-buffers",
+                  "nginx.org/proxy-buffer-size", "nginx.org/proxy-max-temp-file-size",
+                  "nginx.org/location-snippets", "nginx.org/lb-method", "nginx.org/keepalive",
+                  "nginx.org/max-fails", "nginx.org/fail-timeout")
+
+
+def get_minions_for_master(master: dict, candidates: list) -> list:
+    """controller.go:1827-1886: minions with the master's host, oldest first; a path that an
+    earlier minion already claimed is dropped (first wins, :1860-1871)."""
+    host = master["spec"]["rules"][0]["host"]
+    mins = [m for m in candidates if (m.get("spec") or {}).get("rules")
+            and m["spec"]["rules"][0].get("host") == host]
+    mins.sort(key=lambda m: (m["metadata"].get("creationTimestamp", ""), _meta(m)))
+    seen = set()
+    out = []
+    for m in mins:
+        m = copy.deepcopy(m)
+        paths = []
+        for pth in m["spec"]["rules"][0]["http"]["paths"]:
+            if pth.get("path", "") in seen:
+                continue
+            seen.add(pth.get("path", ""))
+            paths.append(pth)
+        m["spec"]["rules"][0]["http"]["paths"] = paths
+        if paths:
+            out.append(m)
+    return out
+
+
+def generate_nginx_cfg_for_mergeable(master_ex: dict, minion_exs: list, master_pems: dict, base: dict) -> dict:
+    """ingress.go:364-432 generateNginxCfgForMergeableIngresses."""
+    master_ex = copy.deepcopy(master_ex)
+    # controller.go:1933-1936: the master gets an empty path list so createIngress accepts it
+    master_ex["Ingress"]["spec"]["rules"][0]["http"] = {"paths": []}
+    mann = master_ex["Ingress"]["metadata"].setdefault("annotations", {})
+    for k in MASTER_DENY:
+        mann.pop(k, None)
+    mcfg = generate_nginx_cfg(master_ex, master_pems, False, base)
+    server = mcfg["Servers"][0]
+    upstreams = list(mcfg["Upstreams"])
+    locations = []
+    for mx in minion_exs:
+        mx = copy.deepcopy(mx)
+        mx["Ingress"]["spec"].pop("backend", None)
+        ann = mx["Ingress"]["metadata"].setdefault("annotations", {})
+        for k in MINION_INHERIT:          # mergeMasterAnnotationsIntoMinion (annotations.go:439-465)
+            if k in mann and k not in ann:
+                ann[k] = mann[k]
+        for k in MINION_DENY:             # filterMinionAnnotations (annotations.go:431-437)
+            ann.pop(k, None)
+        cfg = generate_nginx_cfg(mx, {}, True, base)
+        for s in cfg["Servers"]:
+            for loc in s["Locations"]:
+                loc = dict(loc)
+                loc["MinionIngress"] = cfg["Ingress"]   # Location.Wallarm is never set (ingress.go)
+                locations.append(loc)
+        upstreams.extend(cfg["Upstreams"])
+    server["Locations"] = locations
+    return {"Servers": [server], "Upstreams": upstreams, "Keepalive": mcfg["Keepalive"],
+            "Ingress": mcfg["Ingress"]}
+
+
+def tls_pems(ing: dict, wildcard: bool = False, secrets=()) -> dict:
+    """configurator.go:172-190 updateTLSSecrets."""
+    pems = {}
+    ns, _ = _meta(ing)
+    for tls in (ing.get("spec") or {}).get("tls") or []:
+        sn = tls.get("secretName", "")
+        pem = PEM_MISSING
+        if sn == "" and wildcard:
+            pem = PEM_WILDCARD
+        elif sn in secrets:
+            pem = f"/etc/nginx/secrets/{ns}-{sn}"
+        for h in tls.get("hosts") or []:
+            pems[h] = pem
+    return pems
+
+
+# --------------------------------------------------------------------------- VirtualServer
+
+def _vs_upstream_prefix(vs):
+    ns, name = _meta(vs)
+    return f"vs_{ns}_{name}"
+
+
+def _vsr_upstream_prefix(vs, vsr):
+    ns, name = _meta(vs)
+    rns, rname = _meta(vsr)
+    return f"vs_{ns}_{name}_vsr_{rns}_{rname}"
+
+
+def _safe_ns_name(vs):
+    ns, name = _meta(vs)
+    return f"{ns}_{name}".replace("-", "_")
+
+
+SPECIAL_MAP_PARAMS = ("default", "hostnames", "include", "volatile")
+
+
+def generate_value_for_rules_route_map(v: str):
+    """virtualserver.go:387-402."""
+    if len(v) == 0:
+        return '""', False
+    neg = False
+    if v[0] == "!":
+        neg = True
+        v = v[1:]
+    if v in SPECIAL_MAP_PARAMS:
+        return "\\" + v, neg
+    return f'"{v}"', neg
+
+
+def generate_parameters_for_rules_route_map(v: str, ok: str):
+    """virtualserver.go:404-426."""
+    value, neg = generate_value_for_rules_route_map(v)
+    vr, dr = (ok, "0") if not neg else ("0", ok)
+    return [{"Value": value, "Result": vr}, {"Value": "default", "Result": dr}]
+
+
+def source_for_condition(c: dict) -> str:
+    """virtualserver.go:428-442."""
+    if c.get("header"):
+        return "$http_" + c["header"].replace("-", "_")
+    if c.get("cookie"):
+        return "$cookie_" + c["cookie"]
+    if c.get("argument"):
+        return "$arg_" + c["argument"]
+    return c.get("variable", "")
+
+
+def _vs_location(path, ups, p):
+    """virtualserver.go:231-245 generateLocation."""
+    return {"Path": path, "ProxyConnectTimeout": p["ProxyConnectTimeout"],
+            "ProxyReadTimeout": p["ProxyReadTimeout"], "ClientMaxBodySize": p["ClientMaxBodySize"],
+            "ProxyBuffering": p["ProxyBuffering"], "ProxyPass": f"http://{ups}"}
+
+
+def generate_split_route_config(route, prefix, safe, index, p):
+    """virtualserver.go:250-291."""
+    var = f"$vs_{safe}_splits_{index}"
+    dists = [{"Weight": f"{s['weight']}%", "Value": f"@splits_{index}_split_{i}"}
+             for i, s in enumerate(route["splits"])]
+    locs = [_vs_location(f"@splits_{index}_split_{i}", f"{prefix}_{s['upstream']}", p)
+            for i, s in enumerate(route["splits"])]
+    return {"SplitClient": {"Source": "$request_id", "Variable": var, "Distributions": dists},
+            "Locations": locs, "InternalRedirectLocation": {"Path": route["path"], "Destination": var}}
+
+
+def generate_rules_route_config(route, prefix, safe, index, p):
+    """virtualserver.go:299-378."""
+    rules = route["rules"]
+    conds = rules["conditions"]
+    maps = []
+    for i, m in enumerate(rules["matches"]):
+        for j, c in enumerate(conds):
+            ok = "1"
+            if j < len(m["values"]) - 1:
+                ok = f"$vs_{safe}_rules_{index}_match_{i}_cond_{j + 1}"
+            maps.append({"Source": source_for_condition(c),
+                         "Variable": f"$vs_{safe}_rules_{index}_match_{i}_cond_{j}",
+                         "Parameters": generate_parameters_for_rules_route_map(m["values"][j], ok)})
+    src = "".join(f"$vs_{safe}_rules_{index}_match_{i}_cond_0" for i in range(len(rules["matches"])))
+    params = [{"Value": "~^" + "0" * i + "1", "Result": f"@rules_{index}_match_{i}"}
+              for i in range(len(rules["matches"]))]
+    params.append({"Value": "default", "Result": f"@rules_{index}_default"})
+    var = f"$vs_{safe}_rules_{index}"
+    maps.append({"Source": src, "Variable": var, "Parameters": params})
+    locs = [_vs_location(f"@rules_{index}_match_{i}", f"{prefix}_{m['upstream']}", p)
+            for i, m in enumerate(rules["matches"])]
+    locs.append(_vs_location(f"@rules_{index}_default", f"{prefix}_{rules['defaultUpstream']}", p))
+    return {"Maps": maps, "Locations": locs,
+            "InternalRedirectLocation": {"Path": route["path"], "Destination": var}}
+
+
+def generate_ssl_config(tls, pem_name, p):
+    """virtualserver.go:444-472."""
+    if not tls or not tls.get("secret"):
+        return None
+    name, ciphers = (pem_name, "") if pem_name else (PEM_MISSING, "NULL")
+    return {"HTTP2": p["HTTP2"], "Certificate": name, "CertificateKey": name, "Ciphers": ciphers,
+            "RedirectToHTTPS": p["SSLRedirect"]}
+
+
+def generate_virtual_server_config(vs_ex: dict, pem_name: str, base: dict) -> dict:
+    """virtualserver.go:84-196 (OSS)."""
+    vs = vs_ex["VirtualServer"]
+    spec = vs["spec"]
+    p = base
+    prefix = _vs_upstream_prefix(vs)
+    safe = _safe_ns_name(vs)
+    ups = []
+
+    def mk_ups(name, ns, u):
+        key = f"{ns}/{u['service']}:{u['port']}"
+        eps = (vs_ex.get("Endpoints") or {}).get(key) or []
+        servers = [{"Address": e, "MaxFails": p["MaxFails"], "FailTimeout": p["FailTimeout"]} for e in eps]
+        if not servers:
+            servers = [{"Address": NGINX502_SERVER, "MaxFails": p["MaxFails"], "FailTimeout": p["FailTimeout"]}]
+        return {"Name": name, "Servers": servers, "LBMethod": p["LBMethod"]}
+
+    vns, _ = _meta(vs)
+    for u in spec.get("upstreams") or []:
+        ups.append(mk_ups(f"{prefix}_{u['name']}", vns, u))
+    vsrs = vs_ex.get("VirtualServerRoutes") or []
+    for vsr in vsrs:
+        rpre = _vsr_upstream_prefix(vs, vsr)
+        rns, _ = _meta(vsr)
+        for u in vsr["spec"].get("upstreams") or []:
+            ups.append(mk_ups(f"{rpre}_{u['name']}", rns, u))
+    locations, irls, splits, maps = [], [], [], []
+    rules_routes = 0
+
+    def add(r, pre):
+        nonlocal rules_routes
+        if r.get("splits"):
+            cfg = generate_split_route_config(r, pre, safe, len(splits), p)
+            splits.append(cfg["SplitClient"])
+            locations.extend(cfg["Locations"])
+            irls.append(cfg["InternalRedirectLocation"])
+        elif r.get("rules") is not None:
+            cfg = generate_rules_route_config(r, pre, safe, rules_routes, p)
+            maps.extend(cfg["Maps"])
+            locations.extend(cfg["Locations"])
+            irls.append(cfg["InternalRedirectLocation"])
+            rules_routes += 1
+        else:
+            locations.append(_vs_location(r["path"], f"{pre}_{r['upstream']}", p))
+
+    for r in spec.get("routes") or []:
+        if r.get("route"):
+            continue
+        add(r, prefix)
+    for vsr in vsrs:
+        rpre = _vsr_upstream_prefix(vs, vsr)
+        for r in vsr["spec"].get("subroutes") or []:
+            add(r, rpre)
+    return {"Upstreams": ups, "SplitClients": splits, "Maps": maps,
+            "Server": {"ServerName": spec["host"], "ProxyProtocol": p["ProxyProtocol"],
+                       "SSL": generate_ssl_config(spec.get("tls"), pem_name, p),
+                       "RedirectToHTTPSBasedOnXForwarderProto": p["RedirectToHTTPS"],
+                       "ServerTokens": p["ServerTokens"], "Snippets": list(p["ServerSnippets"]),
+                       "InternalRedirectLocations": irls, "Locations": locations},
+            "Keepalive": str(p["Keepalive"]) if p["Keepalive"] > 0 else ""}
+
+
+def vs_file_name(vs) -> str:
+    """configurator.go:564-566."""
+    ns, name = _meta(vs)
+    return f"vs_{ns}_{name}"
+
+
+# --------------------------------------------------------------------------- rendering
+
+def _wallarm_lines(w, ind):
+    if not w:
+        return []
+    out = [f"{ind}wallarm_mode {w['Mode']};", f"{ind}wallarm_mode_allow_override {w['ModeAllowOverride']};",
+           f"{ind}wallarm_fallback {w['Fallback']};"]
+    if w.get("Instance"):
+        out.append(f"{ind}wallarm_instance {w['Instance']};")
+    if w.get("BlockPage"):
+        out.append(f'{ind}wallarm_block_page "{w["BlockPage"]}";')
+    out += [f"{ind}wallarm_parse_response {w['ParseResponse']};",
+            f"{ind}wallarm_parse_websocket {w['ParseWebsocket']};",
+            f"{ind}wallarm_unpack_response {w['UnpackResponse']};"]
+    out += [f"{ind}wallarm_parser_disable {x};" for x in w.get("ParserDisable") or []]
+    return out
+
+
+def render_ingress(cfg: dict) -> str:
+    """Directive sequence of version1/nginx.ingress.tmpl (OSS, non-gRPC)."""
+    ing = cfg["Ingress"]
+    L = [f"# configuration for {ing['Namespace']}/{ing['Name']}"]
+    for u in cfg["Upstreams"]:
+        L.append(f"upstream {u['Name']} {{")
+        if u.get("LBMethod"):
+            L.append(f"\t{u['LBMethod']};")
+        for s in u["UpstreamServers"]:
+            L.append(f"\tserver {s['Address']}:{s['Port']} max_fails={s['MaxFails']} fail_timeout={s['FailTimeout']};")
+        if cfg.get("Keepalive"):
+            L.append(f"\tkeepalive {cfg['Keepalive']};")
+        L.append("}")
+    for s in cfg["Servers"]:
+        L.append("server {")
+        L += _wallarm_lines(s.get("Wallarm"), "\t")
+        for port in s["Ports"]:
+            L.append(f"\tlisten {port}{' proxy_protocol' if s['ProxyProtocol'] else ''};")
+        if s["SSL"]:
+            for port in s["SSLPorts"]:
+                L.append(f"\tlisten {port} ssl{' http2' if s['HTTP2'] else ''}"
+                         f"{' proxy_protocol' if s['ProxyProtocol'] else ''};")
+            L.append(f"\tssl_certificate {s['SSLCertificate']};")
+            L.append(f"\tssl_certificate_key {s['SSLCertificateKey']};")
+            if s.get("SSLCiphers"):
+                L.append(f"\tssl_ciphers {s['SSLCiphers']};")
+        L.append(f"\tserver_tokens {s['ServerTokens']};")
+        L.append(f"\tserver_name {s['Name']};")
+        if s["SSL"] and s["SSLRedirect"]:
+            L += ["\tif ($scheme = http) {", f"\t\treturn 301 https://$host:{s['SSLPorts'][0]}$request_uri;", "\t}"]
+        if s["RedirectToHTTPS"]:
+            L += ["\tif ($http_x_forwarded_proto = 'http') {", "\t\treturn 301 https://$host$request_uri;", "\t}"]
+        for v in s.get("ServerSnippets") or []:
+            L.append("\t" + v)
+        for loc in s["Locations"]:
+            L.append(f"\tlocation {loc['Path']} {{")
+            L += _wallarm_lines(loc.get("Wallarm"), "\t\t")
+            mi = loc.get("MinionIngress")
+            if mi:
+                L.append(f"\t\t# location for minion {mi['Namespace']}/{mi['Name']}")
+            L.append("\t\tproxy_http_version 1.1;")
+            if cfg.get("Keepalive"):
+                L.append('\t\tproxy_set_header Connection "";')
+            L.append(f"\t\tproxy_connect_timeout {loc['ProxyConnectTimeout']};")
+            L.append(f"\t\tproxy_read_timeout {loc['ProxyReadTimeout']};")
+            L.append(f"\t\tclient_max_body_size {loc['ClientMaxBodySize']};")
+            L.append("\t\tproxy_set_header Host $host;")
+            L.append("\t\tproxy_set_header X-Real-IP $remote_addr;")
+            L.append("\t\tproxy_set_header X-Forwarded-For $proxy_add_x_forwarded_for;")
+            L.append("\t\tproxy_set_header X-Forwarded-Host $host;")
+            L.append("\t\tproxy_set_header X-Forwarded-Port $server_port;")
+            L.append(f"\t\tproxy_set_header X-Forwarded-Proto {'https' if s['RedirectToHTTPS'] else '$scheme'};")
+            L.append(f"\t\tproxy_buffering {'on' if loc['ProxyBuffering'] else 'off'};")
+            scheme = "https" if loc["SSL"] else "http"
+            L.append(f"\t\tproxy_pass {scheme}://{loc['Upstream']['Name']}{loc['Rewrite']};")
+            L.append("\t}")
+        L.append("}")
+    return "\n".join(L) + "\n"
+
+
+def render_virtual_server(cfg: dict) -> str:
+    """Directive sequence of version2/nginx.virtualserver.tmpl (OSS)."""
+    L = []
+    for u in cfg["Upstreams"]:
+        L.append(f"upstream {u['Name']} {{")
+        L.append(f"    zone {u['Name']} 256k;")
+        if u.get("LBMethod"):
+            L.append(f"    {u['LBMethod']};")
+        for s in u["Servers"]:
+            L.append(f"    server {s['Address']} max_fails={s['MaxFails']} fail_timeout={s['FailTimeout']};")
+        if cfg.get("Keepalive"):
+            L.append(f"    keepalive {cfg['Keepalive']};")
+        L.append("}")
+    for sc in cfg["SplitClients"]:
+        L.append(f"split_clients {sc['Source']} {sc['Variable']} {{")
+        for d in sc["Distributions"]:
+            L.append(f"    {d['Weight']} {d['Value']};")
+        L.append("}")
+    for m in cfg["Maps"]:
+        L.append(f"map {m['Source']} {m['Variable']} {{")
+        for prm in m["Parameters"]:
+            L.append(f"    {prm['Value']} {prm['Result']};")
+        L.append("}")
+    s = cfg["Server"]
+    L.append("server {")
+    L.append(f"    listen 80{' proxy_protocol' if s['ProxyProtocol'] else ''};")
+    L.append(f"    server_name {s['ServerName']};")
+    ssl = s.get("SSL")
+    if ssl:
+        L.append(f"    listen 443 ssl{' http2' if ssl['HTTP2'] else ''}{' proxy_protocol' if s['ProxyProtocol'] else ''};")
+        L.append(f"    ssl_certificate {ssl['Certificate']};")
+        L.append(f"    ssl_certificate_key {ssl['CertificateKey']};")
+        if ssl.get("Ciphers"):
+            L.append(f"    ssl_ciphers {ssl['Ciphers']};")
+        if ssl["RedirectToHTTPS"]:
+            L += ["    if ($scheme = http) {", "        return 301 https://$host$request_uri;", "    }"]
+    if s["RedirectToHTTPSBasedOnXForwarderProto"]:
+        L += ["    if ($http_x_forwarded_proto = 'http') {", "        return 301 https://$host$request_uri;", "    }"]
+    L.append(f'    server_tokens "{s["ServerTokens"]}";')
+    for v in s.get("Snippets") or []:
+        L.append("    " + v)
+    for irl in s["InternalRedirectLocations"]:
+        L += [f"    location {irl['Path']} {{", f"        error_page 418 = {irl['Destination']};",
+              "        return 418;", "    }"]
+    for loc in s["Locations"]:
+        L.append(f"    location {loc['Path']} {{")
+        L.append(f"        proxy_connect_timeout {loc['ProxyConnectTimeout']};")
+        L.append(f"        proxy_read_timeout {loc['ProxyReadTimeout']};")
+        L.append(f"        client_max_body_size {loc['ClientMaxBodySize']};")
+        L.append(f"        proxy_buffering {'on' if loc['ProxyBuffering'] else 'off'};")
+        L.append("        proxy_http_version 1.1;")
+        if cfg.get("Keepalive"):
+            L.append('        proxy_set_header Connection "";')
+        L.append("        proxy_set_header Host $host;")
+        L.append("        proxy_set_header X-Forwarded-Proto $scheme;")
+        L.append(f"        proxy_pass {loc['ProxyPass']};")
+        L.append("    }")
+    L.append("}")
+    return "\n".join(L) + "\n"
+
+
+def render_main(params: dict | None = None, wallarm_global_mode: str | None = None) -> str:
+    """The http{} part of version1/nginx.tmpl that affects request classification:
+    the default server (:81-102) and the conf.d include point (:128-129)."""
+    p = params or default_config_params()
+    L = []
+    if p.get("MainEnableWallarm"):
+        L.append("load_module /etc/nginx/modules/ngx_http_wallarm_module.so;")
+    L += ["events {", "    worker_connections 1024;", "}", "http {"]
+    if wallarm_global_mode:
+        L.append(f"    wallarm_mode {wallarm_global_mode};")
+    L += ["    map $http_upgrade $connection_upgrade {", "        default upgrade;", "        ''      close;", "    }",
+          "    server {", "        listen 80 default_server;",
+          f"        listen 443 ssl default_server{' http2' if p.get('HTTP2') else ''};",
+          "        ssl_certificate /etc/nginx/secrets/default;", "        ssl_certificate_key /etc/nginx/secrets/default;",
+          "        server_name _;", f'        server_tokens "{p.get("ServerTokens", "on")}";', "        access_log off;"]
+    if p.get("HealthStatus"):
+        L += ["        location /nginx-health {", "            default_type text/plain;",
+              '            return 200 "healthy\\n";', "        }"]
+    L += ["        location / {", "           return 404;", "        }", "    }",
+          "    include /etc/nginx/config-version.conf;", "    include /etc/nginx/conf.d/*.conf;",
+          "    server {", "        listen unix:/var/run/nginx-502-server.sock;", "        access_log off;",
+          "        location / {", "            return 502;", "        }", "    }", "}"]
+    return "\n".join(L) + "\n"
+
+
+# --------------------------------------------------------------------------- convenience
+
+def ingress_files(ingresses, base=None, wildcard=False, secrets=()):
+    """Configurator.AddOrUpdateIngress for a list of plain Ingress objects -> {file stem: text}."""
+    base = base or default_config_params()
+    out = {}
+    for ing in ingresses:
+        ex = {"Ingress": ing, "Endpoints": {}}
+        cfg = generate_nginx_cfg(ex, tls_pems(ing, wildcard, secrets), False, base)
+        out[object_meta_to_file_name(ing)] = render_ingress(cfg)
+    return out
+
+
+def mergeable_files(masters, minions, base=None, wildcard=False, secrets=()):
+    """Configurator.AddOrUpdateMergeableIngress for masters + the minion pool."""
+    base = base or default_config_params()
+    out = {}
+    for m in masters:
+        mins = get_minions_for_master(m, minions)
+        cfg = generate_nginx_cfg_for_mergeable({"Ingress": m, "Endpoints": {}},
+                                               [{"Ingress": x, "Endpoints": {}} for x in mins],
+                                               tls_pems(m, wildcard, secrets), base)
+        out[object_meta_to_file_name(m)] = render_ingress(cfg)
+    return out
+
+
+def virtual_server_files(vss, base=None, vsrs_by_vs=None, pem_name="/etc/nginx/secrets/default-cafe-secret"):
+    base = base or default_config_params()
+    out = {}
+    for vs in vss:
+        key = "%s/%s" % _meta(vs)
+        ex = {"VirtualServer": vs, "Endpoints": {}, "VirtualServerRoutes": (vsrs_by_vs or {}).get(key, [])}
+        cfg = generate_virtual_server_config(ex, pem_name, base)
+        out[vs_file_name(vs)] = render_virtual_server(cfg)
+    return out

@@ -1,0 +1,171 @@
+"""ctypes binding of libgpumatch.so (the C-ABI declared in include/gpumatch.h).
+
+No fallback: if the HIP library is missing this module raises at import, and every compute
+call goes through the gfx950 kernels.  torch is used only as the device-memory / stream
+allocator in ``match_torch`` (plumbing, not the product).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .records import REQ_DTYPE, VERDICT_DTYPE
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(HERE), "libgpumatch.so")
+
+GM_OK = 0
+GM_E_OVERFLOW = -4
+GM_CREATE_COMPILE_ONLY = 0x1
+GM_BATCH_HOST = 0x1
+
+ACT = {0: "PROXY", 1: "REDIRECT", 2: "RETURN", 3: "AUTO_301", 4: "NOT_FOUND", 5: "BAD_REQUEST", 6: "BLOCK",
+       7: "ERRPAGE", 8: "UNSUPPORTED", 9: "NO_LISTENER"}
+
+STATS_FIELDS = ["gen", "n_servers", "n_locations", "n_upstreams", "n_routes_rules", "n_routes_split", "n_sigs",
+                "n_sig_literals", "n_sig_regex", "n_sig_regex_always", "n_rejected_pcre", "n_rejected_other",
+                "n_dfa_states", "n_counters"]
+STATS_FIELDS64 = ["table_bytes", "lds_bytes_scan", "last_candidates", "last_pairs", "last_hits"]
+
+
+STATS_FIELDS_MS = ["last_ms_route", "last_ms_scan", "last_ms_verify", "last_ms_tail"]
+GM_CREATE_PROFILE = 0x2
+
+
+class GmStats(ctypes.Structure):
+    _fields_ = ([(f, ctypes.c_uint32) for f in STATS_FIELDS] + [(f, ctypes.c_uint64) for f in STATS_FIELDS64] +
+                [(f, ctypes.c_float) for f in STATS_FIELDS_MS])
+
+
+class GmBatch(ctypes.Structure):
+    _fields_ = [("reqs", ctypes.c_void_p), ("arena", ctypes.c_void_p), ("arena_len", ctypes.c_uint64),
+                ("n", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+EXPORTS = ["gm_create", "gm_destroy", "gm_abi_version", "gm_load_generation", "gm_match_batch", "gm_sync",
+           "gm_counters", "gm_counters_reset", "gm_comm_unique_id", "gm_comm_init", "gm_counters_allreduce",
+           "gm_stats", "gm_last_error"]
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libgpumatch.so not built ({LIB_PATH}); run __graft_entry__.build()")
+        L = ctypes.CDLL(LIB_PATH)
+        L.gm_create.restype = ctypes.c_void_p
+        L.gm_create.argtypes = [ctypes.c_int, ctypes.c_uint32]
+        L.gm_destroy.argtypes = [ctypes.c_void_p]
+        L.gm_abi_version.restype = ctypes.c_uint32
+        L.gm_load_generation.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
+        L.gm_match_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(GmBatch), ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_size_t, ctypes.c_void_p]
+        L.gm_sync.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.gm_counters.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        L.gm_counters_reset.argtypes = [ctypes.c_void_p]
+        L.gm_comm_unique_id.argtypes = [ctypes.c_void_p]
+        L.gm_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.gm_counters_allreduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.gm_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(GmStats)]
+        L.gm_last_error.restype = ctypes.c_char_p
+        L.gm_last_error.argtypes = [ctypes.c_void_p]
+        _lib = L
+    return _lib
+
+
+class GmError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"gpumatch error {code}: {msg}")
+        self.code = code
+
+
+class Engine:
+    """One context per HIP device (one process per GPU)."""
+
+    def __init__(self, device: int = 0, compile_only: bool = False, profile: bool = False):
+        L = lib()
+        fl = (GM_CREATE_COMPILE_ONLY if compile_only else 0) | (GM_CREATE_PROFILE if profile else 0)
+        self.h = L.gm_create(device, fl)
+        if not self.h:
+            raise GmError(-1, L.gm_last_error(None).decode())
+        self.device = device
+        self.compile_only = compile_only
+
+    def close(self):
+        if self.h:
+            lib().gm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc):
+        if rc != GM_OK:
+            raise GmError(rc, lib().gm_last_error(self.h).decode())
+
+    def load(self, blob: bytes, gen: int = 1):
+        self._chk(lib().gm_load_generation(self.h, blob, len(blob), gen))
+
+    def stats(self) -> dict:
+        s = GmStats()
+        self._chk(lib().gm_stats(self.h, ctypes.byref(s)))
+        return {f: getattr(s, f) for f in STATS_FIELDS + STATS_FIELDS64 + STATS_FIELDS_MS}
+
+    def match_ptr(self, reqs_ptr, arena_ptr, arena_len, n, out_ptr, hits_ptr, hit_cap, stream=0, host=False):
+        b = GmBatch(reqs_ptr, arena_ptr, arena_len, n, GM_BATCH_HOST if host else 0)
+        self._chk(lib().gm_match_batch(self.h, ctypes.byref(b), out_ptr, hits_ptr, hit_cap, stream))
+
+    def sync(self, stream=0):
+        self._chk(lib().gm_sync(self.h, stream))
+
+    def match_host(self, reqs: np.ndarray, arena: np.ndarray, hit_cap: int | None = None):
+        """Host numpy in, host numpy out (staged through HBM by the library)."""
+        n = len(reqs)
+        reqs = np.ascontiguousarray(reqs, dtype=REQ_DTYPE)
+        arena = np.ascontiguousarray(arena) if len(arena) else np.zeros(16, np.uint8)
+        out = np.zeros(n, dtype=VERDICT_DTYPE)
+        cap = hit_cap if hit_cap is not None else max(1024, 4 * n)
+        hits = np.zeros(cap, dtype=np.uint32)
+        self.match_ptr(reqs.ctypes.data, arena.ctypes.data, len(arena), n, out.ctypes.data, hits.ctypes.data,
+                       cap, 0, host=True)
+        self.sync(0)
+        total = self.stats()["last_hits"]
+        return out, hits[:total]
+
+    def match_torch(self, reqs_t, arena_t, arena_len: int, out_t, hits_t, stream=None):
+        """Device tensors (torch.uint8 / structured views) -> verdicts in out_t (async)."""
+        import torch
+        s = stream if stream is not None else torch.cuda.current_stream()
+        self.match_ptr(reqs_t.data_ptr(), arena_t.data_ptr(), arena_len, reqs_t.numel() // 64, out_t.data_ptr(),
+                       hits_t.data_ptr(), hits_t.numel(), s.cuda_stream)
+
+    def counters(self) -> np.ndarray:
+        n = self.stats()["n_counters"]
+        out = np.zeros(max(n, 1), dtype=np.uint64)
+        self._chk(lib().gm_counters(self.h, out.ctypes.data, n))
+        return out[:n]
+
+    def counters_reset(self):
+        self._chk(lib().gm_counters_reset(self.h))
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        rc = lib().gm_comm_unique_id(buf)
+        if rc != GM_OK:
+            raise GmError(rc, lib().gm_last_error(None).decode())
+        return buf.raw
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        self._chk(lib().gm_comm_init(self.h, uid, nranks, rank))
+
+    def counters_allreduce(self, stream=0):
+        self._chk(lib().gm_counters_allreduce(self.h, stream))

@@ -1,0 +1,1103 @@
+/*
+ * gm_oracle.c -- CPU ORACLE for the gpumatch engine.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library,
+ * and only as the checker / the timed CPU baseline.  The product path (libgpumatch.so) never
+ * links, loads or calls it.
+ *
+ * What it restates.  The reference (wallarm/ingress-plus 1.5.5) renders nginx config text
+ * (the internal/configs version1 and version2 templates) and nginx 1.17.3 (build/Dockerfile:1)
+ * classifies each request.  nginx's C source is not in /root/reference (third-party, pinned by
+ * build/Dockerfile:1), so the request-time algorithm restated here is nginx 1.17.3's, written
+ * from its published behaviour and anchored on the reference's call sites:
+ *   - config tokens: ngx_conf_read_token (quotes, \" \' \\ \t \r \n escapes, ')' after quote)
+ *   - host validation:   ngx_http_validate_host            
+ *   - server by name:    ngx_http_find_virtual_server; exact > *.x > x.* > ~regex, first wins
+ *                        (server_name at nginx.ingress.tmpl:53, nginx.virtualserver.tmpl:37,
+ *                         default server nginx.tmpl:81-102, conf.d order nginx.tmpl:128-129)
+ *   - server rewrite:    `if ($scheme = http) { return 301 ...; }` / x-forwarded-proto
+ *                        (nginx.ingress.tmpl:76-88, nginx.virtualserver.tmpl:49-60)
+ *   - location lookup:   ngx_http_core_find_location: '=' exact, longest prefix, '^~',
+ *                        regex in config order, auto_redirect
+ *   - error_page 418 = $var + return 418 (nginx.virtualserver.tmpl:78-83) and named locations
+ *   - map:               ngx_http_map_find: lowercased hash keys, then regexes (only for a
+ *                        non-empty value), else default   (virtualserver.go:299-426)
+ *   - split_clients:     ngx_murmur_hash2 over $request_id, percent*0xffffffff/10000 bounds
+ *                        (virtualserver.go:250-291, nginx.virtualserver.tmpl:17-23)
+ *   - variables:         $http_* (ngx_http_variable_unknown_header, cookie / x-forwarded-for
+ *                        joins), $cookie_* (ngx_http_parse_multi_header_lines), $arg_*
+ *                        (ngx_http_arg), the 11 whitelisted variables (validation.go:353-365)
+ *   - regex:             the real PCRE 8.39 (libpcre.so.3, the library nginx:1.17.3 links)
+ *   - WAF layer:         build-defined signature set (ingress-plus_amd/gpumatch/sigs.py):
+ *                        Aho-Corasick for literals, PCRE for regexes, per zone; mode from
+ *                        wallarm_mode (annotations.go:294-330, nginx.ingress.tmpl:12-29).
+ * Pinning: tests/golden holds the reference's own known answers (e2e KATs of
+ * tests/suite/test_virtual_server_advanced_routing.py, docs/virtualserver-and-
+ * virtualserverroute.md:264-271, virtualserver_test.go map structs) and PCRE-generated
+ * vectors; see DESIGN.md §Oracle for what remains unpinned.
+ */
+#define _GNU_SOURCE
+#include <ctype.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/gpumatch.h"
+
+/* ---- PCRE 8.39 (no headers in the image: declare the stable C API) ---- */
+typedef struct real_pcre pcre;
+typedef struct pcre_extra pcre_extra;
+extern pcre *pcre_compile(const char *, int, const char **, int *, const unsigned char *);
+extern pcre_extra *pcre_study(const pcre *, int, const char **);
+extern int pcre_exec(const pcre *, const pcre_extra *, const char *, int, int, int, int *, int);
+#define PCRE_CASELESS 0x00000001
+#define PCRE_STUDY_JIT_COMPILE 0x0001
+
+
+/* ------------------------------------------------------------------ small utils */
+typedef struct { const char *p; int n; } sv;
+
+static __thread char g_err[512];
+const char *orc_error(void) { return g_err; }
+static void seterr(const char *m, const char *a) { snprintf(g_err, sizeof g_err, "%s%s", m, a ? a : ""); }
+
+static int sv_eq(sv a, const char *b) { int n = (int)strlen(b); return a.n == n && memcmp(a.p, b, n) == 0; }
+static int sv_eqsv(sv a, sv b) { return a.n == b.n && memcmp(a.p, b.p, a.n) == 0; }
+static char *xstrndup(const char *p, int n) { char *s = malloc(n + 1); memcpy(s, p, n); s[n] = 0; return s; }
+static unsigned char lc(unsigned char c) { return (c >= 'A' && c <= 'Z') ? (unsigned char)(c | 0x20) : c; }
+
+/* ------------------------------------------------------------------ config tokens (ngx_conf_read_token) */
+typedef struct dir {
+    int nargs; char **args; int *alen;
+    struct dir *kids; int nkids, capkids; int block;
+} dir_t;
+
+typedef struct { const char *s; int n; int i; char *buf; } lexer;
+
+static void dir_push_arg(dir_t *d, const char *p, int n) {
+    d->args = realloc(d->args, sizeof(char *) * (d->nargs + 1));
+    d->alen = realloc(d->alen, sizeof(int) * (d->nargs + 1));
+    d->args[d->nargs] = xstrndup(p, n); d->alen[d->nargs] = n; d->nargs++;
+}
+
+/* copy token with nginx escape rules */
+static int unescape(const char *src, int n, char *dst) {
+    int o = 0;
+    for (int i = 0; i < n; i++) {
+        if (src[i] == '\\' && i + 1 < n) {
+            char c = src[i + 1];
+            if (c == '"' || c == '\'' || c == '\\') { dst[o++] = c; i++; continue; }
+            if (c == 't') { dst[o++] = '\t'; i++; continue; }
+            if (c == 'r') { dst[o++] = '\r'; i++; continue; }
+            if (c == 'n') { dst[o++] = '\n'; i++; continue; }
+        }
+        dst[o++] = src[i];
+    }
+    return o;
+}
+
+/* returns 0 = ';' ended, 1 = '{' block start, 2 = '}' block end, 3 = EOF, -1 error */
+static int read_directive(lexer *L, dir_t *d) {
+    char *buf = L->buf;
+    for (;;) {
+        while (L->i < L->n && strchr(" \t\r\n", L->s[L->i])) L->i++;
+        if (L->i >= L->n) { return d->nargs ? -1 : 3; }
+        char c = L->s[L->i];
+        if (c == '#') { while (L->i < L->n && L->s[L->i] != '\n') L->i++; continue; }
+        if (c == ';') { L->i++; return d->nargs ? 0 : -1; }
+        if (c == '{') { L->i++; return 1; }
+        if (c == '}') { L->i++; if (d->nargs) return -1; return 2; }
+        if (c == '"' || c == '\'') {
+            char q = c; int st = ++L->i;
+            while (L->i < L->n && L->s[L->i] != q) { if (L->s[L->i] == '\\') L->i++; L->i++; }
+            if (L->i >= L->n) { return -1; }
+            int m = unescape(L->s + st, L->i - st, buf); L->i++;
+            dir_push_arg(d, buf, m);
+            if (L->i < L->n && L->s[L->i] == ')') { dir_push_arg(d, ")", 1); L->i++; }
+            else if (L->i < L->n && !strchr(" \t\r\n;{", L->s[L->i])) { return -1; }
+            continue;
+        }
+        int st = L->i; int var = 0;
+        while (L->i < L->n) {
+            char ch = L->s[L->i];
+            if (ch == '{' && var) { L->i++; continue; }
+            var = 0;
+            if (ch == '\\') { L->i += 2; continue; }
+            if (ch == '$') { var = 1; L->i++; continue; }
+            if (strchr(" \t\r\n;{", ch)) break;
+            L->i++;
+        }
+        if (L->i > L->n) L->i = L->n;
+        int m = unescape(L->s + st, L->i - st, buf);
+        dir_push_arg(d, buf, m);
+    }
+}
+
+static int parse_block(lexer *L, dir_t *parent, int depth) {
+    for (;;) {
+        dir_t d; memset(&d, 0, sizeof d);
+        int r = read_directive(L, &d);
+        if (r == 3) return depth == 0 ? 0 : -1;
+        if (r == 2) return depth > 0 ? 0 : -1;
+        if (r < 0) return -1;
+        if (r == 1) { d.block = 1; if (parse_block(L, &d, depth + 1) < 0) return -1; }
+        if (parent->nkids == parent->capkids) {
+            parent->capkids = parent->capkids ? parent->capkids * 2 : 16;
+            parent->kids = realloc(parent->kids, sizeof(dir_t) * parent->capkids);
+        }
+        parent->kids[parent->nkids++] = d;
+    }
+}
+
+/* ------------------------------------------------------------------ model */
+enum { LK_PREFIX, LK_EXACT, LK_NOREGEX, LK_REGEX, LK_REGEX_I, LK_NAMED };
+
+typedef struct {
+    int kind; char *path; int plen; pcre *re;
+    int id, server;
+    int auto_redirect;
+    char *proxy_ups; int upstream_id; int has_proxy;
+    int has_return; int ret_code;
+    char *err418;             /* error_page 418 = <complex value> */
+    int waf_mode;
+} loc_t;
+
+typedef struct { char *var; int op; char *val; pcre *re; int code; char *text; int is_return_only; } sif_t;
+
+typedef struct {
+    int id; int nports; int ports[16]; int ssl[16]; int def[16];
+    int nnames; char **names; int *nlen; pcre **nre;
+    int nifs; sif_t *ifs;
+    int nlocs; int *locs;
+    int waf_mode;
+} srv_t;
+
+typedef struct { char *key; int klen; pcre *re; int is_re; char *val; } mparam_t;
+typedef struct { char *src; char *var; int np; mparam_t *p; char *defval; int hostnames; } map_t;
+typedef struct { uint32_t bound; int star; char *val; } part_t;
+typedef struct { char *src; char *var; int np; part_t *p; } split_t;
+
+typedef struct { int kind; int nocase; int zones; uint8_t *lit; int len; pcre *re; pcre_extra *ex; } sig_t;
+
+typedef struct orc_ctx {
+    uint32_t gen;
+    srv_t *srv; int nsrv;
+    loc_t *loc; int nloc;
+    map_t *map; int nmap;
+    split_t *spl; int nspl;
+    char **ups; int nups;
+    int http_waf;
+    sig_t *sig; int nsig;
+    /* Aho-Corasick over case-folded bytes */
+    int32_t *ac_next; int ac_states; int32_t *ac_out; int32_t *ac_dict; int32_t *ac_pat_next; int *ac_pat;
+} orc_ctx;
+
+static int waf_mode_of(const char *s) {
+    if (!strcmp(s, "off")) return GM_WAF_OFF;
+    if (!strcmp(s, "monitoring")) return GM_WAF_MONITORING;
+    if (!strcmp(s, "safe_blocking")) return GM_WAF_SAFE_BLOCKING;
+    if (!strcmp(s, "block")) return GM_WAF_BLOCK;
+    return GM_WAF_OFF;
+}
+
+static pcre *re_compile(const char *pat, int caseless) {
+    const char *e; int eo;
+    pcre *r = pcre_compile(pat, caseless ? PCRE_CASELESS : 0, &e, &eo, NULL);
+    return r;
+}
+
+static int cmp_str(const void *a, const void *b) { return strcmp(*(char *const *)a, *(char *const *)b); }
+
+/* ------------------------------------------------------------------ build from directives */
+typedef struct { orc_ctx *c; dir_t **confd; int nconfd; } build_t;
+
+static void add_server(build_t *B, dir_t *s, int http_waf);
+
+static void walk_http(build_t *B, dir_t *h) {
+    orc_ctx *c = B->c;
+    for (int i = 0; i < h->nkids; i++) {
+        dir_t *d = &h->kids[i];
+        if (!d->nargs) continue;
+        const char *n = d->args[0];
+        if (!strcmp(n, "include") && d->nargs == 2 && strstr(d->args[1], "conf.d/")) {
+            for (int k = 0; k < B->nconfd; k++) walk_http(B, B->confd[k]);
+        } else if (!strcmp(n, "wallarm_mode") && d->nargs == 2) {
+            c->http_waf = waf_mode_of(d->args[1]);
+        } else if (!strcmp(n, "upstream") && d->nargs == 2 && d->block) {
+            c->ups = realloc(c->ups, sizeof(char *) * (c->nups + 1));
+            c->ups[c->nups++] = strdup(d->args[1]);
+        } else if (!strcmp(n, "map") && d->nargs == 3 && d->block) {
+            map_t m; memset(&m, 0, sizeof m);
+            m.src = strdup(d->args[1]); m.var = strdup(d->args[2] + 1);
+            for (int k = 0; k < d->nkids; k++) {
+                dir_t *p = &d->kids[k];
+                if (p->nargs == 1 && !strcmp(p->args[0], "hostnames")) { m.hostnames = 1; continue; }
+                if (p->nargs == 1 && !strcmp(p->args[0], "volatile")) continue;
+                if (p->nargs != 2) continue;
+                if (!strcmp(p->args[0], "default")) { m.defval = strdup(p->args[1]); continue; }
+                if (!strcmp(p->args[0], "include")) continue;
+                mparam_t mp; memset(&mp, 0, sizeof mp);
+                mp.val = strdup(p->args[1]);
+                const char *k0 = p->args[0]; int kl = p->alen[0];
+                if (kl && k0[0] == '~') {
+                    int ci = (kl > 1 && k0[1] == '*');
+                    mp.is_re = 1; mp.re = re_compile(k0 + 1 + ci, ci);
+                } else {
+                    if (kl && k0[0] == '\\') { k0++; kl--; }
+                    mp.key = xstrndup(k0, kl); mp.klen = kl;
+                    for (int q = 0; q < kl; q++) mp.key[q] = (char)lc((unsigned char)mp.key[q]);
+                }
+                m.p = realloc(m.p, sizeof(mparam_t) * (m.np + 1)); m.p[m.np++] = mp;
+            }
+            c->map = realloc(c->map, sizeof(map_t) * (c->nmap + 1)); c->map[c->nmap++] = m;
+        } else if (!strcmp(n, "split_clients") && d->nargs == 3 && d->block) {
+            split_t s; memset(&s, 0, sizeof s);
+            s.src = strdup(d->args[1]); s.var = strdup(d->args[2] + 1);
+            uint64_t last = 0; uint32_t sum = 0;
+            for (int k = 0; k < d->nkids; k++) {
+                dir_t *p = &d->kids[k];
+                if (p->nargs != 2) continue;
+                part_t pt; memset(&pt, 0, sizeof pt); pt.val = strdup(p->args[1]);
+                if (!strcmp(p->args[0], "*")) { pt.star = 1; pt.bound = 0; }
+                else {
+                    /* ngx_atofp(value, len-1, 2): fixed point with 2 decimals */
+                    const char *v = p->args[0]; int len = p->alen[0] - 1; uint32_t pc = 0; int dot = -1, dec = 0;
+                    for (int q = 0; q < len; q++) {
+                        if (v[q] == '.') { dot = q; continue; }
+                        if (dot >= 0) { if (dec < 2) { pc = pc * 10 + (v[q] - '0'); dec++; } }
+                        else pc = pc * 10 + (v[q] - '0');
+                    }
+                    while (dec < 2) { pc *= 10; dec++; }
+                    sum += pc;
+                    last += (uint64_t)pc * 0xffffffffull / 10000;
+                    pt.bound = (uint32_t)last;
+                }
+                s.p = realloc(s.p, sizeof(part_t) * (s.np + 1)); s.p[s.np++] = pt;
+            }
+            (void)sum;
+            c->spl = realloc(c->spl, sizeof(split_t) * (c->nspl + 1)); c->spl[c->nspl++] = s;
+        } else if (!strcmp(n, "server") && d->block) {
+            add_server(B, d, c->http_waf);
+        }
+    }
+}
+
+static void add_location(build_t *B, srv_t *S, dir_t *d, int srv_waf) {
+    orc_ctx *c = B->c;
+    loc_t L; memset(&L, 0, sizeof L);
+    L.id = c->nloc; L.server = S->id; L.waf_mode = srv_waf; L.upstream_id = -1;
+    const char *a1 = d->nargs > 1 ? d->args[1] : "";
+    if (d->nargs == 3) {
+        if (!strcmp(a1, "=")) L.kind = LK_EXACT;
+        else if (!strcmp(a1, "^~")) L.kind = LK_NOREGEX;
+        else if (!strcmp(a1, "~")) L.kind = LK_REGEX;
+        else if (!strcmp(a1, "~*")) L.kind = LK_REGEX_I;
+        L.path = strdup(d->args[2]); L.plen = d->alen[2];
+    } else {
+        L.path = strdup(a1); L.plen = d->alen[1];
+        L.kind = (L.plen && L.path[0] == '@') ? LK_NAMED : LK_PREFIX;
+    }
+    if (L.kind == LK_REGEX || L.kind == LK_REGEX_I) L.re = re_compile(L.path, L.kind == LK_REGEX_I);
+    for (int i = 0; i < d->nkids; i++) {
+        dir_t *k = &d->kids[i];
+        if (!k->nargs) continue;
+        if (!strcmp(k->args[0], "proxy_pass") && k->nargs == 2) {
+            const char *u = k->args[1];
+            const char *p = strstr(u, "://"); p = p ? p + 3 : u;
+            int n = 0; while (p[n] && p[n] != '/' && p[n] != '$') n++;
+            L.proxy_ups = xstrndup(p, n); L.has_proxy = 1;
+        } else if (!strcmp(k->args[0], "return") && k->nargs >= 2) {
+            L.has_return = 1; L.ret_code = atoi(k->args[1]);
+            if (!isdigit((unsigned char)k->args[1][0])) L.ret_code = 302;
+        } else if (!strcmp(k->args[0], "error_page") && k->nargs == 4 && !strcmp(k->args[1], "418") &&
+                   !strcmp(k->args[2], "=")) {
+            L.err418 = strdup(k->args[3]);
+        } else if (!strcmp(k->args[0], "wallarm_mode") && k->nargs == 2) {
+            L.waf_mode = waf_mode_of(k->args[1]);
+        }
+    }
+    if (L.has_proxy && L.plen && L.path[L.plen - 1] == '/' && (L.kind == LK_PREFIX || L.kind == LK_EXACT ||
+                                                               L.kind == LK_NOREGEX))
+        L.auto_redirect = 1;
+    c->loc = realloc(c->loc, sizeof(loc_t) * (c->nloc + 1)); c->loc[c->nloc++] = L;
+    S->locs = realloc(S->locs, sizeof(int) * (S->nlocs + 1)); S->locs[S->nlocs++] = L.id;
+}
+
+static void add_server(build_t *B, dir_t *s, int http_waf) {
+    orc_ctx *c = B->c;
+    srv_t S; memset(&S, 0, sizeof S);
+    S.id = c->nsrv; S.waf_mode = http_waf;
+    for (int i = 0; i < s->nkids; i++) {
+        dir_t *d = &s->kids[i];
+        if (d->nargs == 2 && !strcmp(d->args[0], "wallarm_mode")) S.waf_mode = waf_mode_of(d->args[1]);
+    }
+    c->srv = realloc(c->srv, sizeof(srv_t) * (c->nsrv + 1)); c->nsrv++;
+    for (int i = 0; i < s->nkids; i++) {
+        dir_t *d = &s->kids[i];
+        if (!d->nargs) continue;
+        const char *n = d->args[0];
+        if (!strcmp(n, "listen") && d->nargs >= 2) {
+            const char *a = d->args[1];
+            if (!strncmp(a, "unix:", 5)) continue;
+            const char *colon = strrchr(a, ':');
+            int port = atoi(colon ? colon + 1 : a);
+            int ssl = 0, def = 0;
+            for (int k = 2; k < d->nargs; k++) {
+                if (!strcmp(d->args[k], "ssl")) ssl = 1;
+                if (!strcmp(d->args[k], "default_server") || !strcmp(d->args[k], "default")) def = 1;
+            }
+            if (S.nports < 16) { S.ports[S.nports] = port; S.ssl[S.nports] = ssl; S.def[S.nports] = def; S.nports++; }
+        } else if (!strcmp(n, "server_name")) {
+            for (int k = 1; k < d->nargs; k++) {
+                S.names = realloc(S.names, sizeof(char *) * (S.nnames + 1));
+                S.nlen = realloc(S.nlen, sizeof(int) * (S.nnames + 1));
+                S.nre = realloc(S.nre, sizeof(pcre *) * (S.nnames + 1));
+                char *nm = strdup(d->args[k]);
+                S.nre[S.nnames] = NULL;
+                if (nm[0] == '~') S.nre[S.nnames] = re_compile(nm + 1, 0);
+                else for (char *q = nm; *q; q++) *q = (char)lc((unsigned char)*q);
+                S.names[S.nnames] = nm; S.nlen[S.nnames] = (int)strlen(nm); S.nnames++;
+            }
+        } else if (!strcmp(n, "if") && d->block) {
+            /* server rewrite phase: if (<var> [op value]) { return code [text]; } */
+            sif_t f; memset(&f, 0, sizeof f);
+            int a0 = 1, a1 = d->nargs - 1;
+            char *first = d->args[a0]; char *last = d->args[a1];
+            if (first[0] == '(') { if (first[1] == 0) a0++; else memmove(first, first + 1, strlen(first)); }
+            int ll = (int)strlen(d->args[a1]);
+            if (ll && d->args[a1][ll - 1] == ')') { if (ll == 1) a1--; else d->args[a1][ll - 1] = 0; }
+            (void)last;
+            f.var = strdup(d->args[a0]);
+            if (a1 - a0 == 2) {
+                const char *op = d->args[a0 + 1];
+                f.val = strdup(d->args[a0 + 2]);
+                if (!strcmp(op, "=")) f.op = 1;
+                else if (!strcmp(op, "!=")) f.op = 2;
+                else if (!strcmp(op, "~")) { f.op = 3; f.re = re_compile(f.val, 0); }
+                else if (!strcmp(op, "~*")) { f.op = 3; f.re = re_compile(f.val, 1); }
+                else if (!strcmp(op, "!~")) { f.op = 4; f.re = re_compile(f.val, 0); }
+                else if (!strcmp(op, "!~*")) { f.op = 4; f.re = re_compile(f.val, 1); }
+            }
+            int has_ret = 0;
+            for (int k = 0; k < d->nkids; k++) {
+                dir_t *r = &d->kids[k];
+                if (r->nargs >= 2 && !strcmp(r->args[0], "return")) {
+                    has_ret = 1;
+                    if (isdigit((unsigned char)r->args[1][0])) f.code = atoi(r->args[1]); else f.code = 302;
+                }
+            }
+            if (!has_ret) continue;   /* e.g. HSTS `if` only sets a header variable */
+            S.ifs = realloc(S.ifs, sizeof(sif_t) * (S.nifs + 1)); S.ifs[S.nifs++] = f;
+        } else if (!strcmp(n, "return") && d->nargs >= 2) {
+            sif_t f; memset(&f, 0, sizeof f); f.is_return_only = 1;
+            f.code = isdigit((unsigned char)d->args[1][0]) ? atoi(d->args[1]) : 302;
+            S.ifs = realloc(S.ifs, sizeof(sif_t) * (S.nifs + 1)); S.ifs[S.nifs++] = f;
+        } else if (!strcmp(n, "location") && d->block) {
+            add_location(B, &S, d, S.waf_mode);
+        }
+    }
+    c->srv[S.id] = S;
+}
+
+/* ------------------------------------------------------------------ signatures + Aho-Corasick */
+static int hexval(int ch) { return isdigit(ch) ? ch - '0' : (lc((unsigned char)ch) - 'a' + 10); }
+
+static int load_sigs(orc_ctx *c, const char *t, int n) {
+    int i = 0;
+    while (i < n) {
+        int e = i; while (e < n && t[e] != '\n') e++;
+        int ls = i; while (ls < e && (t[ls] == ' ' || t[ls] == '\t' || t[ls] == '\r')) ls++;
+        int le = e; while (le > ls && (t[le - 1] == '\r' || t[le - 1] == ' ' || t[le - 1] == '\t')) le--;
+        i = e + 1;
+        if (ls >= le || t[ls] == '#') continue;
+        char kind[8] = {0}, fl[8] = {0}, zs[8] = {0};
+        int p = ls, f = 0;
+        char *dst[3] = {kind, fl, zs};
+        for (f = 0; f < 3; f++) {
+            int q = 0; while (p < le && t[p] != ' ') { if (q < 7) dst[f][q++] = t[p]; p++; }
+            while (p < le && t[p] == ' ') p++;
+        }
+        sig_t s; memset(&s, 0, sizeof s);
+        s.nocase = fl[0] == 'i';
+        for (char *z = zs; *z; z++) s.zones |= (*z == 'u') ? 1 : (*z == 'a') ? 2 : (*z == 'h') ? 4 : (*z == 'b') ? 8 : 0;
+        if (!strcmp(kind, "lit")) {
+            s.kind = 0; s.len = (le - p) / 2; s.lit = malloc(s.len + 1);
+            for (int k = 0; k < s.len; k++) s.lit[k] = (uint8_t)(hexval(t[p + 2 * k]) * 16 + hexval(t[p + 2 * k + 1]));
+        } else {
+            s.kind = 1;
+            char *pat = xstrndup(t + p, le - p);
+            s.re = re_compile(pat, s.nocase);
+            free(pat);
+            if (!s.re) { seterr("bad signature regex", NULL); return -1; }
+            const char *er;
+            s.ex = pcre_study(s.re, PCRE_STUDY_JIT_COMPILE, &er);
+        }
+        c->sig = realloc(c->sig, sizeof(sig_t) * (c->nsig + 1)); c->sig[c->nsig++] = s;
+    }
+    return 0;
+}
+
+static void build_ac(orc_ctx *c) {
+    int total = 1;
+    for (int i = 0; i < c->nsig; i++) if (c->sig[i].kind == 0) total += c->sig[i].len;
+    int32_t *nx = malloc(sizeof(int32_t) * 256 * (size_t)total);
+    for (size_t k = 0; k < 256 * (size_t)total; k++) nx[k] = -1;
+    int32_t *out = malloc(sizeof(int32_t) * total), *fail = calloc(total, sizeof(int32_t));
+    int32_t *dict = malloc(sizeof(int32_t) * total);
+    for (int k = 0; k < total; k++) { out[k] = -1; dict[k] = -1; }
+    int32_t *pnext = malloc(sizeof(int32_t) * (c->nsig + 1));
+    int ns = 1;
+    for (int i = 0; i < c->nsig; i++) {
+        if (c->sig[i].kind != 0) continue;
+        int s = 0;
+        for (int k = 0; k < c->sig[i].len; k++) {
+            int b = lc(c->sig[i].lit[k]);
+            if (nx[(size_t)s * 256 + b] < 0) nx[(size_t)s * 256 + b] = ns++;
+            s = nx[(size_t)s * 256 + b];
+        }
+        pnext[i] = out[s]; out[s] = i;
+    }
+    int32_t *q = malloc(sizeof(int32_t) * ns); int qh = 0, qt = 0;
+    for (int b = 0; b < 256; b++) {
+        int t = nx[b];
+        if (t < 0) nx[b] = 0; else { fail[t] = 0; q[qt++] = t; }
+    }
+    while (qh < qt) {
+        int s = q[qh++];
+        dict[s] = (out[fail[s]] >= 0) ? fail[s] : dict[fail[s]];
+        for (int b = 0; b < 256; b++) {
+            int t = nx[(size_t)s * 256 + b];
+            if (t < 0) nx[(size_t)s * 256 + b] = nx[(size_t)fail[s] * 256 + b];
+            else { fail[t] = nx[(size_t)fail[s] * 256 + b]; q[qt++] = t; }
+        }
+    }
+    free(q); free(fail);
+    c->ac_next = nx; c->ac_states = ns; c->ac_out = out; c->ac_dict = dict; c->ac_pat_next = pnext;
+}
+
+/* ------------------------------------------------------------------ public: create */
+orc_ctx *orc_create(const void *blob, size_t len, uint32_t gen) {
+    const uint8_t *b = blob;
+    if (len < 8) { seterr("short blob", NULL); return NULL; }
+    uint32_t magic, n; memcpy(&magic, b, 4); memcpy(&n, b + 4, 4);
+    if (magic != GM_BLOB_MAGIC) { seterr("bad magic", NULL); return NULL; }
+    size_t off = 8;
+    dir_t *mainroot = NULL; build_t B; memset(&B, 0, sizeof B);
+    orc_ctx *c = calloc(1, sizeof *c); c->gen = gen; B.c = c;
+    const char *sigt = NULL; int sign = 0;
+    for (uint32_t e = 0; e < n; e++) {
+        uint32_t kind, nl, dl;
+        memcpy(&kind, b + off, 4); memcpy(&nl, b + off + 4, 4); memcpy(&dl, b + off + 8, 4); off += 12;
+        const char *data = (const char *)b + off + nl; off += nl + dl;
+        if (kind == GM_ENTRY_SIGS) { sigt = data; sign = (int)dl; continue; }
+        dir_t *root = calloc(1, sizeof(dir_t));
+        lexer L = {data, (int)dl, 0, malloc(dl + 1)};
+        if (parse_block(&L, root, 0) < 0) { seterr("config parse error", NULL); return NULL; }
+        if (kind == GM_ENTRY_MAIN) mainroot = root;
+        else { B.confd = realloc(B.confd, sizeof(dir_t *) * (B.nconfd + 1)); B.confd[B.nconfd++] = root; }
+    }
+    if (mainroot) {
+        for (int i = 0; i < mainroot->nkids; i++)
+            if (mainroot->kids[i].nargs && !strcmp(mainroot->kids[i].args[0], "http") && mainroot->kids[i].block)
+                walk_http(&B, &mainroot->kids[i]);
+    } else {
+        for (int k = 0; k < B.nconfd; k++) walk_http(&B, B.confd[k]);
+    }
+    /* upstream id = index in the sorted, de-duplicated upstream-name table */
+    qsort(c->ups, c->nups, sizeof(char *), cmp_str);
+    int u = 0;
+    for (int i = 0; i < c->nups; i++) if (u == 0 || strcmp(c->ups[u - 1], c->ups[i])) c->ups[u++] = c->ups[i];
+    c->nups = u;
+    for (int i = 0; i < c->nloc; i++) {
+        loc_t *L = &c->loc[i];
+        if (!L->has_proxy) continue;
+        char *key = L->proxy_ups;
+        char **hit = bsearch(&key, c->ups, c->nups, sizeof(char *), cmp_str);
+        L->upstream_id = hit ? (int)(hit - c->ups) : -1;
+    }
+    if (sigt && load_sigs(c, sigt, sign) < 0) return NULL;
+    build_ac(c);
+    return c;
+}
+
+void orc_destroy(orc_ctx *c) { (void)c; /* test process lifetime; intentionally leaked */ }
+
+int orc_info(orc_ctx *c, uint32_t *out4) {
+    out4[0] = c->nsrv; out4[1] = c->nloc; out4[2] = c->nups; out4[3] = c->nsig; return 0;
+}
+
+/* ------------------------------------------------------------------ request access */
+typedef struct {
+    const gm_req *r; const uint8_t *a;
+    sv uri, args, hdrs, body, host, method, ruri, raddr;
+} rq_t;
+
+static void rq_init(rq_t *q, const gm_req *r, const uint8_t *arena) {
+    q->r = r; q->a = arena;
+    const char *p = (const char *)arena + r->base;
+    q->uri = (sv){p, (int)r->uri_len}; p += r->uri_len;
+    q->args = (sv){p, (int)r->args_len}; p += r->args_len;
+    q->hdrs = (sv){p, (int)r->hdr_len}; p += r->hdr_len;
+    q->body = (sv){p, (int)r->body_len}; p += r->body_len;
+    q->host = (sv){p, r->host_len}; p += r->host_len;
+    q->method = (sv){p, r->method_len}; p += r->method_len;
+    q->ruri = (sv){p, r->ruri_len}; p += r->ruri_len;
+    q->raddr = (sv){p, r->raddr_len};
+}
+
+/* scratch string arena, per thread: chunked so earlier views stay valid until reset */
+typedef struct chunk { struct chunk *next; int cap, used; char data[]; } chunk_t;
+typedef struct { chunk_t *head; } scratch_t;
+static sv sc_put(scratch_t *s, const char *p, int n) {
+    if (!s->head || s->head->used + n > s->head->cap) {
+        int cap = n > (1 << 16) ? n : (1 << 16);
+        chunk_t *c = malloc(sizeof(chunk_t) + cap); c->cap = cap; c->used = 0; c->next = s->head; s->head = c;
+    }
+    char *d = s->head->data + s->head->used;
+    memcpy(d, p, n); s->head->used += n;
+    return (sv){d, n};
+}
+static void sc_reset(scratch_t *s) {
+    while (s->head && s->head->next) { chunk_t *n = s->head->next; free(s->head); s->head = n; }
+    if (s->head) s->head->used = 0;
+}
+
+/* iterate header lines "Name: value\r\n"; value OWS-trimmed */
+static int hdr_next(sv h, int *pos, sv *name, sv *val) {
+    while (*pos < h.n) {
+        int st = *pos, e = st;
+        while (e < h.n && h.p[e] != '\n') e++;
+        *pos = e + 1;
+        int le = e; if (le > st && h.p[le - 1] == '\r') le--;
+        int c = st; while (c < le && h.p[c] != ':') c++;
+        if (c >= le) continue;
+        *name = (sv){h.p + st, c - st};
+        int vs = c + 1; while (vs < le && (h.p[vs] == ' ' || h.p[vs] == '\t')) vs++;
+        int ve = le; while (ve > vs && (h.p[ve - 1] == ' ' || h.p[ve - 1] == '\t')) ve--;
+        *val = (sv){h.p + vs, ve - vs};
+        return 1;
+    }
+    return 0;
+}
+
+/* ngx_http_variable_unknown_header: lowercase, '-' -> '_' compare against var suffix */
+static int hdr_name_match(sv name, const char *var, int vlen) {
+    if (name.n != vlen) return 0;
+    for (int i = 0; i < vlen; i++) {
+        unsigned char ch = (unsigned char)name.p[i];
+        if (ch >= 'A' && ch <= 'Z') ch |= 0x20; else if (ch == '-') ch = '_';
+        if ((unsigned char)var[i] != ch) return 0;
+    }
+    return 1;
+}
+
+static uint32_t murmur2(const uint8_t *data, size_t len) {
+    uint32_t h = 0 ^ (uint32_t)len, k;
+    while (len >= 4) {
+        k = data[0]; k |= data[1] << 8; k |= data[2] << 16; k |= (uint32_t)data[3] << 24;
+        k *= 0x5bd1e995; k ^= k >> 24; k *= 0x5bd1e995;
+        h *= 0x5bd1e995; h ^= k;
+        data += 4; len -= 4;
+    }
+    switch (len) {
+    case 3: h ^= data[2] << 16; /* fallthrough */
+    case 2: h ^= data[1] << 8;  /* fallthrough */
+    case 1: h ^= data[0]; h *= 0x5bd1e995;
+    }
+    h ^= h >> 13; h *= 0x5bd1e995; h ^= h >> 15;
+    return h;
+}
+uint32_t orc_murmur2(const uint8_t *d, size_t n) { return murmur2(d, n); }
+
+typedef struct { orc_ctx *c; rq_t *q; scratch_t *sc; int depth; int *last_param; int *last_part; } ev_t;
+
+static sv eval_complex(ev_t *E, const char *tpl);
+
+static sv get_var(ev_t *E, const char *name, int nlen) {
+    rq_t *q = E->q; const gm_req *r = q->r; orc_ctx *c = E->c;
+    char nm[256]; if (nlen > 255) nlen = 255; memcpy(nm, name, nlen); nm[nlen] = 0;
+    for (int i = 0; i < nlen; i++) nm[i] = (char)lc((unsigned char)nm[i]);
+    if (!strcmp(nm, "scheme")) return (r->flags & GM_REQ_HTTPS) ? (sv){"https", 5} : (sv){"http", 4};
+    if (!strcmp(nm, "https")) return (r->flags & GM_REQ_HTTPS) ? (sv){"on", 2} : (sv){"", 0};
+    if (!strcmp(nm, "http2")) return (r->flags & GM_REQ_HTTP2) ? (sv){"h2", 2} : (sv){"", 0};
+    if (!strcmp(nm, "request_method")) return q->method;
+    if (!strcmp(nm, "args") || !strcmp(nm, "query_string")) return q->args;
+    if (!strcmp(nm, "uri") || !strcmp(nm, "document_uri")) return q->uri;
+    if (!strcmp(nm, "request_body")) return (sv){"", 0};
+    if (!strcmp(nm, "remote_addr")) return q->raddr;
+    if (!strcmp(nm, "remote_port")) { char t[8]; int n = snprintf(t, 8, "%u", r->remote_port); return sc_put(E->sc, t, n); }
+    if (!strcmp(nm, "server_port")) { char t[8]; int n = snprintf(t, 8, "%u", r->port); return sc_put(E->sc, t, n); }
+    if (!strcmp(nm, "request_uri")) {
+        if (q->ruri.n) return q->ruri;
+        char *t = malloc(q->uri.n + q->args.n + 2); int n = 0;
+        memcpy(t, q->uri.p, q->uri.n); n = q->uri.n;
+        if (q->args.n) { t[n++] = '?'; memcpy(t + n, q->args.p, q->args.n); n += q->args.n; }
+        sv s = sc_put(E->sc, t, n); free(t); return s;
+    }
+    if (!strcmp(nm, "request")) {
+        sv ru = get_var(E, "request_uri", 11);
+        const char *proto = (r->flags & GM_REQ_HTTP2) ? "HTTP/2.0" : (r->flags & GM_REQ_HTTP10) ? "HTTP/1.0" : "HTTP/1.1";
+        int pl = (int)strlen(proto);
+        char *t = malloc(q->method.n + ru.n + pl + 3); int n = 0;
+        memcpy(t + n, q->method.p, q->method.n); n += q->method.n; t[n++] = ' ';
+        memcpy(t + n, ru.p, ru.n); n += ru.n; t[n++] = ' ';
+        memcpy(t + n, proto, pl); n += pl;
+        sv s = sc_put(E->sc, t, n); free(t); return s;
+    }
+    if (!strcmp(nm, "request_id")) {
+        char t[32]; static const char hx[] = "0123456789abcdef";
+        for (int i = 0; i < 16; i++) { t[2 * i] = hx[r->rid[i] >> 4]; t[2 * i + 1] = hx[r->rid[i] & 15]; }
+        return sc_put(E->sc, t, 32);
+    }
+    if (!strncmp(nm, "http_", 5)) {
+        const char *hv = nm + 5; int hl = nlen - 5;
+        int joined = !strcmp(hv, "cookie") ? ';' : !strcmp(hv, "x_forwarded_for") ? ',' : 0;
+        int pos = 0; sv hn, vv; sv acc = {"", 0}; int have = 0; char *tmp = NULL; int tn = 0;
+        while (hdr_next(q->hdrs, &pos, &hn, &vv)) {
+            if (!hdr_name_match(hn, hv, hl)) continue;
+            if (!joined) return vv;
+            tmp = realloc(tmp, tn + vv.n + 2);
+            if (have) { tmp[tn++] = (char)joined; tmp[tn++] = ' '; }
+            memcpy(tmp + tn, vv.p, vv.n); tn += vv.n; have = 1;
+        }
+        if (have) { acc = sc_put(E->sc, tmp, tn); }
+        free(tmp);
+        return acc;
+    }
+    if (!strncmp(nm, "cookie_", 7)) {
+        /* ngx_http_parse_multi_header_lines over all Cookie lines */
+        const char *cn = nm + 7; int cl = nlen - 7;
+        int pos = 0; sv hn, vv;
+        while (hdr_next(q->hdrs, &pos, &hn, &vv)) {
+            if (!hdr_name_match(hn, "cookie", 6)) continue;
+            if (cl > vv.n) continue;
+            const char *start = vv.p, *end = vv.p + vv.n;
+            while (start < end) {
+                if (end - start < cl || strncasecmp(start, cn, cl) != 0) goto skip;
+                for (start += cl; start < end && *start == ' '; start++) {}
+                if (start == end || *start++ != '=') goto skip;
+                while (start < end && *start == ' ') start++;
+                const char *last = start;
+                while (last < end && *last != ';') last++;
+                return (sv){start, (int)(last - start)};
+            skip:
+                while (start < end) { char ch = *start++; if (ch == ';' || ch == ',') break; }
+                while (start < end && *start == ' ') start++;
+            }
+        }
+        return (sv){"", 0};
+    }
+    if (!strncmp(nm, "arg_", 4)) {
+        /* ngx_http_arg */
+        const char *an = nm + 4; int alen = nlen - 4;
+        const char *a = q->args.p; int n = q->args.n;
+        for (int p = 0; p + alen < n; p++) {
+            if (strncasecmp(a + p, an, alen) != 0) continue;
+            if ((p == 0 || a[p - 1] == '&') && a[p + alen] == '=') {
+                int vs = p + alen + 1, ve = vs;
+                while (ve < n && a[ve] != '&') ve++;
+                return (sv){a + vs, ve - vs};
+            }
+        }
+        return (sv){"", 0};
+    }
+    if (!strcmp(nm, "host")) {
+        return q->host;   /* not verdict-relevant here (redirect Location text) */
+    }
+    /* map / split_clients variables */
+    if (E->depth > 32) return (sv){"", 0};
+    for (int i = 0; i < c->nmap; i++) {
+        map_t *m = &c->map[i];
+        if (strcmp(m->var, nm)) continue;
+        E->depth++;
+        sv src = eval_complex(E, m->src);
+        const char *res = NULL; int pidx = -1;
+        /* ngx_http_map_find: lowercased exact key, then regexes only for non-empty value */
+        for (int k = 0; k < m->np && !res; k++) {
+            if (m->p[k].is_re) continue;
+            if (m->p[k].klen != src.n) continue;
+            int ok = 1;
+            for (int t = 0; t < src.n; t++) if (lc((unsigned char)src.p[t]) != (unsigned char)m->p[k].key[t]) { ok = 0; break; }
+            if (ok) { res = m->p[k].val; pidx = k; }
+        }
+        if (!res && src.n) {
+            for (int k = 0; k < m->np && !res; k++) {
+                if (!m->p[k].is_re || !m->p[k].re) continue;
+                int ov[30];
+                if (pcre_exec(m->p[k].re, NULL, src.p, src.n, 0, 0, ov, 30) >= 0) { res = m->p[k].val; pidx = k; }
+            }
+        }
+        if (!res) { res = m->defval ? m->defval : ""; pidx = -1; }
+        if (E->last_param) *E->last_param = pidx;
+        sv out = eval_complex(E, res);
+        E->depth--;
+        return out;
+    }
+    for (int i = 0; i < c->nspl; i++) {
+        split_t *s = &c->spl[i];
+        if (strcmp(s->var, nm)) continue;
+        E->depth++;
+        sv src = eval_complex(E, s->src);
+        uint32_t h = murmur2((const uint8_t *)src.p, src.n);
+        sv out = {"", 0}; int part = -1;
+        for (int k = 0; k < s->np; k++) {
+            if (h < s->p[k].bound || s->p[k].star) { part = k; out = eval_complex(E, s->p[k].val); break; }
+        }
+        if (E->last_part) *E->last_part = part;
+        E->depth--;
+        return out;
+    }
+    return (sv){"", 0};
+}
+
+static int is_var_ch(char ch) { return isalnum((unsigned char)ch) || ch == '_'; }
+
+static sv eval_complex(ev_t *E, const char *tpl) {
+    if (!strchr(tpl, '$')) return (sv){tpl, (int)strlen(tpl)};
+    char *out = NULL; int on = 0;
+    for (const char *p = tpl; *p;) {
+        if (*p == '$') {
+            p++;
+            const char *st; int n;
+            if (*p == '{') { st = ++p; while (*p && *p != '}') p++; n = (int)(p - st); if (*p) p++; }
+            else { st = p; while (is_var_ch(*p)) p++; n = (int)(p - st); }
+            sv v = get_var(E, st, n);
+            out = realloc(out, on + v.n + 1); memcpy(out + on, v.p, v.n); on += v.n;
+        } else {
+            out = realloc(out, on + 2); out[on++] = *p++;
+        }
+    }
+    sv r = sc_put(E->sc, out ? out : "", on); free(out); return r;
+}
+
+/* ------------------------------------------------------------------ host (ngx_http_validate_host) */
+static int validate_host(sv h, char *out, int *outlen) {
+    int dot_pos = h.n, host_len = h.n, state = 0; /* 0 usual, 1 literal, 2 rest */
+    for (int i = 0; i < h.n; i++) {
+        unsigned char ch = (unsigned char)h.p[i];
+        switch (ch) {
+        case '.':
+            if (dot_pos == i - 1) return -1;
+            dot_pos = i; break;
+        case ':':
+            if (state == 0) { host_len = i; state = 2; }
+            break;
+        case '[':
+            if (i == 0) state = 1;
+            break;
+        case ']':
+            if (state == 1) { host_len = i + 1; state = 2; }
+            break;
+        case '\0':
+            return -1;
+        default:
+            if (ch == '/') return -1;
+            break;
+        }
+    }
+    if (dot_pos == host_len - 1) host_len--;
+    if (host_len == 0) return -1;
+    for (int i = 0; i < host_len; i++) out[i] = (char)lc((unsigned char)h.p[i]);
+    *outlen = host_len;
+    return 0;
+}
+
+static int find_server(orc_ctx *c, int port, int is_https, sv host, int *bad, int *port_ssl) {
+    /* servers listening on port, config order */
+    int def = -1, first = -1; int ssl = 0;
+    for (int s = 0; s < c->nsrv; s++)
+        for (int k = 0; k < c->srv[s].nports; k++)
+            if (c->srv[s].ports[k] == port) {
+                if (first < 0) first = s;
+                if (c->srv[s].def[k] && def < 0) def = s;
+                if (c->srv[s].ssl[k]) ssl = 1;
+            }
+    *port_ssl = ssl; (void)is_https;
+    if (first < 0) return -1;
+    if (def < 0) def = first;
+    *bad = 0;
+    if (host.n == 0) return def;
+    char hn[65536]; int hl;
+    if (validate_host(host, hn, &hl) < 0) { *bad = 1; return def; }
+    int best = -1, bestlen = -1;
+    /* exact */
+    for (int s = 0; s < c->nsrv && best < 0; s++) {
+        int on = 0; for (int k = 0; k < c->srv[s].nports; k++) if (c->srv[s].ports[k] == port) on = 1;
+        if (!on) continue;
+        for (int k = 0; k < c->srv[s].nnames; k++) {
+            const char *nm = c->srv[s].names[k]; int nl = c->srv[s].nlen[k];
+            if (nm[0] == '*' || nm[0] == '~' || nm[0] == '.' || (nl && nm[nl - 1] == '*')) continue;
+            if (nl == hl && !memcmp(nm, hn, hl)) { best = s; break; }
+        }
+    }
+    if (best >= 0) return best;
+    /* wildcard head: "*.x" / ".x" -- longest suffix wins, earlier server on ties */
+    for (int s = 0; s < c->nsrv; s++) {
+        int on = 0; for (int k = 0; k < c->srv[s].nports; k++) if (c->srv[s].ports[k] == port) on = 1;
+        if (!on) continue;
+        for (int k = 0; k < c->srv[s].nnames; k++) {
+            const char *nm = c->srv[s].names[k]; int nl = c->srv[s].nlen[k];
+            const char *suf = NULL; int sl = 0, dotform = 0;
+            if (nl > 2 && nm[0] == '*' && nm[1] == '.') { suf = nm + 1; sl = nl - 1; }
+            else if (nl > 1 && nm[0] == '.') { suf = nm; sl = nl; dotform = 1; }
+            if (!suf) continue;
+            int m = 0;
+            if (hl > sl && !memcmp(hn + hl - sl, suf, sl)) m = 1;
+            if (dotform && hl == sl - 1 && !memcmp(hn, suf + 1, sl - 1)) m = 1;
+            if (m && sl > bestlen) { best = s; bestlen = sl; }
+        }
+    }
+    if (best >= 0) return best;
+    /* wildcard tail "x.*" */
+    for (int s = 0; s < c->nsrv; s++) {
+        int on = 0; for (int k = 0; k < c->srv[s].nports; k++) if (c->srv[s].ports[k] == port) on = 1;
+        if (!on) continue;
+        for (int k = 0; k < c->srv[s].nnames; k++) {
+            const char *nm = c->srv[s].names[k]; int nl = c->srv[s].nlen[k];
+            if (nl < 3 || nm[nl - 1] != '*' || nm[nl - 2] != '.') continue;
+            int pl = nl - 1;   /* "x." */
+            if (hl > pl && !memcmp(hn, nm, pl) && pl > bestlen) { best = s; bestlen = pl; }
+        }
+    }
+    if (best >= 0) return best;
+    /* regex names in order */
+    for (int s = 0; s < c->nsrv; s++) {
+        int on = 0; for (int k = 0; k < c->srv[s].nports; k++) if (c->srv[s].ports[k] == port) on = 1;
+        if (!on) continue;
+        for (int k = 0; k < c->srv[s].nnames; k++) {
+            if (!c->srv[s].nre[k]) continue;
+            int ov[30];
+            if (pcre_exec(c->srv[s].nre[k], NULL, hn, hl, 0, 0, ov, 30) >= 0) return s;
+        }
+    }
+    return def;
+}
+
+/* ngx_http_core_find_location restated over the server's top-level locations */
+static int find_location(orc_ctx *c, srv_t *S, sv uri, int *auto301) {
+    *auto301 = 0;
+    for (int i = 0; i < S->nlocs; i++) {
+        loc_t *L = &c->loc[S->locs[i]];
+        if (L->kind == LK_EXACT && L->plen == uri.n && !memcmp(L->path, uri.p, uri.n)) return L->id;
+    }
+    int best = -1, bestlen = -1, prefix_equal = 0;
+    for (int i = 0; i < S->nlocs; i++) {
+        loc_t *L = &c->loc[S->locs[i]];
+        if (L->kind != LK_PREFIX && L->kind != LK_NOREGEX) continue;
+        if (L->plen <= uri.n && !memcmp(L->path, uri.p, L->plen) && L->plen > bestlen) {
+            best = L->id; bestlen = L->plen; prefix_equal = (L->plen == uri.n);
+        }
+    }
+    /* auto_redirect: a location named uri + "/" and nothing (prefix or exact) named uri itself */
+    if (!prefix_equal) {
+        for (int i = 0; i < S->nlocs; i++) {
+            loc_t *L = &c->loc[S->locs[i]];
+            if (L->kind == LK_REGEX || L->kind == LK_REGEX_I || L->kind == LK_NAMED) continue;
+            if (L->auto_redirect && L->plen == uri.n + 1 && !memcmp(L->path, uri.p, uri.n)) {
+                *auto301 = 1; return L->id;
+            }
+        }
+    }
+    if (best >= 0 && c->loc[best].kind == LK_NOREGEX) return best;
+    for (int i = 0; i < S->nlocs; i++) {
+        loc_t *L = &c->loc[S->locs[i]];
+        if ((L->kind != LK_REGEX && L->kind != LK_REGEX_I) || !L->re) continue;
+        int ov[30];
+        if (pcre_exec(L->re, NULL, uri.p, uri.n, 0, 0, ov, 30) >= 0) return L->id;
+    }
+    return best;
+}
+
+static int find_named(orc_ctx *c, srv_t *S, sv name) {
+    for (int i = 0; i < S->nlocs; i++) {
+        loc_t *L = &c->loc[S->locs[i]];
+        if (L->kind == LK_NAMED && L->plen == name.n && !memcmp(L->path, name.p, name.n)) return L->id;
+    }
+    return -1;
+}
+
+/* ------------------------------------------------------------------ per request */
+typedef struct { uint32_t *ids; size_t n, cap; } hitbuf_t;
+
+static void hb_push(hitbuf_t *h, uint32_t v) {
+    if (h->n == h->cap) { h->cap = h->cap ? h->cap * 2 : 1024; h->ids = realloc(h->ids, h->cap * 4); }
+    h->ids[h->n++] = v;
+}
+
+static void waf_scan(orc_ctx *c, rq_t *q, uint8_t *mark, hitbuf_t *out) {
+    sv zones[4] = {q->uri, q->args, q->hdrs, q->body};
+    size_t first = out->n;
+    for (int z = 0; z < 4; z++) {
+        sv Z = zones[z];
+        int s = 0;
+        for (int i = 0; i < Z.n; i++) {
+            s = c->ac_next[(size_t)s * 256 + lc((unsigned char)Z.p[i])];
+            int t = (c->ac_out[s] >= 0) ? s : c->ac_dict[s];
+            while (t > 0) {
+                for (int p = c->ac_out[t]; p >= 0; p = c->ac_pat_next[p]) {
+                    sig_t *g = &c->sig[p];
+                    if (mark[p] || !(g->zones & (1 << z))) continue;
+                    int st = i - g->len + 1;
+                    if (!g->nocase && memcmp(Z.p + st, g->lit, g->len)) continue;
+                    mark[p] = 1; hb_push(out, (uint32_t)p);
+                }
+                t = c->ac_dict[t];
+            }
+        }
+    }
+    for (int p = 0; p < c->nsig; p++) {
+        sig_t *g = &c->sig[p];
+        if (g->kind != 1 || !g->re || mark[p]) continue;
+        for (int z = 0; z < 4; z++) {
+            if (!(g->zones & (1 << z))) continue;
+            int ov[30];
+            if (pcre_exec(g->re, g->ex, zones[z].p ? zones[z].p : "", zones[z].n, 0, 0, ov, 30) >= 0) {
+                mark[p] = 1; hb_push(out, (uint32_t)p); break;
+            }
+        }
+    }
+    /* sort this request's ids ascending, clear marks */
+    for (size_t i = first + 1; i < out->n; i++) {
+        uint32_t v = out->ids[i]; size_t j = i;
+        while (j > first && out->ids[j - 1] > v) { out->ids[j] = out->ids[j - 1]; j--; }
+        out->ids[j] = v;
+    }
+    for (size_t i = first; i < out->n; i++) mark[out->ids[i]] = 0;
+}
+
+static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdict *v, scratch_t *sc,
+                     uint8_t *mark, hitbuf_t *hits, uint32_t *nh) {
+    rq_t q; rq_init(&q, r, arena);
+    memset(v, 0, sizeof *v);
+    v->gen = c->gen; v->location_id = GM_NONE; v->upstream_id = GM_NONE; v->split_bucket = 0xFF; v->match_idx = 0xFF;
+    v->route_kind = GM_ROUTE_NONE; v->waf_mode = GM_WAF_OFF; *nh = 0;
+    sc_reset(sc);
+    int bad = 0, port_ssl = 0;
+    int sidx = find_server(c, r->port, r->flags & GM_REQ_HTTPS, q.host, &bad, &port_ssl);
+    if (sidx < 0 || ((r->flags & GM_REQ_HTTPS) && !port_ssl)) {
+        v->server_id = GM_NONE; v->action = GM_ACT_NO_LISTENER; v->status = 0; return;
+    }
+    v->server_id = (uint32_t)sidx;
+    if (bad || (port_ssl && !(r->flags & GM_REQ_HTTPS))) { v->action = GM_ACT_BAD_REQUEST; v->status = 400; return; }
+    srv_t *S = &c->srv[sidx];
+    ev_t E = {c, &q, sc, 0, NULL, NULL};
+    for (int i = 0; i < S->nifs; i++) {
+        sif_t *f = &S->ifs[i];
+        int hit = 0;
+        if (f->is_return_only) hit = 1;
+        else {
+            const char *vn = f->var; sv val = {"", 0};
+            if (vn[0] == '$') val = get_var(&E, vn + 1, (int)strlen(vn + 1));
+            if (f->op == 0) hit = val.n && !(val.n == 1 && val.p[0] == '0');
+            else if (f->op == 1) hit = sv_eq(val, f->val);
+            else if (f->op == 2) hit = !sv_eq(val, f->val);
+            else if (f->re) { int ov[30]; int m = pcre_exec(f->re, NULL, val.p ? val.p : "", val.n, 0, 0, ov, 30) >= 0; hit = (f->op == 3) ? m : !m; }
+        }
+        if (hit) {
+            v->action = (f->code >= 301 && f->code <= 308 && f->code != 304 && f->code != 305 && f->code != 306) ? GM_ACT_REDIRECT : GM_ACT_RETURN;
+            v->status = (uint32_t)f->code; return;
+        }
+    }
+    int a301 = 0;
+    int lid = find_location(c, S, q.uri, &a301);
+    if (lid < 0) { v->action = GM_ACT_NOT_FOUND; v->status = 404; return; }
+    v->location_id = (uint32_t)lid;
+    if (a301) { v->action = GM_ACT_AUTO_301; v->status = 301; return; }
+    loc_t *L = &c->loc[lid];
+    loc_t *F = L;   /* location that runs the content phase */
+    if (L->has_return && L->ret_code == 418 && L->err418) {
+        int pidx = -2, part = -2;
+        E.last_param = &pidx; E.last_part = &part;
+        sv target = eval_complex(&E, L->err418);
+        E.last_param = NULL; E.last_part = NULL;
+        if (part != -2) { v->route_kind = GM_ROUTE_SPLIT; v->split_bucket = part < 0 ? 0xFF : (uint8_t)part; }
+        else if (pidx != -2) { v->route_kind = GM_ROUTE_RULES; v->match_idx = pidx < 0 ? 0xFF : (uint8_t)pidx; }
+        if (target.n && target.p[0] == '@') {
+            int nl = find_named(c, S, target);
+            if (nl < 0) { v->action = GM_ACT_NOT_FOUND; v->status = 404; return; }
+            F = &c->loc[nl];
+        } else if (target.n == 0) {
+            v->action = GM_ACT_ERRPAGE; v->status = 302; return;
+        } else {
+            v->action = GM_ACT_UNSUPPORTED; v->status = 0; return;
+        }
+    } else if (L->has_return) {
+        v->action = (L->ret_code >= 301 && L->ret_code <= 308) ? GM_ACT_REDIRECT : GM_ACT_RETURN;
+        v->status = (uint32_t)L->ret_code; return;
+    } else if (L->has_proxy) {
+        v->route_kind = GM_ROUTE_PLAIN;
+    }
+    if (F->has_return && F != L) {
+        v->action = GM_ACT_RETURN; v->status = (uint32_t)F->ret_code; return;
+    }
+    if (!F->has_proxy) { v->action = GM_ACT_NOT_FOUND; v->status = 404; return; }
+    v->action = GM_ACT_PROXY; v->status = 0;
+    v->upstream_id = F->upstream_id < 0 ? GM_NONE : (uint32_t)F->upstream_id;
+    v->waf_mode = (uint16_t)F->waf_mode;
+    if (F->waf_mode != GM_WAF_OFF && c->nsig) {
+        size_t before = hits->n;
+        waf_scan(c, &q, mark, hits);
+        *nh = (uint32_t)(hits->n - before);
+        v->n_hits = (uint16_t)*nh;
+        if (*nh && F->waf_mode == GM_WAF_BLOCK) { v->action = GM_ACT_BLOCK; v->status = 403; }
+    }
+}
+
+typedef struct {
+    orc_ctx *c; const gm_req *reqs; const uint8_t *arena; gm_verdict *out;
+    size_t lo, hi; hitbuf_t hits;
+} job_t;
+
+static void *worker(void *arg) {
+    job_t *j = arg;
+    scratch_t sc = {NULL};
+    uint8_t *mark = calloc(j->c->nsig + 1, 1);
+    for (size_t i = j->lo; i < j->hi; i++) {
+        uint32_t nh;
+        eval_one(j->c, &j->reqs[i], j->arena, &j->out[i], &sc, mark, &j->hits, &nh);
+    }
+    sc_reset(&sc); free(sc.head); free(mark);
+    return NULL;
+}
+
+/* Evaluate n requests.  Hit ids are laid out exactly as libgpumatch lays them out: request
+ * order, ascending rule id, first_hit_off = running count.  Returns total hits, or -1 if
+ * hit_cap is too small (hit_ids then untouched beyond hit_cap). */
+int64_t orc_match(orc_ctx *c, const gm_req *reqs, const uint8_t *arena, uint32_t n, gm_verdict *out,
+                  uint32_t *hit_ids, size_t hit_cap, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if ((uint32_t)nthreads > n) nthreads = n ? (int)n : 1;
+    job_t *jobs = calloc(nthreads, sizeof(job_t));
+    pthread_t *th = calloc(nthreads, sizeof(pthread_t));
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t].c = c; jobs[t].reqs = reqs; jobs[t].arena = arena; jobs[t].out = out;
+        jobs[t].lo = (size_t)n * t / nthreads; jobs[t].hi = (size_t)n * (t + 1) / nthreads;
+        if (nthreads > 1) pthread_create(&th[t], NULL, worker, &jobs[t]); else worker(&jobs[t]);
+    }
+    if (nthreads > 1) for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    size_t off = 0; int64_t rc = 0;
+    for (int t = 0; t < nthreads; t++) {
+        size_t k = 0;
+        for (size_t i = jobs[t].lo; i < jobs[t].hi; i++) {
+            out[i].first_hit_off = out[i].n_hits ? (uint32_t)off : 0;
+            for (uint32_t h = 0; h < out[i].n_hits; h++, k++, off++) {
+                if (off < hit_cap) hit_ids[off] = jobs[t].hits.ids[k];
+                else rc = -1;
+            }
+        }
+        free(jobs[t].hits.ids);
+    }
+    free(jobs); free(th);
+    return rc < 0 ? -1 : (int64_t)off;
+}
+
+/* Regex probe used by tests to pin PCRE semantics: returns 1 match / 0 no match / -1 error */
+int orc_pcre_match(const char *pat, int caseless, const char *subj, int n) {
+    pcre *r = re_compile(pat, caseless);
+    if (!r) return -1;
+    int ov[30];
+    int m = pcre_exec(r, NULL, subj, n, 0, 0, ov, 30);
+    return m >= 0 ? 1 : 0;
+}

@@ -1,0 +1,176 @@
+"""Generate the committed golden fixtures from the reference's own test data and tests.
+
+Run in the build container (reads /root/reference, writes tests/golden/*.json).  The GPU box
+never runs this; it only reads the JSON.  Nothing here is reference *source*: the fixtures are
+the reference's test inputs (YAML under tests/data, Go test structs) and the known answers its
+tests assert, transcribed as data.
+
+  advanced_routing.json   tests/data/virtual-server-advanced-routing/*.yaml +
+                          tests/suite/test_virtual_server_advanced_routing.py:10-93 (expected backend)
+  split_traffic.json      tests/data/virtual-server-split-traffic/standard/virtual-server.yaml +
+                          tests/suite/test_virtual_server_split_traffic.py:46-66 (ratio +-0.2)
+  match_values.json       docs/virtualserver-and-virtualserverroute.md:264-271 (value semantics)
+  confgen_structs.json    internal/configs/virtualserver_test.go:1018-1399,
+                          internal/configs/ingress_test.go:124-205 (expected typed configs)
+  examples.json           examples/complete-example/cafe-ingress.yaml,
+                          examples-of-custom-resources/{advanced-routing,traffic-splitting}/*.yaml,
+                          examples/mergeable-ingress-types/{cafe-master,coffee-minion,tea-minion}.yaml
+"""
+
+import json
+import os
+
+import yaml
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def y(path):
+    with open(os.path.join(REF, path)) as f:
+        return [d for d in yaml.safe_load_all(f) if d]
+
+
+def dump(name, obj):
+    with open(os.path.join(OUT, name), "w") as f:
+        json.dump(obj, f, indent=1, sort_keys=True)
+    print("wrote", name)
+
+
+def main():
+    d = "tests/data/virtual-server-advanced-routing/"
+    vs = {
+        "header": y(d + "standard/virtual-server.yaml")[0],
+        "argument": y(d + "virtual-server-argument.yaml")[0],
+        "cookie": y(d + "virtual-server-cookie.yaml")[0],
+        "variable": y(d + "virtual-server-variable.yaml")[0],
+        "complex": y(d + "virtual-server-complex.yaml")[0],
+    }
+    B1, B3, B4 = "backend1-future", "backend3-deprecated", "backend4-stable"
+    cases = [
+        # test_flow_with_header
+        ("header", dict(headers=[["x-version", "future"]]), B1),
+        ("header", dict(headers=[["x-version", "deprecated"]]), B3),
+        ("header", dict(headers=[["x-version-invalid", "deprecated"]]), B4),
+        # test_flow_with_argument
+        ("argument", dict(args="arg1=v1"), B1),
+        ("argument", dict(args="arg1=v2"), B3),
+        ("argument", dict(args="argument1=v1"), B4),
+        # test_flow_with_cookie (requests sends "Cookie: user=...")
+        ("cookie", dict(headers=[["Cookie", "user=some"]]), B1),
+        ("cookie", dict(headers=[["Cookie", "user=bad"]]), B3),
+        ("cookie", dict(headers=[["Cookie", "user=anonymous"]]), B4),
+        # test_flow_with_variable: values get / post vs methods GET POST PUT (case-insensitive)
+        ("variable", dict(method="GET"), B1),
+        ("variable", dict(method="POST"), B3),
+        ("variable", dict(method="PUT"), B4),
+        # test_flow_with_complex_conditions
+        ("complex", dict(method="GET", args="arg1=v1", headers=[["x-version", "future"], ["Cookie", "user=some"]]), B1),
+        ("complex", dict(method="POST", args="arg1=v2", headers=[["x-version", "deprecated"], ["Cookie", "user=bad"]]), B3),
+        ("complex", dict(method="GET", args="arg1=v2", headers=[["x-version", "deprecated"], ["Cookie", "user=bad"]]), B4),
+    ]
+    dump("advanced_routing.json", {
+        "source": "tests/suite/test_virtual_server_advanced_routing.py:10-93",
+        "host": "virtual-server-adv-routing.example.com", "uri": "/backends",
+        "virtual_servers": vs,
+        "cases": [{"vs": v, "request": r, "expect_upstream": u} for v, r, u in cases],
+    })
+
+    sp = y("tests/data/virtual-server-split-traffic/standard/virtual-server.yaml")[0]
+    dump("split_traffic.json", {"source": "tests/suite/test_virtual_server_split_traffic.py:46-66",
+                                "virtual_server": sp, "tolerance": 0.2})
+
+    # docs/virtualserver-and-virtualserverroute.md:264-271: (value, subject, matches)
+    mv = [
+        ("john", "john", True), ("john", "John", True), ("john", "JOHN", True), ("john", "bob", False),
+        ("!john", "bob", True), ("!john", "anything", True), ("!john", "", True), ("!john", "John", False),
+        ("~^yes", "yes", True), ("~^yes", "yes123", True), ("~^yes", "YES", False), ("~^yes", "noyes", False),
+        ("!~^yes", "YES", True), ("!~^yes", "Yes123", True), ("!~^yes", "noyes", True), ("!~^yes", "yes", False),
+        ("~*no$", "no", True), ("~*no$", "123no", True), ("~*no$", "123NO", True), ("~*no$", "nope", False),
+    ]
+    dump("match_values.json", {"source": "docs/virtualserver-and-virtualserverroute.md:264-271",
+                               "cases": [{"value": a, "subject": b, "match": c} for a, b, c in mv]})
+
+    # Go expected structs (transcribed from virtualserver_test.go / ingress_test.go)
+    conds = [{"header": "x-version"}, {"cookie": "user"}, {"argument": "answer"}, {"variable": "$request_method"}]
+    vals = [["v1", "john", "yes", "GET"], ["v2", "paul", "no", "POST"]]
+    srcs = ["$http_x_version", "$cookie_user", "$arg_answer", "$request_method"]
+    rules_maps = []
+    for i in range(2):
+        for j in range(4):
+            ok = "1" if j == 3 else f"$vs_default_cafe_rules_1_match_{i}_cond_{j + 1}"
+            rules_maps.append({"Source": srcs[j], "Variable": f"$vs_default_cafe_rules_1_match_{i}_cond_{j}",
+                               "Parameters": [{"Value": f'"{vals[i][j]}"', "Result": ok},
+                                              {"Value": "default", "Result": "0"}]})
+    rules_maps.append({"Source": "$vs_default_cafe_rules_1_match_0_cond_0$vs_default_cafe_rules_1_match_1_cond_0",
+                       "Variable": "$vs_default_cafe_rules_1",
+                       "Parameters": [{"Value": "~^1", "Result": "@rules_1_match_0"},
+                                      {"Value": "~^01", "Result": "@rules_1_match_1"},
+                                      {"Value": "default", "Result": "@rules_1_default"}]})
+    dump("confgen_structs.json", {
+        "split_route": {  # virtualserver_test.go:1018-1079
+            "route": {"path": "/", "splits": [{"weight": 90, "upstream": "coffee-v1"},
+                                              {"weight": 10, "upstream": "coffee-v2"}]},
+            "index": 1,
+            "expected": {
+                "SplitClient": {"Source": "$request_id", "Variable": "$vs_default_cafe_splits_1",
+                                "Distributions": [{"Weight": "90%", "Value": "@splits_1_split_0"},
+                                                  {"Weight": "10%", "Value": "@splits_1_split_1"}]},
+                "Locations": [{"Path": "@splits_1_split_0", "ProxyPass": "http://vs_default_cafe_coffee-v1"},
+                              {"Path": "@splits_1_split_1", "ProxyPass": "http://vs_default_cafe_coffee-v2"}],
+                "InternalRedirectLocation": {"Path": "/", "Destination": "$vs_default_cafe_splits_1"}}},
+        "rules_route": {  # virtualserver_test.go:1081-1291
+            "route": {"path": "/", "rules": {"conditions": conds,
+                                             "matches": [{"values": vals[0], "upstream": "coffee-v1"},
+                                                         {"values": vals[1], "upstream": "coffee-v2"}],
+                                             "defaultUpstream": "tea"}},
+            "index": 1,
+            "expected": {
+                "Maps": rules_maps,
+                "Locations": [{"Path": "@rules_1_match_0", "ProxyPass": "http://vs_default_cafe_coffee-v1"},
+                              {"Path": "@rules_1_match_1", "ProxyPass": "http://vs_default_cafe_coffee-v2"},
+                              {"Path": "@rules_1_default", "ProxyPass": "http://vs_default_cafe_tea"}],
+                "InternalRedirectLocation": {"Path": "/", "Destination": "$vs_default_cafe_rules_1"}}},
+        "value_for_map": [  # virtualserver_test.go:1293-1355
+            ["default", "\\default", False], ["!default", "\\default", True], ["hostnames", "\\hostnames", False],
+            ["include", "\\include", False], ["volatile", "\\volatile", False], ["abc", '"abc"', False],
+            ["!abc", '"abc"', True], ["", '""', False], ["!", '""', True]],
+        "params_for_map": [  # virtualserver_test.go:1357-1399
+            ["abc", "1", [{"Value": '"abc"', "Result": "1"}, {"Value": "default", "Result": "0"}]],
+            ["!abc", "1", [{"Value": '"abc"', "Result": "0"}, {"Value": "default", "Result": "1"}]]],
+        "source_names": [  # virtualserver_test.go:1401-1437
+            [{"header": "x-version"}, "$http_x_version"], [{"cookie": "mycookie"}, "$cookie_mycookie"],
+            [{"argument": "arg"}, "$arg_arg"], [{"variable": "$request_method"}, "$request_method"]],
+        "cafe_ingress": {  # ingress_test.go:124-253
+            "ingress": {"metadata": {"name": "cafe-ingress", "namespace": "default",
+                                     "annotations": {"kubernetes.io/ingress.class": "nginx"}},
+                        "spec": {"tls": [{"hosts": ["cafe.example.com"], "secretName": "cafe-secret"}],
+                                 "rules": [{"host": "cafe.example.com", "http": {"paths": [
+                                     {"path": "/coffee", "backend": {"serviceName": "coffee-svc", "servicePort": "80"}},
+                                     {"path": "/tea", "backend": {"serviceName": "tea-svc", "servicePort": "80"}}]}}]}},
+            "endpoints": {"coffee-svc80": ["10.0.0.1:80"], "tea-svc80": ["10.0.0.2:80"]},
+            "pems": {"cafe.example.com": "/etc/nginx/secrets/default-cafe-secret"},
+            "expected": {
+                "upstream_names": ["default-cafe-ingress-cafe.example.com-coffee-svc-80",
+                                   "default-cafe-ingress-cafe.example.com-tea-svc-80"],
+                "upstream_servers": [[["10.0.0.1", "80"]], [["10.0.0.2", "80"]]],
+                "server": {"Name": "cafe.example.com", "SSL": True,
+                           "SSLCertificate": "/etc/nginx/secrets/default-cafe-secret",
+                           "Ports": [80], "SSLPorts": [443], "SSLRedirect": True, "StatusZone": "cafe.example.com"},
+                "locations": [["/coffee", "default-cafe-ingress-cafe.example.com-coffee-svc-80"],
+                              ["/tea", "default-cafe-ingress-cafe.example.com-tea-svc-80"]]}},
+    })
+
+    ex = {
+        "cafe_ingress": y("examples/complete-example/cafe-ingress.yaml")[0],
+        "advanced_routing_vs": y("examples-of-custom-resources/advanced-routing/cafe-virtual-server.yaml")[0],
+        "traffic_splitting_vs": y("examples-of-custom-resources/traffic-splitting/cafe-virtual-server.yaml")[0],
+        "mergeable_master": y("examples/mergeable-ingress-types/cafe-master.yaml")[0],
+        "mergeable_minions": [y("examples/mergeable-ingress-types/coffee-minion.yaml")[0],
+                              y("examples/mergeable-ingress-types/tea-minion.yaml")[0]],
+    }
+    dump("examples.json", ex)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,68 @@
+"""ctypes binding of oracle/liboracle.so (CPU oracle).  Test / baseline infrastructure only."""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "liboracle.so")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = ctypes.CDLL(LIB)
+        L.orc_create.restype = ctypes.c_void_p
+        L.orc_create.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
+        L.orc_error.restype = ctypes.c_char_p
+        L.orc_match.restype = ctypes.c_int64
+        L.orc_match.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        L.orc_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_murmur2.restype = ctypes.c_uint32
+        L.orc_murmur2.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.orc_pcre_match.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+class Oracle:
+    def __init__(self, blob: bytes, gen: int = 1):
+        self._blob = blob
+        self.h = lib().orc_create(blob, len(blob), gen)
+        if not self.h:
+            raise RuntimeError("oracle: " + lib().orc_error().decode())
+        info = np.zeros(4, dtype=np.uint32)
+        lib().orc_info(self.h, info.ctypes.data)
+        self.n_servers, self.n_locations, self.n_upstreams, self.n_sigs = (int(x) for x in info)
+
+    def match(self, reqs: np.ndarray, arena: np.ndarray, nthreads: int = 0, hit_cap: int | None = None):
+        from gpumatch.records import VERDICT_DTYPE
+        n = len(reqs)
+        out = np.zeros(n, dtype=VERDICT_DTYPE)
+        cap = hit_cap if hit_cap is not None else max(1024, 4 * n)
+        hits = np.zeros(cap, dtype=np.uint32)
+        reqs = np.ascontiguousarray(reqs)
+        arena = np.ascontiguousarray(arena) if len(arena) else np.zeros(16, np.uint8)
+        nt = nthreads or min(os.cpu_count() or 1, 16)
+        tot = lib().orc_match(self.h, reqs.ctypes.data, arena.ctypes.data, n, out.ctypes.data,
+                              hits.ctypes.data, cap, nt)
+        if tot < 0:
+            raise RuntimeError("oracle hit buffer too small")
+        return out, hits[:tot]
+
+
+def murmur2(b: bytes) -> int:
+    return int(lib().orc_murmur2(b, len(b)))
+
+
+def pcre_match(pat: str, subj: bytes, caseless: bool = False) -> int:
+    return int(lib().orc_pcre_match(pat.encode(), 1 if caseless else 0, subj, len(subj)))

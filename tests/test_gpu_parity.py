@@ -1,0 +1,190 @@
+"""Parity of the gfx950 path (libgpumatch.so kernels) with the CPU oracle: bit-exact verdicts and
+hit-id lists on the same seeded inputs, plus the reference's known answers run on the GPU."""
+
+import numpy as np
+import pytest
+
+from gpumatch import blob, engine, records, sigs, workloads
+from helpers import assert_verdicts_equal, golden, kat_request, upstream_table, vs_blob
+from oracle_py import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import torch
+    assert torch.cuda.is_available(), "GPU test without a GPU"
+    return engine.Engine(0)
+
+
+def run_both(eng, b, reqs, arena, gen=5, hit_cap=None):
+    eng.load(b, gen)
+    got, gh = eng.match_host(reqs, arena, hit_cap)
+    exp, eh = Oracle(b, gen).match(reqs, arena)
+    return got, gh, exp, eh
+
+
+def test_c1_cafe_parity(eng):
+    reqs, arena = records.gen_c1(300_000)
+    got, gh, exp, eh = run_both(eng, workloads.c1_blob(), reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "C1")
+    assert len(set(exp["action"].tolist())) >= 4   # the sample exercises several verdict kinds
+
+
+def test_c2_advanced_routing_parity(eng):
+    reqs, arena = records.gen_c2(100_000)
+    got, gh, exp, eh = run_both(eng, workloads.c2_blob(), reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "C2")
+    assert (exp["route_kind"] == 2).any() and (exp["route_kind"] == 3).any()
+    assert (exp["match_idx"] != 0xFF).any() and (exp["split_bucket"] == 1).any()
+
+
+def test_c5_mergeable_parity(eng):
+    reqs, arena = workloads.gen_c5(200_000)
+    got, gh, exp, eh = run_both(eng, workloads.c5_blob(), reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "C5")
+
+
+@pytest.mark.parametrize("mode", ["block", "monitoring", "off"])
+def test_c4_waf_parity_small_set(eng, mode):
+    ss = workloads.c4_sigset(800, 200)
+    reqs, arena = records.gen_c4(20_000, ss, plant_rate=0.05)
+    got, gh, exp, eh = run_both(eng, workloads.c4_blob(ss, mode), reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, f"C4-{mode}")
+    if mode != "off":
+        assert len(eh) > 500
+    else:
+        assert len(eh) == 0
+
+
+def test_c4_waf_parity_10k_rules(eng):
+    ss = workloads.c4_sigset()
+    reqs, arena = records.gen_c4(6_000, ss, plant_rate=0.05)
+    got, gh, exp, eh = run_both(eng, workloads.c4_blob(ss), reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "C4-10k")
+    assert (exp["action"] == 6).sum() > 100
+
+
+def test_waf_edge_cases(eng):
+    rules = [sigs.Rule("lit", True, "uahb", b"evil"), sigs.Rule("lit", False, "b", b"CaseSensitive"),
+             sigs.Rule("lit", True, "u", b"/tea/x"), sigs.Rule("re", True, "ah", r"sel\s*ect\d+"),
+             sigs.Rule("re", False, "b", r"^start"), sigs.Rule("re", False, "b", r"end$"),
+             sigs.Rule("re", False, "uahb", r"[0-9]{3}x"),           # no >= 4-byte factor: always-run
+             sigs.Rule("lit", True, "h", b"evil"),                    # duplicate literal, other zone
+             sigs.Rule("re", False, "a", r"(a)\1")]                   # PCRE-only: rejected
+    b = workloads.c4_blob(sigs.SigSet(rules))
+    items = [
+        {"host": "cafe.example.com", "uri": "/tea/x", "https": True, "body": b"xxEVILxx"},
+        {"host": "cafe.example.com", "uri": "/tea/a", "https": True, "body": b"casesensitive CaseSensitive"},
+        {"host": "cafe.example.com", "uri": "/tea/a", "https": True, "body": b"casesensitive"},
+        {"host": "cafe.example.com", "uri": "/tea/a", "https": True, "args": "q=SEL  ECT42"},
+        {"host": "cafe.example.com", "uri": "/tea/a", "https": True, "body": b"start...end\n"},
+        {"host": "cafe.example.com", "uri": "/tea/a", "https": True, "body": b"x start end\n\n"},
+        {"host": "cafe.example.com", "uri": "/tea/ev", "args": "il=1", "https": True},   # no cross-zone match
+        {"host": "cafe.example.com", "uri": "/coffee", "https": True, "headers": [("X-A", "123x evil")]},
+        {"host": "cafe.example.com", "uri": "/tea", "https": False, "body": b"evil"},      # redirected: no WAF
+        {"host": "cafe.example.com", "uri": "/tea/", "https": True, "body": b"ev"},
+        {"host": "cafe.example.com", "uri": "/tea/q", "https": True, "body": b"evi"},     # tail of arena
+    ]
+    reqs, arena = records.from_dicts(items)
+    got, gh, exp, eh = run_both(eng, b, reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "edge")
+    assert got[0]["n_hits"] == 2 and got[1]["n_hits"] == 1 and got[2]["n_hits"] == 0
+    assert got[6]["n_hits"] == 0 and got[8]["n_hits"] == 0
+
+
+def test_e2e_kats_on_gpu(eng):
+    adv = golden("advanced_routing.json")
+    for case in adv["cases"]:
+        vs = adv["virtual_servers"][case["vs"]]
+        b = vs_blob([vs])
+        eng.load(b, 1)
+        reqs, arena = records.from_dicts([kat_request(adv["host"], adv["uri"], case["request"])])
+        v, _ = eng.match_host(reqs, arena)
+        ups = upstream_table(b)
+        assert v[0]["action"] == 0
+        assert ups[v[0]["upstream_id"]] == f"vs_default_{vs['metadata']['name']}_{case['expect_upstream']}", case
+
+
+def test_match_values_on_gpu(eng):
+    from test_oracle import _value_vs
+    for case in golden("match_values.json")["cases"]:
+        b = vs_blob([_value_vs(case["value"])])
+        eng.load(b, 1)
+        reqs, arena = records.from_dicts([{"host": "mv.example.com", "uri": "/x",
+                                           "headers": [("X-V", case["subject"])]}])
+        v, _ = eng.match_host(reqs, arena)
+        ups = upstream_table(b)
+        assert ups[v[0]["upstream_id"]] == ("vs_default_mv_m" if case["match"] else "vs_default_mv_d"), case
+
+
+def test_location_semantics_on_gpu(eng):
+    from test_oracle import test_location_lookup_semantics  # noqa: F401 (same config, GPU vs oracle)
+    conf = """
+    http {
+      upstream u1 { server 1.1.1.1; }
+      upstream u2 { server 1.1.1.2; }
+      server {
+        listen 80 default_server;
+        server_name t.example.com *.wild.example.com .dot.example.com www.tail.*;
+        if ($http_x_forwarded_proto = 'http') { return 301 https://$host$request_uri; }
+        location = /exact { proxy_pass http://u1; }
+        location /tea/ { proxy_pass http://u1; }
+        location /img/ { return 403; }
+        location ^~ /static { proxy_pass http://u2; }
+        location ~ \\.php$ { proxy_pass http://u2; }
+        location ~* \\.JPG$ { proxy_pass http://u1; }
+        location / { proxy_pass http://u1; }
+      }
+      server { listen 80; server_name other.example.com a.wild.example.com; location / { return 404; } }
+    }"""
+    b = blob.make_blob(conf, {})
+    uris = ["/exact", "/exact/", "/tea", "/tea/x", "/img", "/static/a.php", "/a.php", "/b.jpg", "/b.jpgx",
+            "/img/x", "", "/t\x00"]
+    hosts = ["t.example.com", "x.wild.example.com", "a.wild.example.com", "dot.example.com", "z.dot.example.com",
+             "www.tail.org", "www.tail.", "other.example.com", "[::1]:80", "T.EXAMPLE.COM.", "x/y", ".lead.example.com"]
+    items = [{"host": h, "uri": u} for h in hosts for u in uris]
+    items += [{"host": "t.example.com", "uri": "/a", "headers": [("X-Forwarded-Proto", "http")]},
+              {"host": "t.example.com", "uri": "/a", "headers": [("X-Forwarded-Proto", "HTTP")]}]
+    reqs, arena = records.from_dicts(items)
+    got, gh, exp, eh = run_both(eng, b, reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "locations")
+
+
+def test_counters(eng):
+    ss = workloads.c4_sigset(400, 100)
+    reqs, arena = records.gen_c4(10_000, ss, plant_rate=0.1)
+    b = workloads.c4_blob(ss, "monitoring")
+    eng.load(b, 3)
+    eng.counters_reset()
+    got, gh = eng.match_host(reqs, arena)
+    c = eng.counters()
+    st = eng.stats()
+    nl = st["n_locations"]
+    loc = got["location_id"][got["location_id"] != 0xFFFFFFFF]
+    assert np.array_equal(c[:nl], np.bincount(loc, minlength=nl))
+    assert np.array_equal(c[nl:], np.bincount(gh, minlength=st["n_sigs"]))
+
+
+def test_hit_cap_overflow_reported(eng):
+    ss = workloads.c4_sigset(200, 50)
+    reqs, arena = records.gen_c4(5_000, ss, plant_rate=0.5)
+    eng.load(workloads.c4_blob(ss), 3)
+    with pytest.raises(engine.GmError) as ei:
+        eng.match_host(reqs, arena, hit_cap=10)
+    assert ei.value.code == engine.GM_E_OVERFLOW
+
+
+def test_empty_and_generation_swap(eng):
+    eng.load(workloads.c1_blob(), 9)
+    reqs, arena = records.from_dicts([])
+    v, h = eng.match_host(reqs, arena)
+    assert len(v) == 0
+    reqs, arena = records.gen_c1(1000)
+    v1, _ = eng.match_host(reqs, arena)
+    assert (v1["gen"] == 9).all()
+    with pytest.raises(engine.GmError):
+        eng.load(b"GMB1\x00", 10)
+    v2, _ = eng.match_host(reqs, arena)
+    assert np.array_equal(v1, v2)

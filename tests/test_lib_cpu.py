@@ -1,0 +1,123 @@
+"""libgpumatch.so on the CPU: it loads, exports every symbol include/*.h declares, and its
+generation compiler (host code) behaves -- no classification calls without a GPU."""
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from gpumatch import engine, sigs, workloads
+from oracle_py import pcre_match
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared(header):
+    txt = open(os.path.join(ROOT, "include", header)).read()
+    return set(re.findall(r"^\s*[\w\s\*]+?\b(gm_\w+)\s*\(", txt, flags=re.M))
+
+
+def test_exports_every_declared_symbol():
+    L = ctypes.CDLL(engine.LIB_PATH)
+    syms = _declared("gpumatch.h") | _declared("gpumatch_debug.h")
+    assert set(engine.EXPORTS) <= syms
+    for s in sorted(syms):
+        assert hasattr(L, s), s
+    assert L.gm_abi_version() == 1
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return engine.Engine(compile_only=True)
+
+
+def test_compile_cafe(eng):
+    eng.load(workloads.c1_blob(), 7)
+    s = eng.stats()
+    assert s["gen"] == 7 and s["n_servers"] == 3 and s["n_locations"] == 4 and s["n_upstreams"] == 2
+    assert s["n_rejected_other"] == 0 and s["n_rejected_pcre"] == 0
+
+
+def test_compile_vs_routes(eng):
+    eng.load(workloads.c2_blob(), 1)
+    s = eng.stats()
+    assert s["n_routes_rules"] == 3 and s["n_routes_split"] == 1 and s["n_rejected_other"] == 0
+
+
+def test_bad_blob_keeps_previous_generation(eng):
+    eng.load(workloads.c1_blob(), 11)
+    with pytest.raises(engine.GmError):
+        eng.load(b"GMB1garbage", 12)
+    assert eng.stats()["gen"] == 11
+    from gpumatch import blob
+    with pytest.raises(engine.GmError):
+        eng.load(blob.make_blob("http { server { listen 80; ", {}), 13)
+    assert eng.stats()["gen"] == 11
+
+
+def test_pcre_only_rules_rejected_and_counted(eng):
+    rules = [sigs.Rule("re", False, "u", p) for p in
+             [r"(a)\1", r"foo(?=bar)", r"(?<!x)abcd", r"a++b", r"(?>abc)", r"ab\Kcd", r"abcd"]]
+    rules.append(sigs.Rule("lit", True, "u", b"abcdef"))
+    b = workloads.c4_blob(sigs.SigSet(rules))
+    eng.load(b, 2)
+    s = eng.stats()
+    assert s["n_rejected_pcre"] == 6
+    assert s["n_sig_regex"] == 1 and s["n_sig_literals"] == 1 and s["n_sigs"] == 8
+
+
+REGEX_CASES = [
+    (r"union\s+select", False), (r"^/api/v[0-9]+/", False), (r"\.php$", False), (r"(?i)select.{0,8}from", False),
+    (r"<script[^>]{0,16}on[a-z]{2,8}\s*=", True), (r"(abc|abd|xyz)[a-z0-9]+--", False), (r"a$", False),
+    (r"^$", False), (r"x*", False), (r"[^a-c]+z", True), (r"\d{3}-\d{2}", False), (r"(?s)a.b", False),
+    (r"colou?r", True), (r"a|^b|c$", False), (r"[\w.-]+@[\w-]+\.com", False), (r"\x41\x42", False),
+    (r"a{2,}b{0,1}c{3}", False), (r"[]a]", False), (r"[a\-z]", False), (r"a\.b\*c", False),
+]
+
+
+def test_regex_dfa_matches_pcre_on_random_subjects():
+    """The engine's DFA compiler agrees with PCRE 8.39 (the library nginx links)."""
+    L = ctypes.CDLL(engine.LIB_PATH)
+    L.gm_debug_regex.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
+    rng = np.random.default_rng(3)
+    alpha = np.frombuffer(b"abcxyzABCz019-_.@ \t\n\x0b<>=/uniosetlcfrmphSELECTFROM*", dtype=np.uint8)
+    seeds = [b"union  select", b"/api/v2/x", b"a.php", b"SELECT x FROM", b"<script a=1 onload =", b"abd9--",
+             b"a\n", b"", b"zz", b"color", b"123-45", b"a\nb", b"b", b"ab@c-d.com", b"AB", b"aabccc",
+             b"]", b"-", b"a.b*c"]
+    for pat, ci in REGEX_CASES:
+        subjects = list(seeds)
+        for _ in range(300):
+            k = int(rng.integers(0, 24))
+            subjects.append(bytes(alpha[rng.integers(0, len(alpha), k)]))
+        for s in subjects:
+            got = L.gm_debug_regex(pat.encode(), 1 if ci else 0, s, len(s))
+            assert got >= 0, (pat, got)
+            assert got == pcre_match(pat, s, ci), (pat, ci, s)
+
+
+def test_regex_factors():
+    L = ctypes.CDLL(engine.LIB_PATH)
+    L.gm_debug_regex_factors.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
+    buf = ctypes.create_string_buffer(4096)
+
+    def f(p):
+        m = L.gm_debug_regex_factors(p.encode(), 0, buf, 4096)
+        return m, sorted(x for x in buf.value.decode().split("\n") if x)
+    assert f(r"union\s+select") == (6, ["select"])
+    assert f(r"(abcd|efgh)x") == (5, ["abcdx", "efghx"])
+    assert f(r"SeLect.{0,8}from")[1] == ["select"]
+    assert f(r"[a-z]+\d+")[0] == 0
+    for p in [r"(a)\1", r"x(?=y)"]:
+        assert L.gm_debug_regex_factors(p.encode(), 0, buf, 4096) < 0
+
+
+def test_c4_signature_set_compiles():
+    ss = workloads.c4_sigset(800, 200)
+    e = engine.Engine(compile_only=True)
+    e.load(workloads.c4_blob(ss), 3)
+    s = e.stats()
+    assert s["n_sigs"] == 1000 and s["n_sig_literals"] == 800 and s["n_sig_regex"] == 200
+    assert s["n_rejected_pcre"] == 0 and s["n_rejected_other"] == 0
+    assert s["n_sig_regex_always"] == 0
