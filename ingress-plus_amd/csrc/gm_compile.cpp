@@ -608,9 +608,39 @@ bool parse_sigs(const char *t, size_t n, std::vector<SigRule> &out) {
     return true;
 }
 
-uint32_t load4(const std::string &s) {
-    return (uint32_t)(uint8_t)s[0] | (uint32_t)(uint8_t)s[1] << 8 | (uint32_t)(uint8_t)s[2] << 16 |
-           (uint32_t)(uint8_t)s[3] << 24;
+uint32_t load4(const std::string &s, size_t o = 0) {
+    return (uint32_t)(uint8_t)s[o] | (uint32_t)(uint8_t)s[o + 1] << 8 | (uint32_t)(uint8_t)s[o + 2] << 16 |
+           (uint32_t)(uint8_t)s[o + 3] << 24;
+}
+
+// Key window choice: the prefilter's candidate rate is dominated by 4-grams that benign
+// traffic really contains ("from", "into", "kind", "upda"...), so each literal is keyed on its
+// rarest window under an English / HTTP bigram-frequency model (any window is correct:
+// verification re-checks the whole literal at pos - key_off).
+int bigram_commonness(uint8_t a, uint8_t b) {
+    if (a >= 'A' && a <= 'Z') a |= 0x20;
+    if (b >= 'A' && b <= 'Z') b |= 0x20;
+    static const char *top = "thheineranreonatenndtiesortesofedisitalarsttontngsehaasouioleveco"
+                             "medehiriroicneearacelichllbemasiomurelwhlaotraelsnc";
+    const bool la = a >= 'a' && a <= 'z', lb = b >= 'a' && b <= 'z';
+    if (la && lb) {
+        for (const char *p = top; p[0] && p[1]; p += 2) if (p[0] == a && p[1] == b) return 4;
+        return 2;
+    }
+    if ((la && b == ' ') || (a == ' ' && lb)) return 3;
+    if ((a >= '0' && a <= '9') && (b >= '0' && b <= '9')) return 2;
+    if (la || lb) return (strchr("/.-_=&:,;", la ? b : a) && (la ? b : a)) ? 2 : 1;
+    return 0;
+}
+
+uint16_t rarest_window(const std::string &p) {
+    int best = 1 << 30; uint16_t bo = 0;
+    for (size_t o = 0; o + 4 <= p.size(); o++) {
+        int s = 0;
+        for (int k = 0; k < 3; k++) s += bigram_commonness((uint8_t)p[o + k], (uint8_t)p[o + k + 1]);
+        if (s < best) { best = s; bo = (uint16_t)o; }
+    }
+    return bo;
 }
 
 }  // namespace
@@ -854,8 +884,9 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         if (g.lit) {
             if (g.pat.size() < 4 || g.pat.size() > 0xFFFF) { st.n_rejected_other++; continue; }
             std::string b = g.nocase ? lower(g.pat) : g.pat;
-            LitE e{fold4(load4(g.pat)), DLit{(uint32_t)r, 0, (uint16_t)b.size(),
-                                             (uint8_t)(g.nocase ? LIT_NOCASE : 0), (uint8_t)g.zones, 0}, b};
+            uint16_t ko = rarest_window(g.pat);
+            LitE e{fold4(load4(g.pat, ko)), DLit{(uint32_t)r, 0, (uint16_t)b.size(),
+                                                 (uint8_t)(g.nocase ? LIT_NOCASE : 0), (uint8_t)g.zones, ko, 0}, b};
             lits.push_back(e);
             st.n_sig_literals++;
         } else {
@@ -866,16 +897,31 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             }
             int d = C.add_dfa(ri.dfa);
             uint32_t ridx = (uint32_t)sregex.size();
-            bool alw = ri.min_factor < 4;
-            sregex.push_back(DSigRegex{(uint32_t)d, (uint32_t)r, (uint32_t)g.zones, alw ? 1u : 0u});
+            DSigRegex sr{(uint32_t)d, 0, (uint32_t)r, (uint16_t)g.zones, (uint16_t)RXM_TRIGGER};
             st.n_sig_regex++;
-            if (alw) { always.push_back(ridx); st.n_sig_regex_always++; }
-            else
-                for (auto &f : ri.factors) {
-                    LitE e{fold4(load4(f)), DLit{ridx, 0, (uint16_t)f.size(), (uint8_t)(LIT_NOCASE | LIT_TRIGGER),
-                                                 (uint8_t)g.zones, 0}, f};
+            if (ri.prefix_mode) {
+                sr.mode = RXM_PREFIX;
+                sr.adfa = (uint32_t)C.add_dfa(ri.anchored);
+                for (auto &f : ri.prefix) {
+                    uint16_t ko = rarest_window(f);
+                    LitE e{fold4(load4(f, ko)), DLit{ridx, 0, (uint16_t)f.size(),
+                                                     (uint8_t)(LIT_NOCASE | LIT_TRIGGER | LIT_PREFIX),
+                                                     (uint8_t)g.zones, ko, 0}, f};
                     lits.push_back(e);
                 }
+            } else if (ri.min_factor < 4) {
+                sr.mode = RXM_ALWAYS;
+                always.push_back(ridx);
+                st.n_sig_regex_always++;
+            } else {
+                for (auto &f : ri.factors) {
+                    uint16_t ko = rarest_window(f);
+                    LitE e{fold4(load4(f, ko)), DLit{ridx, 0, (uint16_t)f.size(), (uint8_t)(LIT_NOCASE | LIT_TRIGGER),
+                                                     (uint8_t)g.zones, ko, 0}, f};
+                    lits.push_back(e);
+                }
+            }
+            sregex.push_back(sr);
         }
     }
     st.n_sigs = (uint32_t)sig.size();

@@ -533,221 +533,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) void k_route(const gm_req *__restrict_
     }
 }
 
-constexpr int SCAN_BLOCK = 1024;
-constexpr int SCAN_WAVES = SCAN_BLOCK / 64;
-constexpr uint32_t WAF_A_WORDS = (1u << WAF_A_BITS) / 32, WAF_B_WORDS = (1u << WAF_B_BITS) / 32;
-
-__device__ __forceinline__ uint32_t load_u32_guard(const uint8_t *A, uint64_t off, uint64_t len) {
-    if (off + 4 <= len) return *reinterpret_cast<const uint32_t *>(A + off);
-    uint32_t w = 0;
-    for (int k = 0; k < 4; k++) if (off + k < len) w |= (uint32_t)A[off + k] << (8 * k);
-    return w;
-}
-
-__global__ __launch_bounds__(SCAN_BLOCK) void k_waf_scan(const uint8_t *__restrict__ A, uint64_t len,
-                                                         const uint32_t *__restrict__ bmA,
-                                                         const uint32_t *__restrict__ bmB,
-                                                         unsigned long long *__restrict__ cand, uint32_t cap,
-                                                         uint32_t *__restrict__ status) {
-    extern __shared__ uint32_t lds[];
-    uint32_t *la = lds, *lb = lds + WAF_A_WORDS;
-    {
-        const uint4 *ga = reinterpret_cast<const uint4 *>(bmA);
-        const uint4 *gb = reinterpret_cast<const uint4 *>(bmB);
-        uint4 *sa = reinterpret_cast<uint4 *>(la), *sb = reinterpret_cast<uint4 *>(lb);
-        for (uint32_t k = threadIdx.x; k < WAF_A_WORDS / 4; k += SCAN_BLOCK) sa[k] = ga[k];
-        for (uint32_t k = threadIdx.x; k < WAF_B_WORDS / 4; k += SCAN_BLOCK) sb[k] = gb[k];
-    }
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t nchunks = (len + 1023) >> 10;
-    const uint64_t stride = (uint64_t)gridDim.x * SCAN_WAVES;
-    for (uint64_t ch = (uint64_t)blockIdx.x * SCAN_WAVES + wave; ch < nchunks; ch += stride) {
-        const uint64_t off = (ch << 10) + lane * 16;
-        uint32_t d[5];
-        if (off + 16 <= len) {
-            uint4 q = *reinterpret_cast<const uint4 *>(A + off);
-            d[0] = q.x; d[1] = q.y; d[2] = q.z; d[3] = q.w;
-        } else {
-            for (int k = 0; k < 4; k++) d[k] = load_u32_guard(A, off + 4 * k, len);
-        }
-        uint32_t nx = __shfl_down(d[0], 1);
-        if (lane == 63) nx = load_u32_guard(A, off + 16, len);
-        d[4] = nx;
-#pragma unroll
-        for (int k = 0; k < 5; k++) d[k] = fold4(d[k]);
-        uint32_t mask = 0;
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const uint32_t w = __builtin_amdgcn_alignbyte(d[(j >> 2) + 1], d[j >> 2], j & 3);
-            const uint32_t ha = waf_hash_a(w);
-            if ((la[ha >> 5] >> (ha & 31)) & 1u) {
-                const uint32_t hb = waf_hash_b(w);
-                if (((lb[hb >> 5] >> (hb & 31)) & 1u) && off + j + 4 <= len) mask |= 1u << j;
-            }
-        }
-        if (__ballot(mask != 0) == 0ull) continue;
-        // wave-wide exclusive prefix of per-lane counts
-        uint32_t cnt = __popc(mask), incl = cnt;
-#pragma unroll
-        for (int s = 1; s < 64; s <<= 1) {
-            uint32_t y = __shfl_up(incl, s);
-            if (lane >= (uint32_t)s) incl += y;
-        }
-        uint32_t total = __shfl(incl, 63);
-        uint32_t base = 0;
-        if (lane == 63) base = atomicAdd(status + 0, total);
-        base = __shfl(base, 63) + incl - cnt;
-        while (mask) {
-            int j = __ffs(mask) - 1;
-            mask &= mask - 1;
-            if (base < cap) cand[base] = off + j;
-            base++;
-        }
-    }
-}
-
-__device__ __forceinline__ uint32_t find_rec(const gm_req *reqs, uint32_t n, const uint32_t *blk2rec, uint64_t pos) {
-    uint32_t r = blk2rec[pos >> BLK_SHIFT];
-    while (r + 1 < n && reqs[r + 1].base <= pos) r++;
-    return r;
-}
-
-__device__ __forceinline__ void push_u64(unsigned long long *buf, uint32_t cap, uint32_t *ctr, unsigned long long v,
-                                         uint32_t *status) {
-    uint32_t k = atomicAdd(ctr, 1u);
-    if (k < cap) buf[k] = v; else atomicOr(status + 3, 1u);
-}
-
-__global__ __launch_bounds__(256) void k_waf_verify(const uint8_t *__restrict__ A, uint64_t len,
-                                                    const gm_req *__restrict__ reqs, uint32_t n,
-                                                    const uint32_t *__restrict__ blk2rec, GTab t,
-                                                    const unsigned long long *__restrict__ cand, uint32_t ccap,
-                                                    unsigned long long *__restrict__ pairs, uint32_t pcap,
-                                                    unsigned long long *__restrict__ jobs, uint32_t jcap,
-                                                    uint32_t *__restrict__ status) {
-    const uint32_t nc = min(status[0], ccap);
-    if (status[0] > ccap && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(status + 3, 4u);
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nc; i += gridDim.x * blockDim.x) {
-        const uint64_t pos = cand[i];
-        uint32_t w = 0;
-        for (int k = 0; k < 4; k++) w |= (uint32_t)A[pos + k] << (8 * k);
-        w = fold4(w);
-        uint32_t b = lit_bucket_hash(w) & t.lit_mask;
-        DLitBucket bk;
-        for (;; b = (b + 1) & t.lit_mask) {
-            bk = t.lit_buckets[b];
-            if (bk.count == 0 || bk.key == w) break;
-        }
-        if (bk.count == 0) continue;
-        const uint32_t r = find_rec(reqs, n, blk2rec, pos);
-        const Rec rc = load_rec(reqs + r);
-        if (pos < rc.base) continue;
-        const uint64_t rel = pos - rc.base;
-        uint32_t z; uint64_t zend;
-        if (rel < rc.uri_len) { z = 0; zend = rc.uri_len; }
-        else if (rel < (uint64_t)rc.uri_len + rc.args_len) { z = 1; zend = rc.uri_len + rc.args_len; }
-        else if (rel < (uint64_t)rc.uri_len + rc.args_len + rc.hdr_len) { z = 2; zend = (uint64_t)rc.uri_len + rc.args_len + rc.hdr_len; }
-        else if (rel < (uint64_t)rc.uri_len + rc.args_len + rc.hdr_len + rc.body_len) {
-            z = 3; zend = (uint64_t)rc.uri_len + rc.args_len + rc.hdr_len + rc.body_len;
-        } else continue;
-        zend += rc.base;
-        for (uint32_t k = 0; k < bk.count; k++) {
-            const DLit L = t.lits[bk.first + k];
-            if (!(L.zones & (1u << z)) || pos + L.len > zend) continue;
-            const uint8_t *pat = t.bytes + L.bytes_off;
-            bool ok = true;
-            if (L.flags & LIT_NOCASE) { for (uint32_t q = 0; ok && q < L.len; q++) if (lc(A[pos + q]) != pat[q]) ok = false; }
-            else { for (uint32_t q = 0; ok && q < L.len; q++) if (A[pos + q] != pat[q]) ok = false; }
-            if (!ok) continue;
-            if (L.flags & LIT_TRIGGER)
-                push_u64(jobs, jcap, status + 2, ((unsigned long long)r << 32) | (L.id << 2) | z, status);
-            else
-                push_u64(pairs, pcap, status + 1, ((unsigned long long)r << 32) | L.id, status);
-        }
-    }
-}
-
-__device__ __forceinline__ void zone_of(const Rec &rc, uint32_t z, uint64_t &zs, uint32_t &zl) {
-    uint64_t o = rc.base;
-    const uint32_t lens[4] = {rc.uri_len, rc.args_len, rc.hdr_len, rc.body_len};
-    for (uint32_t k = 0; k < z; k++) o += lens[k];
-    zs = o; zl = lens[z];
-}
-
-__global__ __launch_bounds__(256) void k_waf_regex(const uint8_t *__restrict__ A, const gm_req *__restrict__ reqs,
-                                                   GTab t, const unsigned long long *__restrict__ jobs, uint32_t nj,
-                                                   unsigned long long *__restrict__ pairs, uint32_t pcap,
-                                                   uint32_t *__restrict__ status) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nj; i += gridDim.x * blockDim.x) {
-        const unsigned long long j = jobs[i];
-        if (i > 0 && jobs[i - 1] == j) continue;
-        const uint32_t r = (uint32_t)(j >> 32), lo = (uint32_t)j, rx = lo >> 2, z = lo & 3;
-        const Rec rc = load_rec(reqs + r);
-        uint64_t zs; uint32_t zl;
-        zone_of(rc, z, zs, zl);
-        const DSigRegex g = t.sig_regex[rx];
-        if (dfa_run_bytes(t, g.dfa, A + zs, zl))
-            push_u64(pairs, pcap, status + 1, ((unsigned long long)r << 32) | g.rule, status);
-    }
-}
-
-__global__ __launch_bounds__(256) void k_waf_always(const uint8_t *__restrict__ A, const gm_req *__restrict__ reqs,
-                                                    uint32_t n, GTab t, unsigned long long *__restrict__ pairs,
-                                                    uint32_t pcap, uint32_t *__restrict__ status) {
-    const uint64_t total = (uint64_t)n * t.n_always;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t r = (uint32_t)(i / t.n_always), a = (uint32_t)(i % t.n_always);
-        const DSigRegex g = t.sig_regex[t.always[a]];
-        const Rec rc = load_rec(reqs + r);
-        for (uint32_t z = 0; z < 4; z++) {
-            if (!(g.zones & (1u << z))) continue;
-            uint64_t zs; uint32_t zl;
-            zone_of(rc, z, zs, zl);
-            if (dfa_run_bytes(t, g.dfa, A + zs, zl)) {
-                push_u64(pairs, pcap, status + 1, ((unsigned long long)r << 32) | g.rule, status);
-                break;
-            }
-        }
-    }
-}
-
-__device__ __forceinline__ bool waf_active(const gm_verdict &v) {
-    return v.action == GM_ACT_PROXY && v.waf_mode != GM_WAF_OFF;
-}
-
-__global__ __launch_bounds__(256) void k_pairs_mark(const unsigned long long *__restrict__ p, uint32_t m,
-                                                    const gm_verdict *__restrict__ out, uint32_t *__restrict__ keep) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-        const unsigned long long x = p[i];
-        bool k = (i == 0 || p[i - 1] != x) && waf_active(out[(uint32_t)(x >> 32)]);
-        keep[i] = k ? 1u : 0u;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_pairs_emit(const unsigned long long *__restrict__ p, uint32_t m,
-                                                    const uint32_t *__restrict__ keep, const uint32_t *__restrict__ idx,
-                                                    gm_verdict *__restrict__ out, uint32_t *__restrict__ hit_ids,
-                                                    uint64_t hit_cap, unsigned long long *__restrict__ counters,
-                                                    uint32_t n_locs, uint32_t *__restrict__ status) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-        if (i == m - 1) status[4] = idx[i] + keep[i];
-        if (!keep[i]) continue;
-        const unsigned long long x = p[i];
-        const uint32_t r = (uint32_t)(x >> 32), rule = (uint32_t)x;
-        const uint32_t o = idx[i];
-        if (o < hit_cap) hit_ids[o] = rule; else atomicOr(status + 3, 2u);
-        atomicAdd(&counters[n_locs + rule], 1ull);
-        if (i == 0 || (uint32_t)(p[i - 1] >> 32) != r) {
-            uint32_t cnt = 0;
-            for (uint32_t j = i; j < m && (uint32_t)(p[j] >> 32) == r; j++) cnt += keep[j];
-            gm_verdict &v = out[r];
-            v.first_hit_off = o;
-            v.n_hits = (uint16_t)min(cnt, 0xFFFFu);
-            if (v.waf_mode == GM_WAF_BLOCK && cnt) { v.action = GM_ACT_BLOCK; v.status = 403; }
-        }
-    }
-}
+#include "gm_waf.inc"
 
 }  // namespace
 
@@ -772,6 +558,7 @@ struct gm_ctx {
     unsigned long long *d_pairs = nullptr, *d_pairs2 = nullptr; size_t cap_pairs = 0;
     unsigned long long *d_jobs = nullptr, *d_jobs2 = nullptr; size_t cap_jobs = 0;
     uint32_t *d_keep = nullptr, *d_idx = nullptr; size_t cap_keep = 0, cap_idx = 0;
+    uint32_t *d_ccnt = nullptr; size_t cap_ccnt = 0;
     uint8_t *d_temp = nullptr; size_t cap_temp = 0;
     // host-staging (GM_BATCH_HOST)
     uint8_t *d_stage = nullptr; size_t cap_stage = 0;
@@ -822,8 +609,8 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
             c->cu_count = cus;
-        if (hipMalloc((void **)&c->d_status, 64) != hipSuccess ||
-            hipHostMalloc((void **)&c->h_status, 64, hipHostMallocDefault) != hipSuccess) {
+        if (hipMalloc((void **)&c->d_status, STATUS_WORDS * 4) != hipSuccess ||
+            hipHostMalloc((void **)&c->h_status, STATUS_WORDS * 4, hipHostMallocDefault) != hipSuccess) {
             t_err = "status alloc failed"; delete c; return nullptr;
         }
         (void)hipFuncSetAttribute((const void *)k_waf_scan, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -842,7 +629,8 @@ void gm_destroy(gm_ctx *c) {
         if (c->gen) (void)hipFree(c->gen->d_image);
         for (void *p : {(void *)c->d_counters, (void *)c->d_status, (void *)c->d_blk2rec, (void *)c->d_cand,
                         (void *)c->d_pairs, (void *)c->d_pairs2, (void *)c->d_jobs, (void *)c->d_jobs2,
-                        (void *)c->d_keep, (void *)c->d_idx, (void *)c->d_temp, (void *)c->d_stage})
+                        (void *)c->d_keep, (void *)c->d_idx, (void *)c->d_temp, (void *)c->d_stage,
+                        (void *)c->d_ccnt})
             if (p) (void)hipFree(p);
         if (c->h_status) (void)hipHostFree(c->h_status);
         if (c->comm) ncclCommDestroy(c->comm);
@@ -908,7 +696,7 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
         return GM_OK;
     };
     c->ev_used = 0;
-    HIPCHK(c, hipMemsetAsync(c->d_status, 0, 64, s));
+    HIPCHK(c, hipMemsetAsync(c->d_status, 0, STATUS_WORDS * 4, s));
     if (mark(0)) return GM_E_HIP;
     {
         uint32_t blocks = std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK, (uint32_t)c->cu_count * 8);
@@ -923,32 +711,28 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
 
     const size_t ccap = alen / 64 + 65536, pcap = (size_t)n * 2 + 65536, jcap = (size_t)n + 65536;
     int e;
-    if ((e = grow(c, c->d_cand, c->cap_cand, ccap))) return e;
+    // persistent scan grid: one 1024-thread workgroup per CU (96 KiB of LDS bitmaps each);
+    // every wave owns a contiguous arena range and a private candidate region of wcap entries
+    const uint32_t scan_blocks = (uint32_t)c->cu_count;
+    const uint32_t W = scan_blocks * SCAN_WAVES;
+    if ((e = grow(c, c->d_cand, c->cap_cand, std::max<size_t>(ccap, (size_t)W * 1024)))) return e;
+    if ((e = grow(c, c->d_ccnt, c->cap_ccnt, W))) return e;
+    const uint32_t wcap = (uint32_t)std::min<size_t>(c->cap_cand / W, 0xFFFFFFFFu);
     { size_t cp = c->cap_pairs; if ((e = grow(c, c->d_pairs, cp, pcap))) return e;
       size_t cp2 = c->cap_pairs; if ((e = grow(c, c->d_pairs2, cp2, pcap))) return e; c->cap_pairs = std::max(cp, cp2); }
     { size_t cj = c->cap_jobs; if ((e = grow(c, c->d_jobs, cj, jcap))) return e;
       size_t cj2 = c->cap_jobs; if ((e = grow(c, c->d_jobs2, cj2, jcap))) return e; c->cap_jobs = std::max(cj, cj2); }
 
-    {
-        const uint64_t nchunks = (alen + 1023) >> 10;
-        uint32_t blocks = (uint32_t)std::min<uint64_t>((nchunks + SCAN_WAVES - 1) / SCAN_WAVES, (uint64_t)c->cu_count * 2 * 8);
-        if (blocks == 0) blocks = 1;
-        k_waf_scan<<<blocks, SCAN_BLOCK, (WAF_A_WORDS + WAF_B_WORDS) * 4, s>>>(
-            A, alen, t.waf_a, t.waf_b, c->d_cand, (uint32_t)std::min<size_t>(c->cap_cand, 0xFFFFFFFFu), c->d_status);
-        HIPCHK(c, hipGetLastError());
-    }
+    k_waf_scan<<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
+    HIPCHK(c, hipGetLastError());
     if (mark(2)) return GM_E_HIP;
-    {
-        uint32_t blocks = (uint32_t)c->cu_count * 8;
-        k_waf_verify<<<blocks, 256, 0, s>>>(A, alen, reqs, n, c->d_blk2rec, t, c->d_cand,
-                                            (uint32_t)std::min<size_t>(c->cap_cand, 0xFFFFFFFFu), c->d_pairs,
-                                            (uint32_t)c->cap_pairs, c->d_jobs, (uint32_t)c->cap_jobs, c->d_status);
-        HIPCHK(c, hipGetLastError());
-    }
+    k_waf_verify<<<W, 256, 0, s>>>(A, alen, reqs, n, c->d_blk2rec, t, c->d_cand, wcap, c->d_ccnt, W, c->d_pairs,
+                                   (uint32_t)c->cap_pairs, c->d_jobs, (uint32_t)c->cap_jobs, c->d_status);
+    HIPCHK(c, hipGetLastError());
     if (mark(3)) return GM_E_HIP;
-    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, 64, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, STATUS_WORDS * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    c->last_candidates = c->h_status[0];
+    c->last_candidates = c->h_status[5];
     if (c->h_status[3]) return fail(c, GM_E_OVERFLOW, "WAF candidate/pair/job capacity exceeded");
     uint32_t nj = std::min<uint32_t>(c->h_status[2], (uint32_t)c->cap_jobs);
     int rec_bits = 1;
@@ -966,7 +750,7 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
         k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(A, reqs, n, t, c->d_pairs, (uint32_t)c->cap_pairs, c->d_status);
         HIPCHK(c, hipGetLastError());
     }
-    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, 64, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, STATUS_WORDS * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     if (c->h_status[3]) return fail(c, GM_E_OVERFLOW, "WAF pair capacity exceeded");
     uint32_t m = std::min<uint32_t>(c->h_status[1], (uint32_t)c->cap_pairs);
@@ -998,7 +782,7 @@ int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit
     std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(c, hipSetDevice(c->dev));
     hipStream_t s = (hipStream_t)stream;
-    if (in->n == 0) return GM_OK;
+    if (in->n == 0) { HIPCHK(c, hipMemsetAsync(c->d_status, 0, STATUS_WORDS * 4, s)); return GM_OK; }
     if (((uintptr_t)in->arena & 15) || ((uintptr_t)in->reqs & 15) || ((uintptr_t)out & 15))
         return fail(c, GM_E_INVAL, "reqs / arena / out must be 16-byte aligned");
     if (!(in->flags & GM_BATCH_HOST))
@@ -1028,7 +812,7 @@ int gm_sync(gm_ctx *c, void *stream) {
     if (c->flags & GM_CREATE_COMPILE_ONLY) return GM_OK;
     HIPCHK(c, hipSetDevice(c->dev));
     hipStream_t s = (hipStream_t)stream;
-    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, 64, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, STATUS_WORDS * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     c->last_hits = c->h_status[4];
     if (c->ev_pending) {

@@ -374,8 +374,21 @@ struct NfaBuilder {
 struct FI {
     bool exact_ok = false;
     std::vector<std::string> exact;
-    std::vector<std::string> best;   // best OR-set found anywhere inside (empty = none)
+    std::vector<std::string> best;     // best OR-set found anywhere inside (empty = none)
+    std::vector<std::string> prefix = {""};   // every match starts with one of these (folded)
 };
+
+bool small_set(const std::vector<std::string> &v) {
+    if (v.size() > 16) return false;
+    for (auto &s : v) if (s.size() > 32) return false;
+    return true;
+}
+std::vector<std::string> cross(const std::vector<std::string> &a, const std::vector<std::string> &b) {
+    std::vector<std::string> r;
+    for (auto &x : a) for (auto &y : b) r.push_back(x + y);
+    std::sort(r.begin(), r.end()); r.erase(std::unique(r.begin(), r.end()), r.end());
+    return r;
+}
 
 int score_len(const std::vector<std::string> &s) {
     if (s.empty()) return -1;
@@ -406,14 +419,16 @@ FI factors(const std::vector<Node> &N, int n) {
         if (f.count() <= 4) {
             r.exact_ok = true;
             for (int c = 0; c < 256; c++) if (f[c]) r.exact.push_back(std::string(1, (char)c));
+            r.prefix = r.exact;
         }
         return r;
     }
     case Node::CAT: {
         std::vector<std::string> cur = {""};
         bool cur_ok = true, all_exact = true;
-        for (int k : x.kids) {
-            FI g = factors(N, k);
+        std::vector<FI> gs;
+        for (int k : x.kids) gs.push_back(factors(N, k));
+        for (const FI &g : gs) {
             take_best(r.best, g.best);
             if (g.exact_ok && cur_ok && cur.size() * g.exact.size() <= 16) {
                 std::vector<std::string> nx;
@@ -430,13 +445,26 @@ FI factors(const std::vector<Node> &N, int n) {
         }
         take_best(r.best, cur);
         if (all_exact) { r.exact_ok = true; r.exact = cur; }
+        std::vector<std::string> pre = {""};
+        for (const FI &g : gs) {
+            if (g.exact_ok) {
+                auto nx = cross(pre, g.exact);
+                if (small_set(nx)) { pre = nx; continue; }
+                break;
+            }
+            auto nx = cross(pre, g.prefix);
+            if (small_set(nx)) pre = nx;
+            break;
+        }
+        r.prefix = pre;
         return r;
     }
     case Node::ALT: {
         bool all_exact = true, all_req = true;
-        std::vector<std::string> ex, un;
+        std::vector<std::string> ex, un, pu;
         for (int k : x.kids) {
             FI g = factors(N, k);
+            pu.insert(pu.end(), g.prefix.begin(), g.prefix.end());
             if (g.exact_ok) ex.insert(ex.end(), g.exact.begin(), g.exact.end()); else all_exact = false;
             std::vector<std::string> b = g.best;
             if (g.exact_ok) take_best(b, g.exact);
@@ -445,11 +473,14 @@ FI factors(const std::vector<Node> &N, int n) {
         uniq(ex); uniq(un);
         if (all_exact && ex.size() <= 16) { r.exact_ok = true; r.exact = ex; }
         if (all_req) r.best = un;
+        uniq(pu);
+        r.prefix = small_set(pu) ? pu : std::vector<std::string>{""};
         return r;
     }
     case Node::REP: {
         FI g = factors(N, x.kids[0]);
         if (x.mn >= 1) {
+            r.prefix = g.prefix;
             r.best = g.best;
             if (g.exact_ok) take_best(r.best, g.exact);
             if (x.mn == x.mx && g.exact_ok) {
@@ -549,59 +580,73 @@ RegexInfo compile_regex(const std::string &pattern, bool caseless, int max_state
     };
 
     std::vector<int> restart = closure({start}, false);
-    bool has_restart = false;
-    for (int s : restart) if (S[s].t == NS::SET || S[s].t == NS::MATCH || S[s].t == NS::EOL) has_restart = true;
-    out.dfa.anchored_start = !has_restart;
+    bool can_restart = false;
+    for (int s : restart) if (S[s].t == NS::SET || S[s].t == NS::MATCH || S[s].t == NS::EOL) can_restart = true;
 
-    std::map<std::vector<int>, int> ids;
-    std::vector<std::vector<int>> sets;
-    sets.push_back({});                       // 0 = dead
-    std::vector<int> s0 = closure({start}, true);
-    ids[s0] = 1; sets.push_back(s0);
-    std::vector<uint16_t> trans;
-    std::vector<uint8_t> acc;
-    const int C = out.dfa.n_classes;
-    for (size_t cur = 0; cur < sets.size(); cur++) {
-        trans.resize((cur + 1) * C, 0);
-        uint8_t a = 0;
-        if (cur != 0) {
-            for (int s : sets[cur]) if (S[s].t == NS::MATCH) a |= 1;
-            if (end_accept(sets[cur])) a |= 2;
-        }
-        acc.push_back(a);
-        if (cur == 0) continue;
-        if (a & 1) {   // absorbing: a match already exists
-            for (int c = 0; c < C; c++) trans[cur * C + c] = (uint16_t)cur;
-            continue;
-        }
-        for (int c = 0; c < C; c++) {
-            int b = rep[c];
-            std::vector<int> seeds;
-            for (int s : sets[cur]) if (S[s].t == NS::SET && B.sets[S[s].set][b]) seeds.push_back(S[s].out);
-            if (has_restart) seeds.push_back(start);
-            std::vector<int> nx = closure(seeds, false);
-            int id;
-            if (!useful(nx) || (!has_restart && nx.empty())) id = 0;
-            else {
-                auto it = ids.find(nx);
-                if (it == ids.end()) {
-                    id = (int)sets.size();
-                    if (id >= max_states) { out.status = RX_TOO_BIG; out.error = "dfa too big"; return out; }
-                    ids[nx] = id; sets.push_back(nx);
-                } else id = it->second;
+    // search = true: unanchored PCRE search DFA (start set re-entered at every byte);
+    // search = false: a DFA anchored at the first byte (prefix-trigger verification).
+    auto build = [&](bool search, Dfa &D) -> bool {
+        const bool has_restart = search && can_restart;
+        D.anchored_start = !has_restart;
+        D.n_classes = out.dfa.n_classes;
+        std::map<std::vector<int>, int> ids;
+        std::vector<std::vector<int>> sets;
+        sets.push_back({});                       // 0 = dead
+        std::vector<int> s0 = closure({start}, true);
+        ids[s0] = 1; sets.push_back(s0);
+        std::vector<uint16_t> trans;
+        std::vector<uint8_t> acc;
+        const int C = D.n_classes;
+        for (size_t cur = 0; cur < sets.size(); cur++) {
+            trans.resize((cur + 1) * C, 0);
+            uint8_t a = 0;
+            if (cur != 0) {
+                for (int s : sets[cur]) if (S[s].t == NS::MATCH) a |= 1;
+                if (end_accept(sets[cur])) a |= 2;
             }
-            trans[cur * C + c] = (uint16_t)id;
+            acc.push_back(a);
+            if (cur == 0) continue;
+            if (a & 1) {   // absorbing: a match already exists
+                for (int c = 0; c < C; c++) trans[cur * C + c] = (uint16_t)cur;
+                continue;
+            }
+            for (int c = 0; c < C; c++) {
+                int b = rep[c];
+                std::vector<int> seeds;
+                for (int s : sets[cur]) if (S[s].t == NS::SET && B.sets[S[s].set][b]) seeds.push_back(S[s].out);
+                if (has_restart) seeds.push_back(start);
+                std::vector<int> nx = closure(seeds, false);
+                int id;
+                if (!useful(nx) || nx.empty()) id = 0;
+                else {
+                    auto it = ids.find(nx);
+                    if (it == ids.end()) {
+                        id = (int)sets.size();
+                        if (id >= max_states) return false;
+                        ids[nx] = id; sets.push_back(nx);
+                    } else id = it->second;
+                }
+                trans[cur * C + c] = (uint16_t)id;
+            }
         }
-    }
-    out.dfa.trans = std::move(trans);
-    out.dfa.acc = std::move(acc);
-    out.dfa.n_states = (int)sets.size();
-    for (int b = 0; b < 256; b++) out.dfa.cls[b] = (uint8_t)cls[b];
+        D.trans = std::move(trans);
+        D.acc = std::move(acc);
+        D.n_states = (int)sets.size();
+        for (int b = 0; b < 256; b++) D.cls[b] = (uint8_t)cls[b];
+        return true;
+    };
+    if (!build(true, out.dfa)) { out.status = RX_TOO_BIG; out.error = "dfa too big"; return out; }
 
     FI fi = factors(P.nodes, root);
     std::vector<std::string> best = fi.best;
     if (fi.exact_ok) take_best(best, fi.exact);
     if (score_len(best) > 0) { out.factors = best; out.min_factor = score_len(best); }
+    bool has_bol = false;
+    for (auto &nd : P.nodes) if (nd.k == Node::BOL) has_bol = true;
+    if (!has_bol && score_len(fi.prefix) >= 4 && build(false, out.anchored)) {
+        out.prefix = fi.prefix;
+        out.prefix_mode = true;
+    }
     out.status = RX_OK;
     return out;
 }

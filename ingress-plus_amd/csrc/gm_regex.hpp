@@ -31,6 +31,11 @@ struct RegexInfo {
     Dfa dfa;
     std::vector<std::string> factors;  // case-folded literals; every match contains one of them
     int min_factor = 0;                // shortest factor length (0 = no factor)
+    // prefix mode: every match *starts* with one of `prefix` (case-folded, all >= 4 bytes) and the
+    // pattern has no '^': a match exists iff `anchored` accepts from some occurrence of a prefix.
+    bool prefix_mode = false;
+    std::vector<std::string> prefix;
+    Dfa anchored;
 };
 
 RegexInfo compile_regex(const std::string &pattern, bool caseless, int max_states = 8192);

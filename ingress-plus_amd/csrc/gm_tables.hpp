@@ -127,10 +127,11 @@ struct DDfa {
 
 // ---- WAF signatures ----------------------------------------------------------------------
 constexpr int WAF_A_BITS = 19;       // LDS bitmap A: 2^19 bits = 64 KiB
-constexpr int WAF_B_BITS = 16;       // LDS bitmap B: 2^16 bits =  8 KiB (only probed on A hits)
+constexpr int WAF_B_BITS = 18;       // LDS bitmap B: 2^18 bits = 32 KiB (only probed on A hits)
+constexpr int CAND_SHARDS = 64;      // candidate-list shards (one atomic tail per shard)
 constexpr int BLK_SHIFT = 10;        // arena block (1 KiB) -> first record index (blk2rec)
 
-enum : uint8_t { LIT_NOCASE = 1, LIT_TRIGGER = 2 };
+enum : uint8_t { LIT_NOCASE = 1, LIT_TRIGGER = 2, LIT_PREFIX = 4 };
 struct DLitBucket { uint32_t key; uint32_t first; uint32_t count; uint32_t pad; };  // key = folded 4-gram + 1? see kWafEmpty
 struct DLit {
     uint32_t id;             // signature rule id (LIT) or regex index (TRIGGER)
@@ -138,13 +139,17 @@ struct DLit {
     uint16_t len;
     uint8_t  flags;          // LIT_*
     uint8_t  zones;          // bit0 uri, bit1 args, bit2 hdrs, bit3 body
-    uint32_t pad;
+    uint16_t key_off;        // offset of the 4-byte key window inside the pattern (rarest window)
+    uint16_t pad;
 };
+enum : uint32_t { RXM_TRIGGER = 0, RXM_ALWAYS = 1, RXM_PREFIX = 2 };
 struct DSigRegex {
-    uint32_t dfa;
+    uint32_t dfa;            // search DFA (whole zone)
+    uint32_t adfa;           // anchored DFA (RXM_PREFIX: run from each prefix occurrence)
     uint32_t rule;           // signature rule id
-    uint32_t zones;
-    uint32_t always;         // no >= 4-byte required factor: run on every request
+    uint16_t zones;
+    uint16_t mode;           // RXM_*: TRIGGER = factor hit -> zone job; ALWAYS = no >= 4-byte
+                             // factor, every request; PREFIX = verified inline in k_waf_verify
 };
 
 struct TabHeader {
