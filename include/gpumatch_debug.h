@@ -15,6 +15,10 @@ int gm_debug_regex(const char *pat, int caseless, const uint8_t *subject, size_t
 /* Required-literal factors ('\n'-separated, case-folded) the WAF prefilter uses for `pat`;
  * returns the shortest factor length (0 = none), < 0 if rejected. */
 int gm_debug_regex_factors(const char *pat, int caseless, char *out, size_t cap);
+/* The distinct case-folded 4-byte key windows of the loaded generation's WAF prefilter (all
+ * literals + regex triggers); returns their number (writes at most `cap`). */
+struct gm_ctx;
+int gm_debug_waf_keys(struct gm_ctx *ctx, uint32_t *out, size_t cap);
 #ifdef __cplusplus
 }
 #endif

@@ -12,6 +12,7 @@
 #include "gm_compile.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <map>
 #include <set>
@@ -614,31 +615,87 @@ uint32_t load4(const std::string &s, size_t o = 0) {
 }
 
 // Key window choice: the prefilter's candidate rate is dominated by 4-grams that benign
-// traffic really contains ("from", "into", "kind", "upda"...), so each literal is keyed on its
-// rarest window under an English / HTTP bigram-frequency model (any window is correct:
-// verification re-checks the whole literal at pos - key_off).
-int bigram_commonness(uint8_t a, uint8_t b) {
-    if (a >= 'A' && a <= 'Z') a |= 0x20;
-    if (b >= 'A' && b <= 'Z') b |= 0x20;
-    static const char *top = "thheineranreonatenndtiesortesofedisitalarsttontngsehaasouioleveco"
-                             "medehiriroicneearacelichllbemasiomurelwhlaotraelsnc";
-    const bool la = a >= 'a' && a <= 'z', lb = b >= 'a' && b <= 'z';
-    if (la && lb) {
-        for (const char *p = top; p[0] && p[1]; p += 2) if (p[0] == a && p[1] == b) return 4;
-        return 2;
-    }
-    if ((la && b == ' ') || (a == ' ' && lb)) return 3;
-    if ((a >= '0' && a <= '9') && (b >= '0' && b <= '9')) return 2;
-    if (la || lb) return (strchr("/.-_=&:,;", la ? b : a) && (la ? b : a)) ? 2 : 1;
-    return 0;
+// traffic really contains ("from", "into", "inse", "form"...), so each literal is keyed on its
+// least probable window under a unigram English/HTTP byte-frequency model (any window is
+// correct: verification re-checks the whole literal at pos - key_off).
+double byte_logfreq(uint8_t c) {
+    static const double letters[26] = {8.2, 1.5, 2.8, 4.3, 12.7, 2.2, 2.0, 6.1, 7.0, 0.15, 0.8, 4.0, 2.4,
+                                       6.7, 7.5, 1.9, 0.1, 6.0, 6.3, 9.1, 2.8, 1.0, 2.4, 0.15, 2.0, 0.07};
+    double f;
+    if (c >= 'A' && c <= 'Z') c |= 0x20;
+    if (c >= 'a' && c <= 'z') f = letters[c - 'a'] * 0.8;
+    else if (c == ' ') f = 15.0;
+    else if (c >= '0' && c <= '9') f = 0.5;
+    else if (strchr("/.-_=&:,;\r\n", c) && c) f = 1.0;
+    else if (c >= 0x20 && c < 0x7f) f = 0.2;
+    else f = 0.05;
+    return std::log2(f);
+}
+
+// Background model: 4-grams of frequent English words and HTTP header tokens.  A window that
+// occurs in ordinary text is a bad prefilter key however rare its letters are ("from", "kind").
+const char *kBackground =
+    "the of and to in is it you that he was for on are with as his they be at one have this from or had "
+    "by hot word but what some we can out other were all there when up use your how said an each she "
+    "which do their time if will way about many then them write would like so these her long make thing "
+    "see him two has look more day could go come did number sound no most people my over know water "
+    "than call first who may down side been now find any new work part take get place made live where "
+    "after back little only round man year came show every good me give our under name very through "
+    "just form sentence great think say help low line differ turn cause much mean before move right boy "
+    "old too same tell does set three want air well also play small end put home read hand port large "
+    "spell add even land here must big high such follow act why ask men change went light kind off need "
+    "house picture try us again animal point mother world near build self earth father head stand own "
+    "page should country found answer school grow study still learn plant cover food sun four between "
+    "state keep eye never last let thought city tree cross farm hard start might story saw far sea draw "
+    "left late run don't while press close night real life few north open seem together next white "
+    "children begin got walk example ease paper group always music those both mark often letter until "
+    "mile river car feet care second book carry took science eat room friend began idea fish mountain "
+    "stop once base hear horse cut sure watch color face wood main enough plain girl usual young ready "
+    "above ever red list though feel talk bird soon body dog family direct pose leave song measure door "
+    "product black short numeral class wind question happen complete ship area half rock order fire "
+    "south problem piece told knew pass since top whole king space heard best hour better true during "
+    "hundred five remember step early hold west ground interest reach fast verb sing listen six table "
+    "travel less morning ten simple several vowel toward war lay against pattern slow center love person "
+    "money serve appear road map rain rule govern pull cold notice voice unit power town fine certain fly "
+    "fall lead cry dark machine note wait plan figure star box noun field rest correct able pound done "
+    "beauty drive stood contain front teach week final gave green quick develop ocean warm free minute "
+    "strong special mind behind clear tail produce fact street inch multiply nothing course stay wheel "
+    "full force blue object decide surface deep moon island foot system busy test record boat common "
+    "gold possible plane stead dry wonder laugh thousand ago ran check game shape equate miss brought "
+    "heat snow tire bring yes distant fill east paint language among customer price cart checkout "
+    "account login session token user email address phone item items quantity total shipping billing "
+    "status created updated update insert delete select value values content information schema "
+    "mozilla windows linux x86_64 applewebkit khtml like gecko chrome safari firefox text/html "
+    "application/json application/xml application/xhtml+xml image/webp accept language encoding gzip "
+    "deflate keep-alive connection cache-control no-cache max-age referer origin cookie set-cookie "
+    "authorization bearer content-type content-length user-agent host http https www. .com .org .net "
+    "navigate same-origin cors upgrade-insecure-requests x-forwarded-for x-request x-trace-id "
+    "if-none-match etag utf-8 charset boundary multipart form-data urlencoded";
+
+const std::set<uint32_t> &background_grams() {
+    static std::set<uint32_t> g = [] {
+        std::set<uint32_t> s;
+        std::string t(kBackground);
+        for (size_t i = 0; i + 4 <= t.size(); i++) {
+            uint32_t w = (uint8_t)t[i] | (uint32_t)(uint8_t)t[i + 1] << 8 | (uint32_t)(uint8_t)t[i + 2] << 16 |
+                         (uint32_t)(uint8_t)t[i + 3] << 24;
+            s.insert(fold4(w));
+        }
+        return s;
+    }();
+    return g;
 }
 
 uint16_t rarest_window(const std::string &p) {
-    int best = 1 << 30; uint16_t bo = 0;
+    double best = 1e30; uint16_t bo = 0;
+    const auto &bg = background_grams();
     for (size_t o = 0; o + 4 <= p.size(); o++) {
-        int s = 0;
-        for (int k = 0; k < 3; k++) s += bigram_commonness((uint8_t)p[o + k], (uint8_t)p[o + k + 1]);
-        if (s < best) { best = s; bo = (uint16_t)o; }
+        double s = 0;
+        for (int k = 0; k < 4; k++) s += byte_logfreq((uint8_t)p[o + k]);
+        uint32_t w = (uint8_t)p[o] | (uint32_t)(uint8_t)p[o + 1] << 8 | (uint32_t)(uint8_t)p[o + 2] << 16 |
+                     (uint32_t)(uint8_t)p[o + 3] << 24;
+        if (bg.count(fold4(w))) s += 40.0;
+        if (s < best - 1e-9) { best = s; bo = (uint16_t)o; }
     }
     return bo;
 }
@@ -929,7 +986,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         return a.key != b.key ? a.key < b.key : a.lit.id < b.lit.id;
     });
     std::vector<DLit> dlits;
-    std::vector<uint32_t> waf_a((1u << WAF_A_BITS) / 32, 0), waf_b((1u << WAF_B_BITS) / 32, 0);
+    std::vector<uint64_t> waf_a((size_t)1 << BLOOM_WORDS_LOG2, 0);
+    std::vector<uint32_t> waf_b(4, 0);   // unused (kept for layout stability)
     std::vector<std::pair<uint32_t, std::pair<uint32_t, uint32_t>>> buckets;
     for (size_t i = 0; i < lits.size(); i++) {
         LitE &e = lits[i];
@@ -937,9 +995,9 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         dlits.push_back(e.lit);
         if (i == 0 || lits[i - 1].key != e.key) {
             buckets.push_back({e.key, {(uint32_t)i, 0}});
-            uint32_t ha = waf_hash_a(e.key), hb = waf_hash_b(e.key);
-            waf_a[ha >> 5] |= 1u << (ha & 31);
-            waf_b[hb >> 5] |= 1u << (hb & 31);
+            uint32_t wd, b0, b1, b2, b3;
+            bloom_probe(e.key, wd, b0, b1, b2, b3);
+            waf_a[wd] |= (1ull << b0) | (1ull << b1) | (1ull << b2) | (1ull << b3);
         }
         buckets.back().second.second++;
     }
@@ -955,7 +1013,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     st.n_servers = (uint32_t)M.servers.size();
     st.n_locations = (uint32_t)M.locs.size();
     st.n_counters = st.n_locations + st.n_sigs;
-    st.lds_bytes_scan = ((1u << WAF_A_BITS) + (1u << WAF_B_BITS)) / 8;
+    st.lds_bytes_scan = ((size_t)8 << BLOOM_WORDS_LOG2);
 
     // ---- image
     Image I;

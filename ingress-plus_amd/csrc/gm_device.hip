@@ -543,6 +543,7 @@ struct Generation {
     TabHeader hdr{};
     GTab tab{};
     gm_stats_t stats{};
+    std::vector<uint8_t> host_image;   // kept for host-side introspection (gpumatch_debug.h)
 };
 
 struct gm_ctx {
@@ -614,7 +615,7 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
             t_err = "status alloc failed"; delete c; return nullptr;
         }
         (void)hipFuncSetAttribute((const void *)k_waf_scan, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (WAF_A_WORDS + WAF_B_WORDS) * 4);
+                                  SCAN_LDS_BYTES);
         if (flags & GM_CREATE_PROFILE)
             for (auto &e : c->ev) (void)hipEventCreate(&e);
     }
@@ -649,6 +650,7 @@ int gm_load_generation(gm_ctx *c, const void *blob, size_t len, uint32_t gen) {
     if (!R.ok) return fail(c, R.code, R.err);   // previous generation stays live
     Generation *g = new Generation();
     g->hdr = R.hdr;
+    g->host_image = R.image;
     g->stats = R.stats;
     if (!(c->flags & GM_CREATE_COMPILE_ONLY)) {
         HIPCHK(c, hipSetDevice(c->dev));
@@ -711,9 +713,9 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
 
     const size_t ccap = alen / 64 + 65536, pcap = (size_t)n * 2 + 65536, jcap = (size_t)n + 65536;
     int e;
-    // persistent scan grid: one 1024-thread workgroup per CU (96 KiB of LDS bitmaps each);
+    // persistent scan grid: two 1024-thread workgroups per CU (64 KiB LDS Bloom filter each);
     // every wave owns a contiguous arena range and a private candidate region of wcap entries
-    const uint32_t scan_blocks = (uint32_t)c->cu_count;
+    const uint32_t scan_blocks = (uint32_t)c->cu_count * 2;
     const uint32_t W = scan_blocks * SCAN_WAVES;
     if ((e = grow(c, c->d_cand, c->cap_cand, std::max<size_t>(ccap, (size_t)W * 1024)))) return e;
     if ((e = grow(c, c->d_ccnt, c->cap_ccnt, W))) return e;
@@ -871,3 +873,14 @@ int gm_counters_allreduce(gm_ctx *c, void *stream) {
 }
 
 }  // extern "C"
+
+// ============================================================================ debug (gpumatch_debug.h)
+extern "C" int gm_debug_waf_keys(gm_ctx *c, uint32_t *out, size_t cap) {
+    if (!c || !c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
+    const TabHeader &h = c->gen->hdr;
+    const DLitBucket *b = (const DLitBucket *)(c->gen->host_image.data() + h.off_lit_buckets);
+    size_t k = 0;
+    for (uint32_t i = 0; i < h.n_lit_buckets_cap; i++)
+        if (b[i].count) { if (k < cap) out[k] = b[i].key; k++; }
+    return (int)k;
+}

@@ -126,8 +126,8 @@ struct DDfa {
 };
 
 // ---- WAF signatures ----------------------------------------------------------------------
-constexpr int WAF_A_BITS = 19;       // LDS bitmap A: 2^19 bits = 64 KiB
-constexpr int WAF_B_BITS = 18;       // LDS bitmap B: 2^18 bits = 32 KiB (only probed on A hits)
+constexpr int BLOOM_WORDS_LOG2 = 13; // blocked Bloom filter: 8192 x 64-bit words = 64 KiB of LDS
+constexpr int BLOOM_K = 4;           // bits per key, all in one 64-bit word (one ds_read_b64 / probe)
 constexpr int CAND_SHARDS = 64;      // candidate-list shards (one atomic tail per shard)
 constexpr int BLK_SHIFT = 10;        // arena block (1 KiB) -> first record index (blk2rec)
 
@@ -188,9 +188,14 @@ __host__ __device__ inline uint32_t name_hash_fin(uint32_t h, uint32_t port_idx)
 __host__ __device__ inline uint32_t edge_hash(uint32_t key) {
     uint32_t h = key * 0x9E3779B1u; return h ^ (h >> 15);
 }
-__host__ __device__ inline uint32_t waf_hash_a(uint32_t w) { return (w * 0x9E3779B1u) >> (32 - WAF_A_BITS); }
-__host__ __device__ inline uint32_t waf_hash_b(uint32_t w) {
-    uint32_t h = (w ^ (w >> 15)) * 0x85EBCA77u; return h >> (32 - WAF_B_BITS);
+// blocked-Bloom probe of a folded 4-gram: word index (13 bits) and 4 bit positions (6 bits each)
+// from the 64-bit product w * golden-ratio constant (high word well mixed over all 32 input bits)
+__host__ __device__ inline void bloom_probe(uint32_t w, uint32_t &word, uint32_t &b0, uint32_t &b1, uint32_t &b2,
+                                            uint32_t &b3) {
+    const uint64_t p = (uint64_t)w * 0x9E3779B1u;
+    const uint32_t hi = (uint32_t)(p >> 32), lo = (uint32_t)p;
+    word = hi >> (32 - BLOOM_WORDS_LOG2);
+    b0 = (hi >> 13) & 63; b1 = (hi >> 7) & 63; b2 = (hi >> 1) & 63; b3 = lo >> 26;
 }
 __host__ __device__ inline uint32_t lit_bucket_hash(uint32_t w) { uint32_t h = w * 0xC2B2AE3Du; return h ^ (h >> 16); }
 __host__ __device__ inline uint32_t fold4(uint32_t w) {
