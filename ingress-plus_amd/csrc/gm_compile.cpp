@@ -986,7 +986,9 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         return a.key != b.key ? a.key < b.key : a.lit.id < b.lit.id;
     });
     std::vector<DLit> dlits;
-    std::vector<uint64_t> waf_a((size_t)1 << BLOOM_WORDS_LOG2, 0);
+    uint32_t bloom_log2 = BLOOM_WORDS_LOG2_DEFAULT;
+    if (const char *ev = getenv("GM_BLOOM_LOG2")) bloom_log2 = atoi(ev) == 13 ? 13 : 14;   // tuning knob
+    std::vector<uint64_t> waf_a((size_t)1 << bloom_log2, 0);
     std::vector<uint32_t> waf_b(4, 0);   // unused (kept for layout stability)
     std::vector<std::pair<uint32_t, std::pair<uint32_t, uint32_t>>> buckets;
     for (size_t i = 0; i < lits.size(); i++) {
@@ -995,9 +997,9 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         dlits.push_back(e.lit);
         if (i == 0 || lits[i - 1].key != e.key) {
             buckets.push_back({e.key, {(uint32_t)i, 0}});
-            uint32_t wd, b0, b1, b2, b3;
-            bloom_probe(e.key, wd, b0, b1, b2, b3);
-            waf_a[wd] |= (1ull << b0) | (1ull << b1) | (1ull << b2) | (1ull << b3);
+            uint32_t wd, bb[BLOOM_K];
+            bloom_probe_rt(bloom_log2, e.key, wd, bb);
+            for (int q = 0; q < BLOOM_K; q++) waf_a[wd] |= 1ull << bb[q];
         }
         buckets.back().second.second++;
     }
@@ -1013,7 +1015,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     st.n_servers = (uint32_t)M.servers.size();
     st.n_locations = (uint32_t)M.locs.size();
     st.n_counters = st.n_locations + st.n_sigs;
-    st.lds_bytes_scan = ((size_t)8 << BLOOM_WORDS_LOG2);
+    st.lds_bytes_scan = ((size_t)8 << bloom_log2);
 
     // ---- image
     Image I;
@@ -1046,6 +1048,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_bytes = I.put(C.bytes);
     I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
     h.total = I.buf.size();
+    h.bloom_log2 = bloom_log2;
     memcpy(I.buf.data(), &h, sizeof h);
     st.table_bytes = h.total;
     R.image = std::move(I.buf);
@@ -1089,6 +1092,7 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;
     t.n_locs = h.n_locs; t.n_sigs = h.n_sigs; t.n_sig_regex = h.n_sig_regex; t.n_always = h.n_always;
     t.n_lits = h.n_lits;
+    t.bloom_log2 = h.bloom_log2;
     t.gen = gen;
     return t;
 }

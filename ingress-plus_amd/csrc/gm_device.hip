@@ -614,8 +614,10 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
             hipHostMalloc((void **)&c->h_status, STATUS_WORDS * 4, hipHostMallocDefault) != hipSuccess) {
             t_err = "status alloc failed"; delete c; return nullptr;
         }
-        (void)hipFuncSetAttribute((const void *)k_waf_scan, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  SCAN_LDS_BYTES);
+        (void)hipFuncSetAttribute((const void *)k_waf_scan<13>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  scan_lds_bytes<13>());
+        (void)hipFuncSetAttribute((const void *)k_waf_scan<14>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  scan_lds_bytes<14>());
         if (flags & GM_CREATE_PROFILE)
             for (auto &e : c->ev) (void)hipEventCreate(&e);
     }
@@ -715,7 +717,7 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
     int e;
     // persistent scan grid: two 1024-thread workgroups per CU (64 KiB LDS Bloom filter each);
     // every wave owns a contiguous arena range and a private candidate region of wcap entries
-    const uint32_t scan_blocks = (uint32_t)c->cu_count * 2;
+    const uint32_t scan_blocks = (uint32_t)c->cu_count * (t.bloom_log2 == 14 ? 1 : 2);
     const uint32_t W = scan_blocks * SCAN_WAVES;
     if ((e = grow(c, c->d_cand, c->cap_cand, std::max<size_t>(ccap, (size_t)W * 1024)))) return e;
     if ((e = grow(c, c->d_ccnt, c->cap_ccnt, W))) return e;
@@ -725,7 +727,10 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
     { size_t cj = c->cap_jobs; if ((e = grow(c, c->d_jobs, cj, jcap))) return e;
       size_t cj2 = c->cap_jobs; if ((e = grow(c, c->d_jobs2, cj2, jcap))) return e; c->cap_jobs = std::max(cj, cj2); }
 
-    k_waf_scan<<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
+    if (t.bloom_log2 == 14)
+        k_waf_scan<14><<<scan_blocks, SCAN_BLOCK, scan_lds_bytes<14>(), s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
+    else
+        k_waf_scan<13><<<scan_blocks, SCAN_BLOCK, scan_lds_bytes<13>(), s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
     HIPCHK(c, hipGetLastError());
     if (mark(2)) return GM_E_HIP;
     k_waf_verify<<<W, 256, 0, s>>>(A, alen, reqs, n, c->d_blk2rec, t, c->d_cand, wcap, c->d_ccnt, W, c->d_pairs,

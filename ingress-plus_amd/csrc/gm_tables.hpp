@@ -126,8 +126,10 @@ struct DDfa {
 };
 
 // ---- WAF signatures ----------------------------------------------------------------------
-constexpr int BLOOM_WORDS_LOG2 = 13; // blocked Bloom filter: 8192 x 64-bit words = 64 KiB of LDS
-constexpr int BLOOM_K = 4;           // bits per key, all in one 64-bit word (one ds_read_b64 / probe)
+// blocked Bloom filter in LDS: 2^13 (64 KiB, 2 WG/CU) or 2^14 (128 KiB, 1 WG/CU) 64-bit words,
+// BLOOM_K bits per key inside one word (one ds_read_b64 per probed byte position)
+constexpr int BLOOM_WORDS_LOG2_DEFAULT = 14;
+constexpr int BLOOM_K = 6;
 constexpr int CAND_SHARDS = 64;      // candidate-list shards (one atomic tail per shard)
 constexpr int BLK_SHIFT = 10;        // arena block (1 KiB) -> first record index (blk2rec)
 
@@ -163,6 +165,8 @@ struct TabHeader {
              off_rtargets, off_splits, off_parts, off_dfas, off_dfa_trans, off_dfa_acc, off_dfa_cls,
              off_bytes, off_waf_a, off_waf_b, off_lit_buckets, off_lits, off_sig_regex, off_always;
     uint64_t total;
+    uint32_t bloom_log2;     // Bloom words log2 (13 or 14)
+    uint32_t pad_end;
 };
 
 struct GTab {                // device pointers, built on host from the image base
@@ -175,7 +179,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const uint8_t *bytes; const uint32_t *waf_a; const uint32_t *waf_b;
     const DLitBucket *lit_buckets; const DLit *lits; const DSigRegex *sig_regex; const uint32_t *always;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
-    uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits;
+    uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2;
     uint32_t gen;
 };
 
@@ -189,13 +193,19 @@ __host__ __device__ inline uint32_t edge_hash(uint32_t key) {
     uint32_t h = key * 0x9E3779B1u; return h ^ (h >> 15);
 }
 // blocked-Bloom probe of a folded 4-gram: word index (13 bits) and 4 bit positions (6 bits each)
-// from the 64-bit product w * golden-ratio constant (high word well mixed over all 32 input bits)
-__host__ __device__ inline void bloom_probe(uint32_t w, uint32_t &word, uint32_t &b0, uint32_t &b1, uint32_t &b2,
-                                            uint32_t &b3) {
-    const uint64_t p = (uint64_t)w * 0x9E3779B1u;
-    const uint32_t hi = (uint32_t)(p >> 32), lo = (uint32_t)p;
-    word = hi >> (32 - BLOOM_WORDS_LOG2);
-    b0 = (hi >> 13) & 63; b1 = (hi >> 7) & 63; b2 = (hi >> 1) & 63; b3 = lo >> 26;
+// from two multiply-xorshift rounds (multiplicative hashing: keep the TOP bits of the low word)
+template <int WL>
+__host__ __device__ inline void bloom_probe(uint32_t w, uint32_t &word, uint32_t (&b)[BLOOM_K]) {
+    uint32_t h1 = w * 0x9E3779B1u;
+    h1 ^= h1 >> 15;
+    uint32_t h2 = h1 * 0x85EBCA77u;
+    h2 ^= h2 >> 13;
+    word = h2 >> (32 - WL);
+    b[0] = (h2 >> 12) & 63; b[1] = (h2 >> 6) & 63; b[2] = h2 & 63;
+    b[3] = h1 >> 26; b[4] = (h1 >> 20) & 63; b[5] = (h1 >> 14) & 63;
+}
+__host__ __device__ inline void bloom_probe_rt(uint32_t wl, uint32_t w, uint32_t &word, uint32_t (&b)[BLOOM_K]) {
+    if (wl == 14) bloom_probe<14>(w, word, b); else bloom_probe<13>(w, word, b);
 }
 __host__ __device__ inline uint32_t lit_bucket_hash(uint32_t w) { uint32_t h = w * 0xC2B2AE3Du; return h ^ (h >> 16); }
 __host__ __device__ inline uint32_t fold4(uint32_t w) {
