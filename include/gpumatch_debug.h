@@ -19,6 +19,9 @@ int gm_debug_regex_factors(const char *pat, int caseless, char *out, size_t cap)
  * literals + regex triggers); returns their number (writes at most `cap`). */
 struct gm_ctx;
 int gm_debug_waf_keys(struct gm_ctx *ctx, uint32_t *out, size_t cap);
+/* Host restatement of the WAF scan kernel's candidate rule over arena bytes A[0, len): writes
+ * the candidate positions (at most `cap`) and returns their number. */
+int64_t gm_debug_waf_prefilter(struct gm_ctx *ctx, const uint8_t *A, size_t len, uint64_t *out, size_t cap);
 #ifdef __cplusplus
 }
 #endif

@@ -625,8 +625,8 @@ double byte_logfreq(uint8_t c) {
     if (c >= 'A' && c <= 'Z') c |= 0x20;
     if (c >= 'a' && c <= 'z') f = letters[c - 'a'] * 0.8;
     else if (c == ' ') f = 15.0;
-    else if (c >= '0' && c <= '9') f = 0.5;
-    else if (strchr("/.-_=&:,;\r\n", c) && c) f = 1.0;
+    else if (c >= '0' && c <= '9') f = 1.5;                  // ids, timestamps, addresses
+    else if (strchr("/.-_=&:,;\r\n", c) && c) f = 2.0;       // URL / form / header punctuation
     else if (c >= 0x20 && c < 0x7f) f = 0.2;
     else f = 0.05;
     return std::log2(f);
@@ -686,18 +686,67 @@ const std::set<uint32_t> &background_grams() {
     return g;
 }
 
+// folded 3-grams of the background corpus, including word boundaries seen as separators
+// ("lay" of "play_" / "delay="): a window containing one is only somewhat rarer than the word
+const std::set<uint32_t> &background_grams3() {
+    static std::set<uint32_t> g = [] {
+        std::set<uint32_t> s;
+        std::string t(kBackground);
+        for (size_t i = 0; i + 3 <= t.size(); i++)
+            s.insert(fold4((uint8_t)t[i] | (uint32_t)(uint8_t)t[i + 1] << 8 | (uint32_t)(uint8_t)t[i + 2] << 16) &
+                     0xFFFFFFu);
+        return s;
+    }();
+    return g;
+}
+
+double window_score(const std::string &p, size_t o) {
+    double s = 0;
+    for (int k = 0; k < 4; k++) s += byte_logfreq((uint8_t)p[o + k]);
+    const uint32_t w = fold4(load4(p, o));
+    if (background_grams().count(w)) s += 40.0;
+    for (int k = 0; k < 2; k++) {
+        const uint32_t g3 = (w >> (8 * k)) & 0xFFFFFFu;
+        if ((g3 & 0xFF) != ' ' && (g3 >> 16) != ' ' && background_grams3().count(g3)) s += 6.0;
+    }
+    return s;
+}
+
 uint16_t rarest_window(const std::string &p) {
     double best = 1e30; uint16_t bo = 0;
-    const auto &bg = background_grams();
     for (size_t o = 0; o + 4 <= p.size(); o++) {
-        double s = 0;
-        for (int k = 0; k < 4; k++) s += byte_logfreq((uint8_t)p[o + k]);
-        uint32_t w = (uint8_t)p[o] | (uint32_t)(uint8_t)p[o + 1] << 8 | (uint32_t)(uint8_t)p[o + 2] << 16 |
-                     (uint32_t)(uint8_t)p[o + 3] << 24;
-        if (bg.count(fold4(w))) s += 40.0;
+        const double s = window_score(p, o);
         if (s < best - 1e-9) { best = s; bo = (uint16_t)o; }
     }
     return bo;
+}
+
+// Bloom multiplier per generation: a Bloom filter's false-positive rate is an average; on real
+// traffic what matters is whether a handful of very frequent benign 4-grams happen to collide.
+// Build the filter with each candidate multiplier and keep the one under which the fewest
+// background-corpus 4-grams (plus their one-byte neighbours in case) test positive.
+const uint32_t kBloomMuls[] = {0x9E3779B1u, 0x85EBCA77u, 0xC2B2AE3Du, 0x27D4EB2Fu, 0x165667B1u, 0xD3A2646Cu | 1u,
+                               0xFD7046C5u, 0xB55A4F09u, 0x7FEB352Du, 0x846CA68Bu, 0x2C1B3C6Du, 0x297A2D39u,
+                               0xE6546B64u | 1u, 0x1B873593u, 0xCC9E2D51u, 0x5BD1E995u};
+
+uint32_t choose_bloom_mul(const std::vector<uint32_t> &keys, std::vector<uint32_t> &filter) {
+    const auto &bg = background_grams();
+    std::set<uint32_t> kset(keys.begin(), keys.end());
+    size_t best_fp = SIZE_MAX; uint32_t best = kBloomMuls[0];
+    for (uint32_t mul : kBloomMuls) {
+        std::fill(filter.begin(), filter.end(), 0u);
+        for (uint32_t k : keys) { const BloomProbe b = bloom_probe(k, mul); filter[b.block] |= b.mask; }
+        size_t fp = 0;
+        for (uint32_t g : bg) {
+            if (kset.count(g)) continue;
+            const BloomProbe b = bloom_probe(g, mul);
+            fp += (filter[b.block] & b.mask) == b.mask;
+        }
+        if (fp < best_fp) { best_fp = fp; best = mul; }
+    }
+    std::fill(filter.begin(), filter.end(), 0u);
+    for (uint32_t k : keys) { const BloomProbe b = bloom_probe(k, best); filter[b.block] |= b.mask; }
+    return best;
 }
 
 }  // namespace
@@ -936,15 +985,17 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     std::vector<LitE> lits;
     std::vector<DSigRegex> sregex;
     std::vector<uint32_t> always;
+    // one prefilter literal, keyed on its least probable 4-byte window
+    auto add_lit = [&](const std::string &pat, const std::string &bytes, uint32_t id, uint8_t flags, uint8_t zones) {
+        const uint16_t ko = rarest_window(pat);
+        lits.push_back(LitE{fold4(load4(pat, ko)), DLit{id, 0, (uint16_t)bytes.size(), flags, zones, ko, 0}, bytes});
+    };
     for (size_t r = 0; r < sig.size(); r++) {
         const SigRule &g = sig[r];
         if (g.lit) {
             if (g.pat.size() < 4 || g.pat.size() > 0xFFFF) { st.n_rejected_other++; continue; }
             std::string b = g.nocase ? lower(g.pat) : g.pat;
-            uint16_t ko = rarest_window(g.pat);
-            LitE e{fold4(load4(g.pat, ko)), DLit{(uint32_t)r, 0, (uint16_t)b.size(),
-                                                 (uint8_t)(g.nocase ? LIT_NOCASE : 0), (uint8_t)g.zones, ko, 0}, b};
-            lits.push_back(e);
+            add_lit(g.pat, b, (uint32_t)r, (uint8_t)(g.nocase ? LIT_NOCASE : 0), (uint8_t)g.zones);
             st.n_sig_literals++;
         } else {
             RegexInfo ri = compile_regex(g.pat, g.nocase);
@@ -959,24 +1010,15 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             if (ri.prefix_mode) {
                 sr.mode = RXM_PREFIX;
                 sr.adfa = (uint32_t)C.add_dfa(ri.anchored);
-                for (auto &f : ri.prefix) {
-                    uint16_t ko = rarest_window(f);
-                    LitE e{fold4(load4(f, ko)), DLit{ridx, 0, (uint16_t)f.size(),
-                                                     (uint8_t)(LIT_NOCASE | LIT_TRIGGER | LIT_PREFIX),
-                                                     (uint8_t)g.zones, ko, 0}, f};
-                    lits.push_back(e);
-                }
+                for (auto &f : ri.prefix)
+                    add_lit(f, f, ridx, (uint8_t)(LIT_NOCASE | LIT_TRIGGER | LIT_PREFIX), (uint8_t)g.zones);
             } else if (ri.min_factor < 4) {
                 sr.mode = RXM_ALWAYS;
                 always.push_back(ridx);
                 st.n_sig_regex_always++;
             } else {
-                for (auto &f : ri.factors) {
-                    uint16_t ko = rarest_window(f);
-                    LitE e{fold4(load4(f, ko)), DLit{ridx, 0, (uint16_t)f.size(), (uint8_t)(LIT_NOCASE | LIT_TRIGGER),
-                                                     (uint8_t)g.zones, ko, 0}, f};
-                    lits.push_back(e);
-                }
+                for (auto &f : ri.factors)
+                    add_lit(f, f, ridx, (uint8_t)(LIT_NOCASE | LIT_TRIGGER), (uint8_t)g.zones);
             }
             sregex.push_back(sr);
         }
@@ -986,23 +1028,21 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         return a.key != b.key ? a.key < b.key : a.lit.id < b.lit.id;
     });
     std::vector<DLit> dlits;
-    uint32_t bloom_log2 = BLOOM_WORDS_LOG2_DEFAULT;
-    if (const char *ev = getenv("GM_BLOOM_LOG2")) bloom_log2 = atoi(ev) == 13 ? 13 : 14;   // tuning knob
-    std::vector<uint64_t> waf_a((size_t)1 << bloom_log2, 0);
+    std::vector<uint32_t> waf_a(BLOOM_WORDS, 0);   // LDS Bloom image
     std::vector<uint32_t> waf_b(4, 0);   // unused (kept for layout stability)
     std::vector<std::pair<uint32_t, std::pair<uint32_t, uint32_t>>> buckets;
+    std::vector<uint32_t> keys;
     for (size_t i = 0; i < lits.size(); i++) {
         LitE &e = lits[i];
         e.lit.bytes_off = C.put_bytes(e.bytes);
         dlits.push_back(e.lit);
         if (i == 0 || lits[i - 1].key != e.key) {
             buckets.push_back({e.key, {(uint32_t)i, 0}});
-            uint32_t wd, bb[BLOOM_K];
-            bloom_probe_rt(bloom_log2, e.key, wd, bb);
-            for (int q = 0; q < BLOOM_K; q++) waf_a[wd] |= 1ull << bb[q];
+            keys.push_back(e.key);
         }
         buckets.back().second.second++;
     }
+    const uint32_t bloom_mul = keys.empty() ? kBloomMuls[0] : choose_bloom_mul(keys, waf_a);
     uint32_t lcap = pow2_at_least(buckets.size() * 2 + 1);
     std::vector<DLitBucket> ltab(lcap, DLitBucket{0, 0, 0, 0});
     for (auto &b : buckets) {
@@ -1015,7 +1055,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     st.n_servers = (uint32_t)M.servers.size();
     st.n_locations = (uint32_t)M.locs.size();
     st.n_counters = st.n_locations + st.n_sigs;
-    st.lds_bytes_scan = ((size_t)8 << bloom_log2);
+    st.lds_bytes_scan = SCAN_LDS_BYTES;
 
     // ---- image
     Image I;
@@ -1048,7 +1088,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_bytes = I.put(C.bytes);
     I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
     h.total = I.buf.size();
-    h.bloom_log2 = bloom_log2;
+    h.bloom_log2 = BLOOM_LOG2; h.bloom_mul = bloom_mul;
     memcpy(I.buf.data(), &h, sizeof h);
     st.table_bytes = h.total;
     R.image = std::move(I.buf);
@@ -1092,7 +1132,7 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;
     t.n_locs = h.n_locs; t.n_sigs = h.n_sigs; t.n_sig_regex = h.n_sig_regex; t.n_always = h.n_always;
     t.n_lits = h.n_lits;
-    t.bloom_log2 = h.bloom_log2;
+    t.bloom_log2 = h.bloom_log2; t.bloom_mul = h.bloom_mul;
     t.gen = gen;
     return t;
 }

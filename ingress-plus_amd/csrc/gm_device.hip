@@ -614,10 +614,6 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
             hipHostMalloc((void **)&c->h_status, STATUS_WORDS * 4, hipHostMallocDefault) != hipSuccess) {
             t_err = "status alloc failed"; delete c; return nullptr;
         }
-        (void)hipFuncSetAttribute((const void *)k_waf_scan<13>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  scan_lds_bytes<13>());
-        (void)hipFuncSetAttribute((const void *)k_waf_scan<14>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  scan_lds_bytes<14>());
         if (flags & GM_CREATE_PROFILE)
             for (auto &e : c->ev) (void)hipEventCreate(&e);
     }
@@ -715,9 +711,9 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
 
     const size_t ccap = alen / 64 + 65536, pcap = (size_t)n * 2 + 65536, jcap = (size_t)n + 65536;
     int e;
-    // persistent scan grid: two 1024-thread workgroups per CU (64 KiB LDS Bloom filter each);
+    // persistent scan grid: one 1024-thread workgroup per CU (144 KiB LDS prefilter);
     // every wave owns a contiguous arena range and a private candidate region of wcap entries
-    const uint32_t scan_blocks = (uint32_t)c->cu_count * (t.bloom_log2 == 14 ? 1 : 2);
+    const uint32_t scan_blocks = (uint32_t)c->cu_count;
     const uint32_t W = scan_blocks * SCAN_WAVES;
     if ((e = grow(c, c->d_cand, c->cap_cand, std::max<size_t>(ccap, (size_t)W * 1024)))) return e;
     if ((e = grow(c, c->d_ccnt, c->cap_ccnt, W))) return e;
@@ -727,10 +723,7 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
     { size_t cj = c->cap_jobs; if ((e = grow(c, c->d_jobs, cj, jcap))) return e;
       size_t cj2 = c->cap_jobs; if ((e = grow(c, c->d_jobs2, cj2, jcap))) return e; c->cap_jobs = std::max(cj, cj2); }
 
-    if (t.bloom_log2 == 14)
-        k_waf_scan<14><<<scan_blocks, SCAN_BLOCK, scan_lds_bytes<14>(), s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
-    else
-        k_waf_scan<13><<<scan_blocks, SCAN_BLOCK, scan_lds_bytes<13>(), s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
+    k_waf_scan<<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
     HIPCHK(c, hipGetLastError());
     if (mark(2)) return GM_E_HIP;
     k_waf_verify<<<W, 256, 0, s>>>(A, alen, reqs, n, c->d_blk2rec, t, c->d_cand, wcap, c->d_ccnt, W, c->d_pairs,
@@ -888,4 +881,21 @@ extern "C" int gm_debug_waf_keys(gm_ctx *c, uint32_t *out, size_t cap) {
     for (uint32_t i = 0; i < h.n_lit_buckets_cap; i++)
         if (b[i].count) { if (k < cap) out[k] = b[i].key; k++; }
     return (int)k;
+}
+
+// Host restatement of k_waf_scan's candidate rule over `len` arena bytes (same tables, same
+// hashes): the CPU tests use it to check that every literal occurrence is a candidate and to
+// measure the prefilter's false-positive rate without a GPU.
+extern "C" int64_t gm_debug_waf_prefilter(gm_ctx *c, const uint8_t *A, size_t len, uint64_t *out, size_t cap) {
+    if (!c || !c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
+    const TabHeader &h = c->gen->hdr;
+    const uint32_t *bloom = (const uint32_t *)(c->gen->host_image.data() + h.off_waf_a);
+    int64_t k = 0;
+    for (size_t p = 0; p + 4 <= len; p++) {
+        uint32_t w;
+        memcpy(&w, A + p, 4);
+        const BloomProbe b = bloom_probe(fold4(w), h.bloom_mul);
+        if ((bloom[b.block] & b.mask) == b.mask) { if ((size_t)k < cap && out) out[k] = p; k++; }
+    }
+    return k;
 }

@@ -126,10 +126,14 @@ struct DDfa {
 };
 
 // ---- WAF signatures ----------------------------------------------------------------------
-// blocked Bloom filter in LDS: 2^13 (64 KiB, 2 WG/CU) or 2^14 (128 KiB, 1 WG/CU) 64-bit words,
-// BLOOM_K bits per key inside one word (one ds_read_b64 per probed byte position)
-constexpr int BLOOM_WORDS_LOG2_DEFAULT = 14;
-constexpr int BLOOM_K = 6;
+// WAF prefilter: a blocked Bloom filter of the folded 4-byte key windows (one window per
+// literal), resident in LDS for the whole scan -- 2^BLOOM_LOG2 32-bit blocks = 128 KiB, one
+// 1024-thread workgroup per CU.  Every arena offset is probed: one ds_read_b32 and BLOOM_PK
+// packed 16-bit shifts (2 bits each) per byte position.
+constexpr int BLOOM_LOG2 = 15;
+constexpr int BLOOM_PK = 3;          // K = 2 * BLOOM_PK bits per key
+constexpr uint32_t BLOOM_WORDS = 1u << BLOOM_LOG2;
+constexpr uint32_t SCAN_LDS_BYTES = 4u * BLOOM_WORDS;
 constexpr int CAND_SHARDS = 64;      // candidate-list shards (one atomic tail per shard)
 constexpr int BLK_SHIFT = 10;        // arena block (1 KiB) -> first record index (blk2rec)
 
@@ -165,8 +169,8 @@ struct TabHeader {
              off_rtargets, off_splits, off_parts, off_dfas, off_dfa_trans, off_dfa_acc, off_dfa_cls,
              off_bytes, off_waf_a, off_waf_b, off_lit_buckets, off_lits, off_sig_regex, off_always;
     uint64_t total;
-    uint32_t bloom_log2;     // Bloom words log2 (13 or 14)
-    uint32_t pad_end;
+    uint32_t bloom_log2;     // BLOOM_LOG2 the image was built for
+    uint32_t bloom_mul;      // Bloom hash multiplier (chosen per generation, see gm_compile.cpp)
 };
 
 struct GTab {                // device pointers, built on host from the image base
@@ -179,7 +183,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const uint8_t *bytes; const uint32_t *waf_a; const uint32_t *waf_b;
     const DLitBucket *lit_buckets; const DLit *lits; const DSigRegex *sig_regex; const uint32_t *always;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
-    uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2;
+    uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul;
     uint32_t gen;
 };
 
@@ -192,29 +196,25 @@ __host__ __device__ inline uint32_t name_hash_fin(uint32_t h, uint32_t port_idx)
 __host__ __device__ inline uint32_t edge_hash(uint32_t key) {
     uint32_t h = key * 0x9E3779B1u; return h ^ (h >> 15);
 }
-// blocked-Bloom probe of a folded 4-gram: word index (13 bits) and 4 bit positions (6 bits each)
-// from two multiply-xorshift rounds (multiplicative hashing: keep the TOP bits of the low word)
-template <int WL>
-__host__ __device__ inline void bloom_probe(uint32_t w, uint32_t &word, uint32_t (&b)[BLOOM_K]) {
-    uint32_t h1 = w * 0x9E3779B1u;
-    h1 ^= h1 >> 15;
-    uint32_t h2 = h1 * 0x85EBCA77u;
-    h2 ^= h2 >> 13;
-    word = h2 >> (32 - WL);
-    b[0] = (h2 >> 12) & 63; b[1] = (h2 >> 6) & 63; b[2] = h2 & 63;
-    b[3] = h1 >> 26; b[4] = (h1 >> 20) & 63; b[5] = (h1 >> 14) & 63;
+// Bloom probe of a folded 4-gram w: p = w * mul (32x32 -> 64 bit).  Block = top BLOOM_LOG2 bits
+// of the low word (multiplicative hashing keeps the TOP bits); the bit positions come from the
+// high word, whose bits all depend on every input bit: BLOOM_PK packed shifts 1 << (hi >> 4q),
+// each setting one bit in each 16-bit half (v_pk_lshlrev_b16: bits [0..3] and [16..19]).
+struct BloomProbe { uint32_t block, mask; };
+__host__ __device__ inline uint32_t pk_bits(uint32_t x) {
+    return (1u << (x & 15)) | (1u << (16 + ((x >> 16) & 15)));
 }
-__host__ __device__ inline void bloom_probe_rt(uint32_t wl, uint32_t w, uint32_t &word, uint32_t (&b)[BLOOM_K]) {
-    if (wl == 14) bloom_probe<14>(w, word, b); else bloom_probe<13>(w, word, b);
+__host__ __device__ inline BloomProbe bloom_probe(uint32_t w, uint32_t mul) {
+    const uint64_t p = (uint64_t)w * mul;
+    const uint32_t lo = (uint32_t)p, hi = (uint32_t)(p >> 32);
+    uint32_t m = 0;
+    for (int q = 0; q < BLOOM_PK; q++) m |= pk_bits(hi >> (4 * q));
+    return BloomProbe{lo >> (32 - BLOOM_LOG2), m};
 }
 __host__ __device__ inline uint32_t lit_bucket_hash(uint32_t w) { uint32_t h = w * 0xC2B2AE3Du; return h ^ (h >> 16); }
-__host__ __device__ inline uint32_t fold4(uint32_t w) {
-    // ASCII A-Z -> a-z on four packed bytes (SWAR)
-    uint32_t x = w & 0x7F7F7F7Fu;
-    uint32_t ge_a = (x + 0x3F3F3F3Fu) & 0x80808080u;   // byte >= 'A'
-    uint32_t gt_z = (x + 0x25252525u) & 0x80808080u;   // byte >  'Z'
-    uint32_t up = ge_a & ~gt_z & ~w & 0x80808080u;     // high bit clear in the original byte
-    return w | (up >> 2);
-}
+// Prefilter fold: OR 0x20 into every byte.  Maps A-Z onto a-z (so case-insensitive keys match)
+// and merges a few other byte pairs (0x40/0x60, 0x00-0x1F/0x20-0x3F, ...); the merge only adds
+// prefilter candidates -- k_waf_verify compares the literal bytes exactly (lc() for nocase).
+__host__ __device__ inline uint32_t fold4(uint32_t w) { return w | 0x20202020u; }
 
 }  // namespace gm
