@@ -94,6 +94,30 @@ def test_waf_edge_cases(eng):
     assert got[6]["n_hits"] == 0 and got[8]["n_hits"] == 0
 
 
+def test_waf_scan_every_alignment(eng):
+    """Literals planted at every residue mod 1024 of the arena (every lane of a scan wave, every
+    byte of a lane, windows straddling lanes 62/63 and chunk ends) plus one ending exactly at the
+    arena's last byte."""
+    rules = [sigs.Rule("lit", True, "b", b"qzxjv"), sigs.Rule("lit", False, "b", b"WXYZ"),
+             sigs.Rule("re", True, "b", r"kqpz=[0-9]{3}")]
+    b = workloads.c4_blob(sigs.SigSet(rules))
+    rng = np.random.Generator(np.random.PCG64(7))
+    items = []
+    pos = 0
+    for i in range(3000):
+        tok = [b"QzXjV", b"WXYZ", b"kqpz=123"][i % 3]
+        blen = int(rng.integers(16, 2200))
+        at = int(rng.integers(0, blen - len(tok)))
+        body = bytearray(b"a" * blen)
+        body[at:at + len(tok)] = tok
+        items.append({"host": "cafe.example.com", "uri": "/tea/x", "https": True, "body": bytes(body)})
+    items.append({"host": "cafe.example.com", "uri": "/tea/x", "https": True, "body": b"aaaqzxjv"})
+    reqs, arena = records.from_dicts(items)
+    got, gh, exp, eh = run_both(eng, b, reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "alignment")
+    assert (exp["n_hits"] == 1).sum() == len(items)
+
+
 def test_e2e_kats_on_gpu(eng):
     adv = golden("advanced_routing.json")
     for case in adv["cases"]:

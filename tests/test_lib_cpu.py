@@ -121,3 +121,43 @@ def test_c4_signature_set_compiles():
     assert s["n_sigs"] == 1000 and s["n_sig_literals"] == 800 and s["n_sig_regex"] == 200
     assert s["n_rejected_pcre"] == 0 and s["n_rejected_other"] == 0
     assert s["n_sig_regex_always"] == 0
+
+
+def _prefilter(e, arena):
+    L = ctypes.CDLL(engine.LIB_PATH)
+    L.gm_debug_waf_prefilter.restype = ctypes.c_int64
+    L.gm_debug_waf_prefilter.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                         ctypes.c_size_t]
+    a = np.ascontiguousarray(arena)
+    n = L.gm_debug_waf_prefilter(e.h, a.ctypes.data, a.size, None, 0)
+    out = np.zeros(max(n, 1), np.uint64)
+    L.gm_debug_waf_prefilter(e.h, a.ctypes.data, a.size, out.ctypes.data, n)
+    return out[:n]
+
+
+def test_prefilter_covers_every_literal_occurrence():
+    """Host restatement of the scan kernel's candidate rule: every occurrence of every literal
+    (any case for nocase rules) yields a candidate inside the occurrence, and the false-positive
+    rate on the C4 traffic stays small."""
+    from gpumatch import records
+    ss = workloads.c4_sigset(800, 200)
+    e = engine.Engine(compile_only=True)
+    e.load(workloads.c4_blob(ss), 3)
+    reqs, arena = records.gen_c4(3000, ss, plant_rate=0.3)
+    cand = np.sort(_prefilter(e, arena))
+    a = bytes(arena)
+    al = a.lower()
+    checked = 0
+    for r in ss.rules:
+        if r.kind != "lit":
+            continue
+        pat = bytes(r.pattern)
+        hay, needle = (al, pat.lower()) if r.nocase else (a, pat)
+        start = hay.find(needle)
+        while start >= 0:
+            k = np.searchsorted(cand, start)
+            assert k < len(cand) and cand[k] <= start + len(pat) - 4, (pat, start)
+            checked += 1
+            start = hay.find(needle, start + 1)
+    assert checked > 200
+    assert len(cand) < len(a) * 2e-3
