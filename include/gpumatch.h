@@ -9,7 +9,7 @@
  *
  * A Go wrapper `gpumatch.Manager{inner nginx.Manager}` binds these entry
  * points through cgo:
- *   - CreateMainConfig/CreateConfig/DeleteConfig (manager.go:108-134) -> cached in the wrapper,
+ *   - CreateMainConfig/CreateConfig/DeleteConfig (manager.go:97-129) -> cached in the wrapper,
  *     serialised into a generation blob (GMB1 format below) at Reload time;
  *   - Reload (manager.go:201-225)        -> gm_load_generation(ctx, blob, len, configVersion);
  *   - the nginx worker's per-request classification (external binary; templates

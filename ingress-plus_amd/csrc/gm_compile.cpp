@@ -913,6 +913,21 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                         if (d < 0) x.op = 0xFF;
                         else { x.op = (f.op == 3 || f.op == 4) ? 5 : 6; x.val_off = (uint32_t)d; }
                     }
+                    const DSrc &ds = C.srcs[s];
+                    if (ds.kind == SRC_VAR && (ds.var == V_SCHEME || ds.var == V_HTTPS || ds.var == V_HTTP2) &&
+                        (x.op == 4 || x.op == SIF_EQ || x.op == SIF_NE)) {
+                        // value per (https, http2) -- get_var's V_SCHEME / V_HTTPS / V_HTTP2 cases
+                        uint32_t tt = 0;
+                        for (uint32_t fl = 0; fl < 4; fl++) {
+                            const bool https = fl & GM_REQ_HTTPS, h2 = fl & GM_REQ_HTTP2;
+                            const std::string v = ds.var == V_SCHEME ? (https ? "https" : "http")
+                                                  : ds.var == V_HTTPS ? (https ? "on" : "") : (h2 ? "h2" : "");
+                            const bool hit = x.op == 4 ? (!v.empty() && v != "0")
+                                             : x.op == SIF_EQ ? v == f.val : v != f.val;
+                            if (hit) tt |= 1u << fl;
+                        }
+                        x.op = SIF_FLAGS; x.tt = tt;
+                    }
                 }
             }
             sifs.push_back(x);

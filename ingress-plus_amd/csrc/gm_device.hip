@@ -348,11 +348,151 @@ struct RouteOut {
     uint16_t waf;
 };
 
-__device__ void route_one(const uint8_t *A, const Rec &r, const GTab &t, RouteOut &o) {
-    o.server = GM_NONE; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0;
-    o.action = GM_ACT_NO_LISTENER; o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF;
+// 32 arena bytes starting at `off` (any alignment) as 8 little-endian dwords, from three aligned
+// 16-B loads; blocks starting at or beyond `lim` are not read (zero).  Callers mask by length.
+__device__ __forceinline__ void load_span32(const uint8_t *A, uint64_t off, uint64_t lim, uint32_t (&w)[8]) {
+    const uint64_t a = off & ~15ull;
+    uint32_t d[12];
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+        uint4 q = make_uint4(0, 0, 0, 0);
+        if (a + 16 * b < lim) q = *reinterpret_cast<const uint4 *>(A + a + 16 * b);
+        d[4 * b] = q.x; d[4 * b + 1] = q.y; d[4 * b + 2] = q.z; d[4 * b + 3] = q.w;
+    }
+    const uint32_t r = (uint32_t)(off & 15), qd = r >> 2, sh = r & 3;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t lo = qd == 0 ? d[k] : qd == 1 ? d[k + 1] : qd == 2 ? d[k + 2] : d[k + 3];
+        const uint32_t hi = qd == 0 ? d[k + 1] : qd == 1 ? d[k + 2] : qd == 2 ? d[k + 3] : d[k + 4];
+        w[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    }
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[8], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xFF; }
+
+// Host of <= 32 bytes held in registers: validate_host + exact-name probe (the common case).
+// Returns the normalised length (-1 = invalid) and the exact-table server (GM_NONE = miss).
+__device__ __forceinline__ int host_fast(const uint32_t (&hw)[8], uint32_t n, const GTab &t, uint32_t pi,
+                                         uint32_t &server) {
+    server = GM_NONE;
+    int dot_pos = (int)n, host_len = (int)n, state = 0;
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        if (i < (int)n) {
+            const uint32_t ch = byte_of(hw, i);
+            if (ch == '.') { bad |= dot_pos == i - 1; dot_pos = i; }
+            else if (ch == ':') { if (state == 0) { host_len = i; state = 2; } }
+            else if (ch == '[') { if (i == 0) state = 1; }
+            else if (ch == ']') { if (state == 1) { host_len = i + 1; state = 2; } }
+            else if (ch == 0 || ch == '/') bad = true;
+        }
+    }
+    if (dot_pos == host_len - 1) host_len--;
+    if (bad || host_len <= 0) return -1;
+    uint32_t hs = 2166136261u;
+#pragma unroll
+    for (int i = 0; i < 32; i++) if (i < host_len) hs = fnv1a_step(hs, lc(byte_of(hw, i)));
+    hs = name_hash_fin(hs, pi);
+    for (uint32_t i = hs & t.names_mask;; i = (i + 1) & t.names_mask) {
+        const DName e = t.names[i];
+        if (e.hash == 0) break;
+        if (e.hash == hs && e.port_idx == pi && e.name_len == (uint32_t)host_len) {
+            uint32_t tw[8];
+            load_span32(t.bytes, e.name_off, ~0ull, tw);   // the bytes pool ends with 64 B of slack
+            uint32_t diff = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int rem = host_len - 4 * k;
+                const uint32_t m = rem >= 4 ? 0xFFFFFFFFu : rem > 0 ? (1u << (8 * rem)) - 1 : 0u;
+                diff |= (lower4(hw[k]) ^ tw[k]) & m;
+            }
+            if (diff == 0) { server = e.server; break; }
+        }
+    }
+    return host_len;
+}
+
+// Wildcard names (*.x / .x, then x.*) for a host that missed the exact table; byte-wise over
+// the arena (rare path).
+__device__ __noinline__ uint32_t host_wildcards(const uint8_t *h, int hl, const GTab &t, uint32_t pi) {
+    uint32_t s = GM_NONE;
+    uint32_t w = name_probe(t.wild_head, t.wild_head_mask, t.bytes, h, 0, (uint32_t)hl, pi);
+    if (w != GM_NONE && (w & 0x80000000u)) s = w & 0x7FFFFFFFu;      // ".x" matches x itself
+    for (int d = 0; s == GM_NONE && d < hl; d++)
+        if (h[d] == '.') {
+            w = name_probe(t.wild_head, t.wild_head_mask, t.bytes, h, d + 1, (uint32_t)(hl - d - 1), pi);
+            if (w != GM_NONE) s = w & 0x7FFFFFFFu;
+        }
+    for (int d = hl - 2; s == GM_NONE && d > 0; d--)
+        if (h[d] == '.') s = name_probe(t.wild_tail, t.wild_tail_mask, t.bytes, h, 0, (uint32_t)d, pi);
+    return s;
+}
+
+// Generic (variable-reading) steps live in non-inlined functions so that the Ctx / Val
+// lane-private arrays only exist on these paths (scratch), never on the host/URI fast path.
+// server rewrite `if` on a request variable: 1 hit, 0 miss
+__device__ __noinline__ int server_if_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t if_idx) {
+    const Rec r = load_rec(rp);
+    const DServerIf f = t.server_ifs[if_idx];
     Ctx c;
     ctx_init(c, A, r);
+    Val v;
+    get_var(c, t, f.src, v);
+    if (f.op == SIF_EQ) return val_eq(v, t.bytes + f.val_off, f.val_len, false);
+    if (f.op == SIF_NE) return !val_eq(v, t.bytes + f.val_off, f.val_len, false);
+    if (f.op == 4) return v.total && !(v.total == 1 && v.p[0][0] == '0');
+    const bool m = dfa_run_val(t, f.val_off, v);
+    return f.op == 5 ? m : !m;
+}
+
+// rules route (compiled map chains) -> result index (0xFF default)
+__device__ __noinline__ uint8_t rules_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t rules_idx) {
+    const Rec r = load_rec(rp);
+    const DRules R = t.rules[rules_idx];
+    Ctx c;
+    ctx_init(c, A, r);
+    Val v;
+    uint32_t bits = 0;
+    for (uint32_t ch = 0; ch < R.n_chains; ch++) {
+        int32_t nd = (int32_t)t.chain_heads[R.first_chain + ch];
+        int guard = 0;
+        while (nd >= 0 && guard++ < 64) {
+            const DCond cd = t.conds[nd];
+            get_var(c, t, cd.src, v);
+            bool m;
+            if (cd.is_regex) m = v.total > 0 && dfa_run_val(t, cd.dfa, v);
+            else m = val_eq(v, t.bytes + cd.key_off, cd.key_len, true);
+            nd = m ? cd.next_true : cd.next_false;
+        }
+        if (nd == NEXT_1) bits |= 1u << ch;
+    }
+    return t.rtab[R.table_off + bits];
+}
+
+// split_clients: murmur2 of the source -> part index (0xFF none, 0xFFFFFFFF unsupported value)
+__device__ __noinline__ uint32_t split_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t split_idx) {
+    const Rec r = load_rec(rp);
+    const DSplit Sp = t.splits[split_idx];
+    Ctx c;
+    ctx_init(c, A, r);
+    Val v;
+    get_var(c, t, Sp.src, v);
+    uint8_t buf[64];
+    bool ok;
+    const uint32_t hsh = murmur2_val(v, buf, ok);
+    if (!ok) return 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < Sp.n_parts; k++) {
+        const DPart pt = t.parts[Sp.first_part + k];
+        if (hsh < pt.bound || pt.star) return k;
+    }
+    return 0xFFu;
+}
+
+__device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const GTab &t, RouteOut &o) {
+    o.server = GM_NONE; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0;
+    o.action = GM_ACT_NO_LISTENER; o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF;
+    const uint64_t f_uri = r.base, f_host = r.base + r.uri_len + r.args_len + r.hdr_len + r.body_len;
     // ---- listen port
     uint32_t pi = GM_NONE;
     for (uint32_t i = 0; i < t.n_ports; i++) if (t.ports[i].port == r.port) { pi = i; break; }
@@ -364,22 +504,19 @@ __device__ void route_one(const uint8_t *A, const Rec &r, const GTab &t, RouteOu
     // ---- host -> server (exact > *.x/.x > x.*)
     bool bad = false;
     if (r.host_len) {
-        const uint8_t *h = A + c.host;
-        int hl = validate_host(h, r.host_len);
+        uint32_t s = GM_NONE;
+        int hl;
+        if (r.host_len <= 32) {
+            uint32_t hw[8];
+            load_span32(A, f_host, alen, hw);
+            hl = host_fast(hw, r.host_len, t, pi, s);
+        } else {
+            hl = validate_host(A + f_host, r.host_len);
+            if (hl >= 0) s = name_probe(t.names, t.names_mask, t.bytes, A + f_host, 0, (uint32_t)hl, pi);
+        }
         if (hl < 0) bad = true;
         else {
-            uint32_t s = name_probe(t.names, t.names_mask, t.bytes, h, 0, (uint32_t)hl, pi);
-            if (s == GM_NONE) {
-                uint32_t w = name_probe(t.wild_head, t.wild_head_mask, t.bytes, h, 0, (uint32_t)hl, pi);
-                if (w != GM_NONE && (w & 0x80000000u)) s = w & 0x7FFFFFFFu;      // ".x" matches x itself
-                for (int d = 0; s == GM_NONE && d < hl; d++)
-                    if (h[d] == '.') {
-                        w = name_probe(t.wild_head, t.wild_head_mask, t.bytes, h, d + 1, (uint32_t)(hl - d - 1), pi);
-                        if (w != GM_NONE) s = w & 0x7FFFFFFFu;
-                    }
-                for (int d = hl - 2; s == GM_NONE && d > 0; d--)
-                    if (h[d] == '.') s = name_probe(t.wild_tail, t.wild_tail_mask, t.bytes, h, 0, (uint32_t)d, pi);
-            }
+            if (s == GM_NONE) s = host_wildcards(A + f_host, hl, t, pi);
             if (s != GM_NONE) sid = s;
         }
     }
@@ -387,23 +524,20 @@ __device__ void route_one(const uint8_t *A, const Rec &r, const GTab &t, RouteOu
     if (bad || (P.ssl && !https)) { o.action = GM_ACT_BAD_REQUEST; o.status = 400; return; }
     const DServer S = t.servers[sid];
     // ---- server rewrite phase
-    Val v;
     for (uint32_t i = 0; i < S.n_if; i++) {
         const DServerIf f = t.server_ifs[S.first_if + i];
         bool hit;
         if (f.op == SIF_RETURN) hit = true;
+        else if (f.op == SIF_FLAGS) hit = (f.tt >> (r.flags & 3)) & 1u;
         else if (f.op == 0xFF) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; return; }
-        else {
-            get_var(c, t, f.src, v);
-            if (f.op == SIF_EQ) hit = val_eq(v, t.bytes + f.val_off, f.val_len, false);
-            else if (f.op == SIF_NE) hit = !val_eq(v, t.bytes + f.val_off, f.val_len, false);
-            else if (f.op == 4) hit = v.total && !(v.total == 1 && v.p[0][0] == '0');
-            else { bool m = dfa_run_val(t, f.val_off, v); hit = f.op == 5 ? m : !m; }
-        }
+        else hit = server_if_generic(A, rp, t, S.first_if + i) != 0;
         if (hit) { o.action = is_redirect(f.code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = f.code; return; }
     }
-    // ---- location: trie walk (exact, longest prefix, auto_redirect), then regex locations
-    const uint8_t *u = A + c.uri;
+    // ---- location: trie walk (exact, longest prefix, auto_redirect), then regex locations.
+    // The first 32 URI bytes come from registers (a window shifted one dword per 4 bytes).
+    const uint8_t *u = A + f_uri;
+    uint32_t uw[8];
+    load_span32(A, f_uri, alen, uw);
     uint32_t node = S.trie_root;
     int32_t best = -1;
     uint32_t i = 0;
@@ -411,7 +545,19 @@ __device__ void route_one(const uint8_t *A, const Rec &r, const GTab &t, RouteOu
         const DNode nd = t.nodes[node];
         if (nd.prefix_loc >= 0) best = nd.prefix_loc;
         if (i == r.uri_len) break;
-        uint32_t key = node * 256u + u[i] + 1u;
+        uint32_t b;
+        if (i < 32) {
+            b = uw[0] & 0xFF;
+            uw[0] >>= 8;
+            if ((i & 3) == 3) {
+#pragma unroll
+                for (int k = 0; k < 7; k++) uw[k] = uw[k + 1];
+                uw[7] = 0;
+            }
+        } else {
+            b = u[i];
+        }
+        const uint32_t key = node * 256u + b + 1u;
         uint32_t slot = edge_hash(key) & t.edges_mask, child = GM_NONE;
         for (;; slot = (slot + 1) & t.edges_mask) {
             const DEdge e = t.edges[slot];
@@ -432,7 +578,6 @@ __device__ void route_one(const uint8_t *A, const Rec &r, const GTab &t, RouteOu
         else {
             for (uint32_t k = 0; k < S.n_rloc && loc < 0; k++) {
                 const DRegexLoc rl = t.rlocs[S.first_rloc + k];
-                Val uv; uv.clear(); uv.add(u, r.uri_len);
                 if (dfa_run_bytes(t, rl.dfa, u, r.uri_len)) loc = (int32_t)rl.loc;
             }
             if (loc < 0) loc = best;
@@ -444,35 +589,15 @@ __device__ void route_one(const uint8_t *A, const Rec &r, const GTab &t, RouteOu
     uint32_t fin = (uint32_t)loc;
     if (L.kind == LK_IRL_RULES) {
         const DRules R = t.rules[L.route];
-        uint32_t bits = 0;
-        for (uint32_t ch = 0; ch < R.n_chains; ch++) {
-            int32_t nd = (int32_t)t.chain_heads[R.first_chain + ch];
-            int guard = 0;
-            while (nd >= 0 && guard++ < 64) {
-                const DCond cd = t.conds[nd];
-                get_var(c, t, cd.src, v);
-                bool m;
-                if (cd.is_regex) m = v.total > 0 && dfa_run_val(t, cd.dfa, v);
-                else m = val_eq(v, t.bytes + cd.key_off, cd.key_len, true);
-                nd = m ? cd.next_true : cd.next_false;
-            }
-            if (nd == NEXT_1) bits |= 1u << ch;
-        }
-        uint8_t idx = t.rtab[R.table_off + bits];
+        const uint8_t idx = rules_generic(A, rp, t, L.route);
         o.kind = GM_ROUTE_RULES; o.match = idx;
         fin = idx == 0xFF ? R.default_target : t.rtargets[R.first_target + idx];
     } else if (L.kind == LK_IRL_SPLIT) {
-        const DSplit Sp = t.splits[L.route];
-        get_var(c, t, Sp.src, v);
-        uint8_t buf[64]; bool ok;
-        uint32_t hsh = murmur2_val(v, buf, ok);
         o.kind = GM_ROUTE_SPLIT;
+        const uint32_t k = split_generic(A, rp, t, L.route);
+        if (k == 0xFFFFFFFFu) { o.action = GM_ACT_UNSUPPORTED; return; }
         fin = GM_NONE;
-        if (!ok) { o.action = GM_ACT_UNSUPPORTED; return; }
-        for (uint32_t k = 0; k < Sp.n_parts; k++) {
-            const DPart pt = t.parts[Sp.first_part + k];
-            if (hsh < pt.bound || pt.star) { o.bucket = (uint8_t)k; fin = pt.target; break; }
-        }
+        if (k != 0xFFu) { o.bucket = (uint8_t)k; fin = t.parts[t.splits[L.route].first_part + k].target; }
     } else if (L.kind == LK_UNSUPPORTED) {
         o.action = GM_ACT_UNSUPPORTED; return;
     }
@@ -503,7 +628,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) void k_route(const gm_req *__restrict_
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const Rec r = load_rec(reqs + i);
         RouteOut o;
-        route_one(A, r, t, o);
+        route_one(A, arena_len, reqs + i, r, t, o);
         uint4 w0, w1;
         w0.x = t.gen; w0.y = o.server; w0.z = o.loc; w0.w = o.ups;
         w1.x = (uint32_t)o.action | ((uint32_t)o.kind << 8) | ((uint32_t)o.bucket << 16) | ((uint32_t)o.match << 24);
@@ -512,9 +637,17 @@ __global__ __launch_bounds__(ROUTE_BLOCK) void k_route(const gm_req *__restrict_
         w1.w = o.status;
         uint4 *dst = reinterpret_cast<uint4 *>(out + i);
         dst[0] = w0; dst[1] = w1;
-        if (o.loc != GM_NONE) {
-            if (use_hist) atomicAdd(&hist[o.loc], 1u);
-            else atomicAdd(&counters[o.loc], 1ull);
+        // per-location counter, aggregated over the wave: one atomic per distinct location
+        unsigned long long todo = __ballot(o.loc != GM_NONE);
+        while (todo) {
+            const int leader = __ffsll(todo) - 1;
+            const uint32_t lk = __shfl(o.loc, leader);
+            const unsigned long long same = __ballot(o.loc == lk) & todo;
+            if ((threadIdx.x & 63) == (uint32_t)leader) {
+                if (use_hist) atomicAdd(&hist[lk], (uint32_t)__popcll(same));
+                else atomicAdd(&counters[lk], (unsigned long long)__popcll(same));
+            }
+            todo &= ~same;
         }
         if (blk2rec) {
             // blocks whose start lies in [base_i, base_{i+1}) belong to record i

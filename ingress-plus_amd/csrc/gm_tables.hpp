@@ -36,7 +36,9 @@ struct DName {
     uint32_t server;
 };
 
-enum : uint32_t { SIF_EQ = 1, SIF_NE = 2, SIF_RETURN = 3 };
+// SIF_FLAGS: the variable depends only on (https, http2) -- $scheme, $https, $http2 -- so the
+// compiler evaluates the condition for the 4 flag combinations: hit = tt >> (flags & 3) & 1.
+enum : uint32_t { SIF_EQ = 1, SIF_NE = 2, SIF_RETURN = 3, SIF_FLAGS = 7 };
 struct DServer {
     uint32_t trie_root;      // node index of this server's location trie
     uint32_t first_if, n_if; // server rewrite-phase `if (...) { return }` list (DServerIf)
@@ -49,7 +51,8 @@ struct DServerIf {
     uint32_t src;            // DSrc index (variable), unused for SIF_RETURN
     uint32_t val_off, val_len;  // literal (case-sensitive compare, ngx_http_script_equal_code)
     uint32_t code;           // return code
-    uint32_t pad[3];
+    uint32_t tt;             // SIF_FLAGS truth table
+    uint32_t pad[2];
 };
 struct DRegexLoc { uint32_t dfa; uint32_t loc; };
 
@@ -216,5 +219,12 @@ __host__ __device__ inline uint32_t lit_bucket_hash(uint32_t w) { uint32_t h = w
 // and merges a few other byte pairs (0x40/0x60, 0x00-0x1F/0x20-0x3F, ...); the merge only adds
 // prefilter candidates -- k_waf_verify compares the literal bytes exactly (lc() for nocase).
 __host__ __device__ inline uint32_t fold4(uint32_t w) { return w | 0x20202020u; }
+// exact ASCII lowercase (A-Z only) of four packed bytes, SWAR
+__host__ __device__ inline uint32_t lower4(uint32_t w) {
+    const uint32_t x = w & 0x7F7F7F7Fu;
+    const uint32_t ge_a = (x + 0x3F3F3F3Fu) & 0x80808080u;   // byte >= 'A'
+    const uint32_t gt_z = (x + 0x25252525u) & 0x80808080u;   // byte >  'Z'
+    return w | ((ge_a & ~gt_z & ~w & 0x80808080u) >> 2);
+}
 
 }  // namespace gm

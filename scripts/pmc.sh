@@ -1,0 +1,22 @@
+#!/bin/bash
+# GPU box: PMC passes over a short bench run (one counter group per rocprofv3 run, kernel trace
+# only -- never combined with sys/runtime traces).  Output: gpurun_out/pmc_${TAG}_<pass>/.
+#   pass hbm: FETCH_SIZE, WRITE_SIZE is a separate pass (TCC slots)  -> roofline.traffic
+#   pass sq : instruction mix and wave stall cycles of the scan / route / verify kernels
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+TAG=${TAG:-r1}
+ARGS="--steps 2 --warmup 1 --no-cpu ${BENCH_ARGS}"
+cd /tmp && export TMPDIR=/tmp
+run() {
+  local name=$1; shift
+  timeout -k 10 600 rocprofv3 --kernel-trace --pmc "$@" --kernel-include-regex 'k_(waf|route|pairs)' \
+    -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_${TAG}_${name}" -o run --output-format csv \
+    -- python "$GRAFT_REPO_ROOT/bench.py" $ARGS > "$GRAFT_REPO_ROOT/gpurun_out/pmc_${TAG}_${name}.log" 2>&1
+  local rc=$?
+  echo "pmc pass $name rc=$rc"
+  return $rc
+}
+run fetch FETCH_SIZE &&
+run write WRITE_SIZE &&
+run sq SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU
