@@ -729,23 +729,23 @@ const uint32_t kBloomMuls[] = {0x9E3779B1u, 0x85EBCA77u, 0xC2B2AE3Du, 0x27D4EB2F
                                0xFD7046C5u, 0xB55A4F09u, 0x7FEB352Du, 0x846CA68Bu, 0x2C1B3C6Du, 0x297A2D39u,
                                0xE6546B64u | 1u, 0x1B873593u, 0xCC9E2D51u, 0x5BD1E995u};
 
-uint32_t choose_bloom_mul(const std::vector<uint32_t> &keys, std::vector<uint32_t> &filter) {
+uint32_t choose_bloom_mul(const std::vector<uint32_t> &keys, uint32_t pk, std::vector<uint32_t> &filter) {
     const auto &bg = background_grams();
     std::set<uint32_t> kset(keys.begin(), keys.end());
     size_t best_fp = SIZE_MAX; uint32_t best = kBloomMuls[0];
     for (uint32_t mul : kBloomMuls) {
         std::fill(filter.begin(), filter.end(), 0u);
-        for (uint32_t k : keys) { const BloomProbe b = bloom_probe(k, mul); filter[b.block] |= b.mask; }
+        for (uint32_t k : keys) { const BloomProbe b = bloom_probe(k, mul, pk); filter[b.block] |= b.mask; }
         size_t fp = 0;
         for (uint32_t g : bg) {
             if (kset.count(g)) continue;
-            const BloomProbe b = bloom_probe(g, mul);
+            const BloomProbe b = bloom_probe(g, mul, pk);
             fp += (filter[b.block] & b.mask) == b.mask;
         }
         if (fp < best_fp) { best_fp = fp; best = mul; }
     }
     std::fill(filter.begin(), filter.end(), 0u);
-    for (uint32_t k : keys) { const BloomProbe b = bloom_probe(k, best); filter[b.block] |= b.mask; }
+    for (uint32_t k : keys) { const BloomProbe b = bloom_probe(k, best, pk); filter[b.block] |= b.mask; }
     return best;
 }
 
@@ -1057,7 +1057,9 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         }
         buckets.back().second.second++;
     }
-    const uint32_t bloom_mul = keys.empty() ? kBloomMuls[0] : choose_bloom_mul(keys, waf_a);
+    uint32_t bloom_pk = BLOOM_PK_DEFAULT;
+    if (const char *ev = getenv("GM_BLOOM_PK")) bloom_pk = std::min(3, std::max(1, atoi(ev)));   // tuning knob
+    const uint32_t bloom_mul = keys.empty() ? kBloomMuls[0] : choose_bloom_mul(keys, bloom_pk, waf_a);
     uint32_t lcap = pow2_at_least(buckets.size() * 2 + 1);
     std::vector<DLitBucket> ltab(lcap, DLitBucket{0, 0, 0, 0});
     for (auto &b : buckets) {
@@ -1103,7 +1105,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_bytes = I.put(C.bytes);
     I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
     h.total = I.buf.size();
-    h.bloom_log2 = BLOOM_LOG2; h.bloom_mul = bloom_mul;
+    h.bloom_log2 = BLOOM_LOG2; h.bloom_mul = bloom_mul; h.bloom_pk = bloom_pk;
     memcpy(I.buf.data(), &h, sizeof h);
     st.table_bytes = h.total;
     R.image = std::move(I.buf);
@@ -1147,7 +1149,7 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;
     t.n_locs = h.n_locs; t.n_sigs = h.n_sigs; t.n_sig_regex = h.n_sig_regex; t.n_always = h.n_always;
     t.n_lits = h.n_lits;
-    t.bloom_log2 = h.bloom_log2; t.bloom_mul = h.bloom_mul;
+    t.bloom_log2 = h.bloom_log2; t.bloom_mul = h.bloom_mul; t.bloom_pk = h.bloom_pk;
     t.gen = gen;
     return t;
 }

@@ -856,7 +856,9 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
     { size_t cj = c->cap_jobs; if ((e = grow(c, c->d_jobs, cj, jcap))) return e;
       size_t cj2 = c->cap_jobs; if ((e = grow(c, c->d_jobs2, cj2, jcap))) return e; c->cap_jobs = std::max(cj, cj2); }
 
-    k_waf_scan<<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
+    if (t.bloom_pk == 1) k_waf_scan<1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
+    else if (t.bloom_pk == 2) k_waf_scan<2><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
+    else k_waf_scan<3><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
     HIPCHK(c, hipGetLastError());
     if (mark(2)) return GM_E_HIP;
     k_waf_verify<<<W, 256, 0, s>>>(A, alen, reqs, n, c->d_blk2rec, t, c->d_cand, wcap, c->d_ccnt, W, c->d_pairs,
@@ -1027,7 +1029,7 @@ extern "C" int64_t gm_debug_waf_prefilter(gm_ctx *c, const uint8_t *A, size_t le
     for (size_t p = 0; p + 4 <= len; p++) {
         uint32_t w;
         memcpy(&w, A + p, 4);
-        const BloomProbe b = bloom_probe(fold4(w), h.bloom_mul);
+        const BloomProbe b = bloom_probe(fold4(w), h.bloom_mul, h.bloom_pk);
         if ((bloom[b.block] & b.mask) == b.mask) { if ((size_t)k < cap && out) out[k] = p; k++; }
     }
     return k;

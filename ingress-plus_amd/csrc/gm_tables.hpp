@@ -131,10 +131,10 @@ struct DDfa {
 // ---- WAF signatures ----------------------------------------------------------------------
 // WAF prefilter: a blocked Bloom filter of the folded 4-byte key windows (one window per
 // literal), resident in LDS for the whole scan -- 2^BLOOM_LOG2 32-bit blocks = 128 KiB, one
-// 1024-thread workgroup per CU.  Every arena offset is probed: one ds_read_b32 and BLOOM_PK
+// 1024-thread workgroup per CU.  Every arena offset is probed: one ds_read_b32 and pk
 // packed 16-bit shifts (2 bits each) per byte position.
 constexpr int BLOOM_LOG2 = 15;
-constexpr int BLOOM_PK = 3;          // K = 2 * BLOOM_PK bits per key
+constexpr int BLOOM_PK_DEFAULT = 3;  // K = 2 * pk bits per key (pk = 1..3, per generation)
 constexpr uint32_t BLOOM_WORDS = 1u << BLOOM_LOG2;
 constexpr uint32_t SCAN_LDS_BYTES = 4u * BLOOM_WORDS;
 constexpr int CAND_SHARDS = 64;      // candidate-list shards (one atomic tail per shard)
@@ -174,6 +174,8 @@ struct TabHeader {
     uint64_t total;
     uint32_t bloom_log2;     // BLOOM_LOG2 the image was built for
     uint32_t bloom_mul;      // Bloom hash multiplier (chosen per generation, see gm_compile.cpp)
+    uint32_t bloom_pk;       // packed shifts per probe (K = 2 * bloom_pk)
+    uint32_t pad_end;
 };
 
 struct GTab {                // device pointers, built on host from the image base
@@ -186,7 +188,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const uint8_t *bytes; const uint32_t *waf_a; const uint32_t *waf_b;
     const DLitBucket *lit_buckets; const DLit *lits; const DSigRegex *sig_regex; const uint32_t *always;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
-    uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul;
+    uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk;
     uint32_t gen;
 };
 
@@ -201,17 +203,17 @@ __host__ __device__ inline uint32_t edge_hash(uint32_t key) {
 }
 // Bloom probe of a folded 4-gram w: p = w * mul (32x32 -> 64 bit).  Block = top BLOOM_LOG2 bits
 // of the low word (multiplicative hashing keeps the TOP bits); the bit positions come from the
-// high word, whose bits all depend on every input bit: BLOOM_PK packed shifts 1 << (hi >> 4q),
+// high word, whose bits all depend on every input bit: pk packed shifts 1 << (hi >> 4q),
 // each setting one bit in each 16-bit half (v_pk_lshlrev_b16: bits [0..3] and [16..19]).
 struct BloomProbe { uint32_t block, mask; };
 __host__ __device__ inline uint32_t pk_bits(uint32_t x) {
     return (1u << (x & 15)) | (1u << (16 + ((x >> 16) & 15)));
 }
-__host__ __device__ inline BloomProbe bloom_probe(uint32_t w, uint32_t mul) {
+__host__ __device__ inline BloomProbe bloom_probe(uint32_t w, uint32_t mul, uint32_t pk) {
     const uint64_t p = (uint64_t)w * mul;
     const uint32_t lo = (uint32_t)p, hi = (uint32_t)(p >> 32);
     uint32_t m = 0;
-    for (int q = 0; q < BLOOM_PK; q++) m |= pk_bits(hi >> (4 * q));
+    for (uint32_t q = 0; q < pk; q++) m |= pk_bits(hi >> (4 * q));
     return BloomProbe{lo >> (32 - BLOOM_LOG2), m};
 }
 __host__ __device__ inline uint32_t lit_bucket_hash(uint32_t w) { uint32_t h = w * 0xC2B2AE3Du; return h ^ (h >> 16); }
