@@ -166,11 +166,29 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
                      "algorithmic_bytes_per_launch": zone_bytes},
     }
+    result["roofline"].update(pmc_traffic())
     if not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(ss, gblob, preqs, parena, args.cpu_seconds)
     if dist:
         dist.destroy_process_group()
     print(json.dumps(result), flush=True)
+
+
+def pmc_traffic():
+    """HBM read bytes per k_waf_scan launch from the committed PMC pass of this workload
+    (scripts/pmc.sh: a separate `rocprofv3 --pmc FETCH_SIZE` run of this bench, FETCH_SIZE x 2 x
+    1024 per the gfx950 correction in MI355X_MICROARCH.md).  Counters cannot be read from inside
+    the timed run, so the value is the profiled one, named with its source file."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
+    if not files:
+        return {}
+    s = json.load(open(files[-1]))
+    b = s.get("k_waf_scan_hbm_read_bytes_per_launch")
+    if b is None:
+        return {}
+    return {"traffic": b, "traffic_unit": "bytes/launch",
+            "traffic_source": os.path.relpath(files[-1], ROOT) + " (rocprofv3 --pmc FETCH_SIZE)"}
 
 
 def cpu_baseline(ss, gblob, preqs, parena, seconds):

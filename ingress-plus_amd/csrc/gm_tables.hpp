@@ -134,7 +134,7 @@ struct DDfa {
 // 1024-thread workgroup per CU.  Every arena offset is probed: one ds_read_b32 and pk
 // packed 16-bit shifts (2 bits each) per byte position.
 constexpr int BLOOM_LOG2 = 15;
-constexpr int BLOOM_PK_DEFAULT = 3;  // K = 2 * pk bits per key (pk = 1..3, per generation)
+constexpr int BLOOM_PK_DEFAULT = 2;  // K = 2 * pk bits per key (pk = 1..3, per generation)
 constexpr uint32_t BLOOM_WORDS = 1u << BLOOM_LOG2;
 constexpr uint32_t SCAN_LDS_BYTES = 4u * BLOOM_WORDS;
 constexpr int CAND_SHARDS = 64;      // candidate-list shards (one atomic tail per shard)
