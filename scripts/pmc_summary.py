@@ -15,7 +15,7 @@ for p in ("fetch", "write", "sq"):
         continue
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0].split("<")[0]
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, d in acc.items():
         for c, v in d.items():
