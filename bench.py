@@ -129,7 +129,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     s = eng.stats()
-    log(f"[rank {rank}] {args.steps} steps in {elapsed:.3f}s; candidates {s['last_candidates']}, pairs "
+    dbg = eng.debug_status()
+    log(f"[rank {rank}] status words: records {dbg[5]}, anchored-DFA bytes {dbg[8]} (max/lane {dbg[9]}), "
+        f"full literal matches {dbg[10]}")
+    log(f"[rank {rank}] {args.steps} steps in {elapsed:.3f}s; candidates {s['last_candidates']}, ctx-pass {s['last_ctx_pass']}, jobs {s['last_jobs']}, pairs "
         f"{s['last_pairs']}, hits {s['last_hits']}; ms route {np.mean(route_ms):.3f} scan {np.mean(scan_ms):.3f} "
         f"verify {np.mean(verify_ms):.3f} tail {np.mean(tail_ms):.3f}")
 

@@ -136,6 +136,7 @@ enum { GM_WAF_OFF = 0, GM_WAF_MONITORING = 1, GM_WAF_SAFE_BLOCKING = 2, GM_WAF_B
 #define GM_ENTRY_MAIN     1u
 #define GM_ENTRY_CONFD    2u
 #define GM_ENTRY_SIGS     3u
+#define GM_ENTRY_SAMPLE   4u   /* optional: benign traffic sample bytes; tunes WAF key choice only */
 
 typedef struct gm_stats_t {
     uint32_t gen;
@@ -161,6 +162,11 @@ typedef struct gm_stats_t {
      * caller's stream: route kernel, WAF scan kernel, verify kernel, and everything after it
      * (regex confirm, sorts, hit emission, incl. the mid-batch host reads of counts). */
     float    last_ms_route, last_ms_scan, last_ms_verify, last_ms_tail;
+    /* WAF prefilter shape: key windows in the Bloom filter, probes per window (K = 2 * pk bits),
+     * and the modelled false-positive weight per probed window (ppm) the compiler chose on. */
+    uint32_t n_waf_keys, bloom_pk, bloom_fp_ppm;
+    /* last batch: candidate windows passing the stage-2 context filter; regex jobs queued */
+    uint32_t last_ctx_pass, last_jobs, reserved0;
 } gm_stats_t;
 
 typedef struct gm_ctx gm_ctx;

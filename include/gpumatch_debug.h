@@ -18,10 +18,21 @@ int gm_debug_regex_factors(const char *pat, int caseless, char *out, size_t cap)
 /* The distinct case-folded 4-byte key windows of the loaded generation's WAF prefilter (all
  * literals + regex triggers); returns their number (writes at most `cap`). */
 struct gm_ctx;
+/* The last batch's device status words (counts, profiling counters) as of the last gm_sync;
+ * returns the number copied. */
+int gm_debug_status(struct gm_ctx *ctx, uint32_t *out, size_t n);
 int gm_debug_waf_keys(struct gm_ctx *ctx, uint32_t *out, size_t cap);
+/* The prefilter's literal table: one row of 4 x uint32 per (key window, pattern) entry --
+ * {key, rule id or regex index, (uint16)key_off | len << 16, flags | zones << 8}; returns the
+ * number of entries (writes at most `cap` rows). */
+int gm_debug_waf_lits(struct gm_ctx *ctx, uint32_t *out, size_t cap);
+/* Pattern bytes (folded if nocase) of row `row` of gm_debug_waf_lits; returns the length. */
+int gm_debug_waf_lit_bytes(struct gm_ctx *ctx, uint32_t row, uint8_t *out, size_t cap);
 /* Host restatement of the WAF scan kernel's candidate rule over arena bytes A[0, len): writes
  * the candidate positions (at most `cap`) and returns their number. */
 int64_t gm_debug_waf_prefilter(struct gm_ctx *ctx, const uint8_t *A, size_t len, uint64_t *out, size_t cap);
+/* The same followed by k_waf_verify's stage-2 context filter: the windows that reach the exact check. */
+int64_t gm_debug_waf_prefilter2(struct gm_ctx *ctx, const uint8_t *A, size_t len, uint64_t *out, size_t cap);
 #ifdef __cplusplus
 }
 #endif

@@ -700,10 +700,11 @@ const std::set<uint32_t> &background_grams3() {
     return g;
 }
 
-double window_score(const std::string &p, size_t o) {
+// model score of a folded window: log2 of a relative frequency, +40 for background 4-grams,
+// +6 per background 3-gram (word-internal)
+double window_score_w(uint32_t w) {
     double s = 0;
-    for (int k = 0; k < 4; k++) s += byte_logfreq((uint8_t)p[o + k]);
-    const uint32_t w = fold4(load4(p, o));
+    for (int k = 0; k < 4; k++) s += byte_logfreq((uint8_t)(w >> (8 * k)));
     if (background_grams().count(w)) s += 40.0;
     for (int k = 0; k < 2; k++) {
         const uint32_t g3 = (w >> (8 * k)) & 0xFFFFFFu;
@@ -712,40 +713,115 @@ double window_score(const std::string &p, size_t o) {
     return s;
 }
 
-uint16_t rarest_window(const std::string &p) {
-    double best = 1e30; uint16_t bo = 0;
-    for (size_t o = 0; o + 4 <= p.size(); o++) {
-        const double s = window_score(p, o);
-        if (s < best - 1e-9) { best = s; bo = (uint16_t)o; }
+// Expected benign occurrences of a folded 4-gram key window.  With a traffic sample in the
+// generation blob (GM_ENTRY_SAMPLE: bytes of benign requests, as a deployment would sample its
+// own traffic) the count in the sample decides; the byte/background model above only ranks
+// windows the sample does not contain.  Without a sample the model alone decides.
+struct KeyModel {
+    std::unordered_map<uint32_t, uint32_t> cnt;
+    double n = 0;
+    void add_sample(const uint8_t *b, size_t len) {
+        for (size_t i = 0; i + 4 <= len; i++) {
+            uint32_t w;
+            memcpy(&w, b + i, 4);
+            cnt[fold4(w)]++;
+        }
+        n += len >= 4 ? (double)(len - 3) : 0.0;
     }
-    return bo;
+    double cost(uint32_t w) const {
+        const double prior = std::exp2(window_score_w(w));
+        if (n == 0) return prior;
+        auto it = cnt.find(w);
+        return (it == cnt.end() ? 0.0 : (double)it->second) + n * prior * std::exp2(-28.0);
+    }
+};
+
+// The scan probes only even arena offsets (k_waf_scan), so every pattern is keyed on a set of
+// windows that catches an occurrence at either parity:
+//   >= 5 bytes: two ADJACENT windows (o, o + 1), the pair of least summed cost;
+//   4 bytes:    the pattern itself plus, for odd occurrences, the window one byte to the left
+//               ("Zabc", key_off -1) or to the right ("bcdY", key_off +1) for each of the 128
+//               folded bytes Z / Y -- whichever family is cheaper.
+struct KeyChoice { std::vector<std::pair<uint32_t, int16_t>> keys; };
+// follow: the bytes that can come right after a 4-byte pattern (regex prefix / factor strings;
+// nullptr = any byte) -- the right-hand family then only needs those
+// use: how many patterns already key on a window.  A >= 5-byte pattern's pair cost is, per
+// window, (benign cost + a floor for attack traffic) x (1 + patterns sharing the key: each is one
+// more literal compare per hit in k_waf_exact) x 8 per missing byte of stage-2 context (the
+// k_waf_ctx filter checks up to two pattern bytes either side of the window).
+KeyChoice choose_keys(const std::string &pat, const KeyModel &M, std::unordered_map<uint32_t, uint32_t> &use,
+                      const std::bitset<256> *follow = nullptr) {
+    KeyChoice r;
+    if (pat.size() >= 5) {
+        const int L = (int)pat.size();
+        auto wcost = [&](int o) {
+            const uint32_t w = fold4(load4(pat, (size_t)o));
+            auto it = use.find(w);
+            const double share = 1.0 + (it == use.end() ? 0.0 : (double)it->second);
+            const int miss = (2 - std::min(2, o)) + (2 - std::max(0, std::min(2, L - o - 4)));
+            return (M.cost(w) + std::exp2(-30.0)) * share * std::exp2(3.0 * miss);
+        };
+        double best = 1e300; int bo = 0;
+        for (int o = 0; o + 5 <= L; o++) {
+            const double c = wcost(o) + wcost(o + 1);
+            if (c < best * (1 - 1e-12)) { best = c; bo = o; }
+        }
+        for (int o = bo; o <= bo + 1; o++) {
+            const uint32_t w = fold4(load4(pat, (size_t)o));
+            r.keys.push_back({w, (int16_t)o});
+            use[w]++;
+        }
+        return r;
+    }
+    const uint32_t w = fold4(load4(pat, 0));
+    std::bitset<256> ys;   // folded right-hand bytes
+    for (uint32_t z = 0; z < 256; z++) if (!follow || (*follow)[z]) ys[z | 0x20u] = true;
+    double cl = 0, cr = 0;
+    for (uint32_t z = 0; z < 256; z++) {
+        if ((z | 0x20u) != z) continue;
+        cl += M.cost(z | (w << 8));
+        if (ys[z]) cr += M.cost((w >> 8) | (z << 24));
+    }
+    r.keys.push_back({w, 0});
+    for (uint32_t z = 0; z < 256; z++) {
+        if ((z | 0x20u) != z) continue;
+        if (cl <= cr) r.keys.push_back({z | (w << 8), -1});
+        else if (ys[z]) r.keys.push_back({(w >> 8) | (z << 24), 1});
+    }
+    return r;
 }
 
-// Bloom multiplier per generation: a Bloom filter's false-positive rate is an average; on real
-// traffic what matters is whether a handful of very frequent benign 4-grams happen to collide.
-// Build the filter with each candidate multiplier and keep the one under which the fewest
-// background-corpus 4-grams (plus their one-byte neighbours in case) test positive.
+// Bloom multiplier and probe count per generation: a Bloom filter's false-positive rate is an
+// average; on real traffic what matters is whether the frequent benign 4-grams collide.  Each
+// candidate multiplier builds the filter and is scored by the benign non-key windows that test
+// positive (weighted by their sample counts; without a sample: the background corpus).
 const uint32_t kBloomMuls[] = {0x9E3779B1u, 0x85EBCA77u, 0xC2B2AE3Du, 0x27D4EB2Fu, 0x165667B1u, 0xD3A2646Cu | 1u,
                                0xFD7046C5u, 0xB55A4F09u, 0x7FEB352Du, 0x846CA68Bu, 0x2C1B3C6Du, 0x297A2D39u,
                                0xE6546B64u | 1u, 0x1B873593u, 0xCC9E2D51u, 0x5BD1E995u};
 
-uint32_t choose_bloom_mul(const std::vector<uint32_t> &keys, uint32_t pk, std::vector<uint32_t> &filter) {
-    const auto &bg = background_grams();
+struct BloomChoice { uint32_t mul = 0; double fp = 0; };   // fp: weighted false positives per window
+BloomChoice choose_bloom_mul(const std::vector<uint32_t> &keys, uint32_t pk, const KeyModel &M,
+                             std::vector<uint32_t> &filter) {
     std::set<uint32_t> kset(keys.begin(), keys.end());
-    size_t best_fp = SIZE_MAX; uint32_t best = kBloomMuls[0];
+    std::vector<std::pair<uint32_t, double>> test;   // benign non-key windows, weight
+    if (M.n > 0) {
+        for (auto &kv : M.cnt) if (!kset.count(kv.first)) test.push_back({kv.first, kv.second / M.n});
+    } else {
+        for (uint32_t g : background_grams()) if (!kset.count(g)) test.push_back({g, 1.0 / 65536});
+    }
+    BloomChoice best{kBloomMuls[0], 1e300};
     for (uint32_t mul : kBloomMuls) {
         std::fill(filter.begin(), filter.end(), 0u);
         for (uint32_t k : keys) { const BloomProbe b = bloom_probe(k, mul, pk); filter[b.block] |= b.mask; }
-        size_t fp = 0;
-        for (uint32_t g : bg) {
-            if (kset.count(g)) continue;
-            const BloomProbe b = bloom_probe(g, mul, pk);
-            fp += (filter[b.block] & b.mask) == b.mask;
+        double fp = 0;
+        for (auto &t : test) {
+            const BloomProbe b = bloom_probe(t.first, mul, pk);
+            if ((filter[b.block] & b.mask) == b.mask) fp += t.second;
         }
-        if (fp < best_fp) { best_fp = fp; best = mul; }
+        if (fp < best.fp) best = BloomChoice{mul, fp};
     }
     std::fill(filter.begin(), filter.end(), 0u);
-    for (uint32_t k : keys) { const BloomProbe b = bloom_probe(k, best, pk); filter[b.block] |= b.mask; }
+    for (uint32_t k : keys) { const BloomProbe b = bloom_probe(k, best.mul, pk); filter[b.block] |= b.mask; }
     return best;
 }
 
@@ -766,6 +842,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     bool have_main = false;
     std::vector<std::vector<Dir>> confd;
     const char *sig_text = nullptr; size_t sig_len = 0;
+    KeyModel KM;
     for (uint32_t e = 0; e < n; e++) {
         if (off + 12 > len) { R.code = GM_E_INVAL; R.err = "truncated blob"; return R; }
         uint32_t kind, nl, dl;
@@ -775,6 +852,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         const char *data = (const char *)blob + off + nl;
         off += nl + dl;
         if (kind == GM_ENTRY_SIGS) { sig_text = data; sig_len = dl; continue; }
+        if (kind == GM_ENTRY_SAMPLE) { KM.add_sample((const uint8_t *)data, dl); continue; }
         Tokenizer T(data, dl);
         std::vector<Dir> body;
         if (!parse_body(T, body, false)) {
@@ -1000,10 +1078,16 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     std::vector<LitE> lits;
     std::vector<DSigRegex> sregex;
     std::vector<uint32_t> always;
-    // one prefilter literal, keyed on its least probable 4-byte window
-    auto add_lit = [&](const std::string &pat, const std::string &bytes, uint32_t id, uint8_t flags, uint8_t zones) {
-        const uint16_t ko = rarest_window(pat);
-        lits.push_back(LitE{fold4(load4(pat, ko)), DLit{id, 0, (uint16_t)bytes.size(), flags, zones, ko, 0}, bytes});
+    // one prefilter pattern -> its key windows (stride-2 scan, see choose_keys)
+    std::unordered_map<uint32_t, uint32_t> key_use;
+    auto add_lit = [&](const std::string &pat, const std::string &bytes, uint32_t id, uint8_t flags, uint8_t zones,
+                       const std::bitset<256> *follow = nullptr) {
+        const DLit d{id, 0, (uint16_t)bytes.size(), flags, zones, 0, 0};
+        for (auto &k : choose_keys(pat, KM, key_use, follow).keys) {
+            LitE e{k.first, d, bytes};
+            e.lit.key_off = k.second;
+            lits.push_back(e);
+        }
     };
     for (size_t r = 0; r < sig.size(); r++) {
         const SigRule &g = sig[r];
@@ -1026,14 +1110,16 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 sr.mode = RXM_PREFIX;
                 sr.adfa = (uint32_t)C.add_dfa(ri.anchored);
                 for (auto &f : ri.prefix)
-                    add_lit(f, f, ridx, (uint8_t)(LIT_NOCASE | LIT_TRIGGER | LIT_PREFIX), (uint8_t)g.zones);
+                    add_lit(f, f, ridx, (uint8_t)(LIT_NOCASE | LIT_TRIGGER | LIT_PREFIX), (uint8_t)g.zones,
+                            ri.has_prefix_follow ? &ri.prefix_follow : nullptr);
             } else if (ri.min_factor < 4) {
                 sr.mode = RXM_ALWAYS;
                 always.push_back(ridx);
                 st.n_sig_regex_always++;
             } else {
                 for (auto &f : ri.factors)
-                    add_lit(f, f, ridx, (uint8_t)(LIT_NOCASE | LIT_TRIGGER), (uint8_t)g.zones);
+                    add_lit(f, f, ridx, (uint8_t)(LIT_NOCASE | LIT_TRIGGER), (uint8_t)g.zones,
+                            ri.has_factor_follow ? &ri.factor_follow : nullptr);
             }
             sregex.push_back(sr);
         }
@@ -1044,7 +1130,18 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     });
     std::vector<DLit> dlits;
     std::vector<uint32_t> waf_a(BLOOM_WORDS, 0);   // LDS Bloom image
-    std::vector<uint32_t> waf_b(4, 0);   // unused (kept for layout stability)
+    // stage-2 context filter: each entry's key window plus the pattern bytes around it
+    std::vector<uint32_t> waf_b(BLOOM_WORDS, 0);
+    for (const LitE &e : lits) {
+        const int k = e.lit.key_off, L = (int)e.bytes.size();
+        auto cb = [&](int i) { return (uint32_t)(uint8_t)e.bytes[i] | 0x20u; };
+        const uint32_t nl = k <= 0 ? 0u : (uint32_t)std::min(2, k);
+        const uint32_t nr = (uint32_t)std::max(0, std::min(2, L - (k + 4)));
+        const uint32_t l2 = (nl >= 2 ? cb(k - 2) : 0u) | (nl >= 1 ? cb(k - 1) << 8 : 0u);
+        const uint32_t r2 = (nr >= 1 ? cb(k + 4) : 0u) | (nr >= 2 ? cb(k + 5) << 8 : 0u);
+        const BloomProbe b = bloom_probe(ctx_key(e.key, l2, r2, nl * 3 + nr), CTX_MUL_DEFAULT, CTX_PK);
+        waf_b[b.block] |= b.mask;
+    }
     std::vector<std::pair<uint32_t, std::pair<uint32_t, uint32_t>>> buckets;
     std::vector<uint32_t> keys;
     for (size_t i = 0; i < lits.size(); i++) {
@@ -1057,9 +1154,24 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         }
         buckets.back().second.second++;
     }
-    uint32_t bloom_pk = BLOOM_PK_DEFAULT;
-    if (const char *ev = getenv("GM_BLOOM_PK")) bloom_pk = std::min(3, std::max(1, atoi(ev)));   // tuning knob
-    const uint32_t bloom_mul = keys.empty() ? kBloomMuls[0] : choose_bloom_mul(keys, bloom_pk, waf_a);
+    // probes per window: pk = 2 or 3 (K = 4 or 6 bits), whichever minimises scan + verify cost:
+    // pk = 3 costs ~17 % more scan VALU per probe; a false positive costs ~700 probes of verify
+    uint32_t bloom_pk = BLOOM_PK_DEFAULT, bloom_mul = kBloomMuls[0];
+    if (!keys.empty()) {
+        int forced = 0;
+        if (const char *ev = getenv("GM_BLOOM_PK")) forced = std::min(3, std::max(1, atoi(ev)));   // tuning knob
+        if (forced) bloom_pk = forced;
+        BloomChoice b = choose_bloom_mul(keys, bloom_pk, KM, waf_a);
+        if (!forced) {
+            std::vector<uint32_t> f3(BLOOM_WORDS, 0);
+            BloomChoice b3 = choose_bloom_mul(keys, 3, KM, f3);
+            if (0.17 + 700.0 * b3.fp < 700.0 * b.fp) { b = b3; bloom_pk = 3; waf_a.swap(f3); }
+        }
+        bloom_mul = b.mul;
+        st.bloom_fp_ppm = (uint32_t)std::min(1e9, b.fp * 1e6);
+    }
+    st.n_waf_keys = (uint32_t)keys.size();
+    st.bloom_pk = bloom_pk;
     uint32_t lcap = pow2_at_least(buckets.size() * 2 + 1);
     std::vector<DLitBucket> ltab(lcap, DLitBucket{0, 0, 0, 0});
     for (auto &b : buckets) {
@@ -1105,7 +1217,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_bytes = I.put(C.bytes);
     I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
     h.total = I.buf.size();
-    h.bloom_log2 = BLOOM_LOG2; h.bloom_mul = bloom_mul; h.bloom_pk = bloom_pk;
+    h.bloom_log2 = BLOOM_LOG2; h.bloom_mul = bloom_mul; h.bloom_pk = bloom_pk; h.ctx_mul = CTX_MUL_DEFAULT;
     memcpy(I.buf.data(), &h, sizeof h);
     st.table_bytes = h.total;
     R.image = std::move(I.buf);
@@ -1149,7 +1261,7 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;
     t.n_locs = h.n_locs; t.n_sigs = h.n_sigs; t.n_sig_regex = h.n_sig_regex; t.n_always = h.n_always;
     t.n_lits = h.n_lits;
-    t.bloom_log2 = h.bloom_log2; t.bloom_mul = h.bloom_mul; t.bloom_pk = h.bloom_pk;
+    t.bloom_log2 = h.bloom_log2; t.bloom_mul = h.bloom_mul; t.bloom_pk = h.bloom_pk; t.ctx_mul = h.ctx_mul;
     t.gen = gen;
     return t;
 }

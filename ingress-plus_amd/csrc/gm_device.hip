@@ -267,20 +267,25 @@ __device__ bool dfa_run_val(const GTab &t, uint32_t dfa_id, const Val &v) {
     return (acc[st] & 2) != 0;
 }
 
-__device__ bool dfa_run_bytes(const GTab &t, uint32_t dfa_id, const uint8_t *p, uint32_t n) {
+// `steps` (optional) accumulates the bytes consumed -- profiling counters of the WAF verify
+__device__ bool dfa_run_bytes(const GTab &t, uint32_t dfa_id, const uint8_t *p, uint32_t n, uint32_t *steps = nullptr) {
     const DDfa d = t.dfas[dfa_id];
     const uint16_t *tr = t.dfa_trans + d.trans_off;
     const uint8_t *acc = t.dfa_acc + d.acc_off, *cls = t.dfa_cls + d.cls_off;
     uint32_t st = 1;
     if (acc[st] & 1) return true;
-    for (uint32_t i = 0; i < n; i++) {
+    uint32_t i = 0;
+    bool r = false;
+    for (; i < n; i++) {
         uint8_t b = p[i];
-        if ((acc[st] & 2) && i + 1 == n && b == '\n') return true;
+        if ((acc[st] & 2) && i + 1 == n && b == '\n') { r = true; break; }
         st = tr[st * d.n_classes + cls[b]];
-        if (st == 0) return false;
-        if (acc[st] & 1) return true;
+        if (st == 0) break;
+        if (acc[st] & 1) { r = true; break; }
     }
-    return (acc[st] & 2) != 0;
+    if (i == n) r = (acc[st] & 2) != 0;
+    if (steps) *steps += i;
+    return r;
 }
 
 __device__ uint32_t murmur2_val(const Val &v, uint8_t *buf, bool &ok) {
@@ -689,6 +694,7 @@ struct gm_ctx {
     uint32_t *d_status = nullptr, *h_status = nullptr;
     uint32_t *d_blk2rec = nullptr; size_t cap_blk = 0;
     unsigned long long *d_cand = nullptr; size_t cap_cand = 0;
+    unsigned long long *d_surv = nullptr; size_t cap_surv = 0;   // stage-2 survivors (arena offsets)
     unsigned long long *d_pairs = nullptr, *d_pairs2 = nullptr; size_t cap_pairs = 0;
     unsigned long long *d_jobs = nullptr, *d_jobs2 = nullptr; size_t cap_jobs = 0;
     uint32_t *d_keep = nullptr, *d_idx = nullptr; size_t cap_keep = 0, cap_idx = 0;
@@ -697,12 +703,13 @@ struct gm_ctx {
     // host-staging (GM_BATCH_HOST)
     uint8_t *d_stage = nullptr; size_t cap_stage = 0;
     ncclComm_t comm = nullptr;
-    uint64_t last_candidates = 0, last_pairs = 0, last_hits = 0;
+    uint64_t last_candidates = 0, last_pairs = 0, last_hits = 0, last_ctx_pass = 0, last_jobs = 0;
     hipEvent_t ev[5] = {};
     bool ev_pending = false;
     int ev_used = 0;
     float last_ms[4] = {0, 0, 0, 0};
     int cu_count = 256;
+    int scan_depth = SCAN_DEPTH;   // chunks in flight per scan wave (GM_SCAN_DEPTH tuning knob)
     std::mutex mu;
 };
 
@@ -743,6 +750,7 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
             c->cu_count = cus;
+        if (const char *ev = getenv("GM_SCAN_DEPTH")) c->scan_depth = atoi(ev);
         if (hipMalloc((void **)&c->d_status, STATUS_WORDS * 4) != hipSuccess ||
             hipHostMalloc((void **)&c->h_status, STATUS_WORDS * 4, hipHostMallocDefault) != hipSuccess) {
             t_err = "status alloc failed"; delete c; return nullptr;
@@ -759,7 +767,7 @@ void gm_destroy(gm_ctx *c) {
         (void)hipSetDevice(c->dev);
         (void)hipDeviceSynchronize();
         if (c->gen) (void)hipFree(c->gen->d_image);
-        for (void *p : {(void *)c->d_counters, (void *)c->d_status, (void *)c->d_blk2rec, (void *)c->d_cand,
+        for (void *p : {(void *)c->d_counters, (void *)c->d_status, (void *)c->d_blk2rec, (void *)c->d_cand, (void *)c->d_surv,
                         (void *)c->d_pairs, (void *)c->d_pairs2, (void *)c->d_jobs, (void *)c->d_jobs2,
                         (void *)c->d_keep, (void *)c->d_idx, (void *)c->d_temp, (void *)c->d_stage,
                         (void *)c->d_ccnt})
@@ -811,6 +819,8 @@ int gm_stats(gm_ctx *c, gm_stats_t *out) {
     out->last_candidates = c->last_candidates;
     out->last_pairs = c->last_pairs;
     out->last_hits = c->last_hits;
+    out->last_ctx_pass = (uint32_t)c->last_ctx_pass;
+    out->last_jobs = (uint32_t)c->last_jobs;
     out->last_ms_route = c->last_ms[0]; out->last_ms_scan = c->last_ms[1];
     out->last_ms_verify = c->last_ms[2]; out->last_ms_tail = c->last_ms[3];
     return GM_OK;
@@ -839,35 +849,51 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
         HIPCHK(c, hipGetLastError());
     }
     if (mark(1)) return GM_E_HIP;
-    c->last_candidates = c->last_pairs = c->last_hits = 0;
+    c->last_candidates = c->last_pairs = c->last_hits = c->last_ctx_pass = c->last_jobs = 0;
     if (!waf || n == 0) return GM_OK;
 
-    const size_t ccap = alen / 64 + 65536, pcap = (size_t)n * 2 + 65536, jcap = (size_t)n + 65536;
+    // candidate records: 32 B (4 x u64) each, room for one per 64 arena bytes (a lane with a
+    // candidate window in every 4th 16-byte slice) -- overflow is reported, never truncated
+    const size_t ccap = 4 * (alen / 64 + 16384), pcap = (size_t)n * 2 + 65536, jcap = (size_t)n + 65536;
     int e;
     // persistent scan grid: one 1024-thread workgroup per CU (144 KiB LDS prefilter);
     // every wave owns a contiguous arena range and a private candidate region of wcap entries
     const uint32_t scan_blocks = (uint32_t)c->cu_count;
     const uint32_t W = scan_blocks * SCAN_WAVES;
-    if ((e = grow(c, c->d_cand, c->cap_cand, std::max<size_t>(ccap, (size_t)W * 1024)))) return e;
-    if ((e = grow(c, c->d_ccnt, c->cap_ccnt, W))) return e;
-    const uint32_t wcap = (uint32_t)std::min<size_t>(c->cap_cand / W, 0xFFFFFFFFu);
+    if ((e = grow(c, c->d_cand, c->cap_cand, std::max<size_t>(ccap, (size_t)W * 4096)))) return e;
+    if ((e = grow(c, c->d_ccnt, c->cap_ccnt, W + scan_blocks))) return e;   // scan-wave + ctx-block counts
+    if ((e = grow(c, c->d_surv, c->cap_surv, std::min<size_t>(alen / 256 + 65536, 0xFFFFFFFFu)))) return e;
+    const uint32_t wcap = (uint32_t)std::min<size_t>(c->cap_cand / 4 / W, 0xFFFFFFFFu);   // records per wave
+    u32x4 *cand = reinterpret_cast<u32x4 *>(c->d_cand);
     { size_t cp = c->cap_pairs; if ((e = grow(c, c->d_pairs, cp, pcap))) return e;
       size_t cp2 = c->cap_pairs; if ((e = grow(c, c->d_pairs2, cp2, pcap))) return e; c->cap_pairs = std::max(cp, cp2); }
     { size_t cj = c->cap_jobs; if ((e = grow(c, c->d_jobs, cj, jcap))) return e;
       size_t cj2 = c->cap_jobs; if ((e = grow(c, c->d_jobs2, cj2, jcap))) return e; c->cap_jobs = std::max(cj, cj2); }
 
-    if (t.bloom_pk == 1) k_waf_scan<1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
-    else if (t.bloom_pk == 2) k_waf_scan<2><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
-    else k_waf_scan<3><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, c->d_cand, wcap, c->d_ccnt);
+    if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+    else if (t.bloom_pk == 2) {
+        if (c->scan_depth == 1) k_waf_scan<2, 1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else if (c->scan_depth == 2) k_waf_scan<2, 2><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else if (c->scan_depth == 6) k_waf_scan<2, 6><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+    } else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
     HIPCHK(c, hipGetLastError());
     if (mark(2)) return GM_E_HIP;
-    k_waf_verify<<<W, 256, 0, s>>>(A, alen, reqs, n, c->d_blk2rec, t, c->d_cand, wcap, c->d_ccnt, W, c->d_pairs,
-                                   (uint32_t)c->cap_pairs, c->d_jobs, (uint32_t)c->cap_jobs, c->d_status);
+    const uint32_t bcap = (uint32_t)std::min<size_t>(c->cap_surv / scan_blocks, 0xFFFFFFFFu);
+    k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, c->d_ccnt, W, t, c->d_surv, bcap, c->d_ccnt + W,
+                                                c->d_status);
+    HIPCHK(c, hipGetLastError());
+    constexpr uint32_t EXACT_SUB = 8;
+    k_waf_exact<<<scan_blocks * EXACT_SUB, 256, 0, s>>>(A, alen, reqs, n, c->d_blk2rec, t, c->d_surv, bcap,
+                                                         c->d_ccnt + W, EXACT_SUB, c->d_pairs, (uint32_t)c->cap_pairs,
+                                                         c->d_jobs, (uint32_t)c->cap_jobs, c->d_status);
     HIPCHK(c, hipGetLastError());
     if (mark(3)) return GM_E_HIP;
     HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, STATUS_WORDS * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    c->last_candidates = c->h_status[5];
+    c->last_candidates = c->h_status[6];
+    c->last_ctx_pass = c->h_status[7];
+    c->last_jobs = c->h_status[2];
     if (c->h_status[3]) return fail(c, GM_E_OVERFLOW, "WAF candidate/pair/job capacity exceeded");
     uint32_t nj = std::min<uint32_t>(c->h_status[2], (uint32_t)c->cap_jobs);
     int rec_bits = 1;
@@ -1018,6 +1044,48 @@ extern "C" int gm_debug_waf_keys(gm_ctx *c, uint32_t *out, size_t cap) {
     return (int)k;
 }
 
+// The last batch's device status words (gm_waf.inc STATUS_WORDS: counts and profiling counters),
+// as of the last gm_sync.
+extern "C" int gm_debug_status(gm_ctx *c, uint32_t *out, size_t n) {
+    if (!c || !out) return fail(c, GM_E_INVAL, "null argument");
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
+    memcpy(out, c->h_status, std::min<size_t>(n, STATUS_WORDS) * 4);
+    return (int)std::min<size_t>(n, STATUS_WORDS);
+}
+
+extern "C" int gm_debug_waf_lits(gm_ctx *c, uint32_t *out, size_t cap) {
+    if (!c || !c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
+    const TabHeader &h = c->gen->hdr;
+    const DLitBucket *b = (const DLitBucket *)(c->gen->host_image.data() + h.off_lit_buckets);
+    const DLit *l = (const DLit *)(c->gen->host_image.data() + h.off_lits);
+    size_t k = 0;
+    for (uint32_t i = 0; i < h.n_lit_buckets_cap; i++)
+        for (uint32_t j = 0; j < b[i].count; j++, k++) {
+            if (k >= cap) continue;
+            const DLit &d = l[b[i].first + j];
+            out[4 * k] = b[i].key; out[4 * k + 1] = d.id;
+            out[4 * k + 2] = (uint32_t)(uint16_t)d.key_off | (uint32_t)d.len << 16;
+            out[4 * k + 3] = (uint32_t)d.flags | (uint32_t)d.zones << 8;
+        }
+    return (int)k;
+}
+
+extern "C" int gm_debug_waf_lit_bytes(gm_ctx *c, uint32_t row, uint8_t *out, size_t cap) {
+    if (!c || !c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
+    const TabHeader &h = c->gen->hdr;
+    const uint8_t *img = c->gen->host_image.data();
+    const DLitBucket *b = (const DLitBucket *)(img + h.off_lit_buckets);
+    const DLit *l = (const DLit *)(img + h.off_lits);
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < h.n_lit_buckets_cap; i++) {
+        if (row >= k + b[i].count) { k += b[i].count; continue; }
+        const DLit &d = l[b[i].first + (row - k)];
+        memcpy(out, img + h.off_bytes + d.bytes_off, std::min<size_t>(cap, d.len));
+        return d.len;
+    }
+    return fail(c, GM_E_INVAL, "row out of range");
+}
+
 // Host restatement of k_waf_scan's candidate rule over `len` arena bytes (same tables, same
 // hashes): the CPU tests use it to check that every literal occurrence is a candidate and to
 // measure the prefilter's false-positive rate without a GPU.
@@ -1026,11 +1094,40 @@ extern "C" int64_t gm_debug_waf_prefilter(gm_ctx *c, const uint8_t *A, size_t le
     const TabHeader &h = c->gen->hdr;
     const uint32_t *bloom = (const uint32_t *)(c->gen->host_image.data() + h.off_waf_a);
     int64_t k = 0;
-    for (size_t p = 0; p + 4 <= len; p++) {
+    for (size_t p = 0; p + 4 <= len; p += 2) {   // even offsets only (stride-2 scan)
         uint32_t w;
         memcpy(&w, A + p, 4);
         const BloomProbe b = bloom_probe(fold4(w), h.bloom_mul, h.bloom_pk);
         if ((bloom[b.block] & b.mask) == b.mask) { if ((size_t)k < cap && out) out[k] = p; k++; }
+    }
+    return k;
+}
+
+// Host restatement of both filter stages: k_waf_scan's candidate rule, then k_waf_verify's
+// stage-2 context filter (bytes outside the arena read as the fold of 0, like the kernels).
+extern "C" int64_t gm_debug_waf_prefilter2(gm_ctx *c, const uint8_t *A, size_t len, uint64_t *out, size_t cap) {
+    if (!c || !c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
+    const TabHeader &h = c->gen->hdr;
+    const uint32_t *bloom = (const uint32_t *)(c->gen->host_image.data() + h.off_waf_a);
+    const uint32_t *ctxb = (const uint32_t *)(c->gen->host_image.data() + h.off_waf_b);
+    auto fb = [&](int64_t i) -> uint32_t { return (i >= 0 && (size_t)i < len ? A[i] : 0u) | 0x20u; };
+    int64_t k = 0;
+    for (size_t p = 0; p + 4 <= len; p += 2) {
+        uint32_t w;
+        memcpy(&w, A + p, 4);
+        w = fold4(w);
+        const BloomProbe b = bloom_probe(w, h.bloom_mul, h.bloom_pk);
+        if ((bloom[b.block] & b.mask) != b.mask) continue;
+        const int64_t q = (int64_t)p;
+        const uint32_t l2 = fb(q - 2) | fb(q - 1) << 8, r2 = fb(q + 4) | fb(q + 5) << 8;
+        bool hit = false;
+        for (uint32_t nl = 0; nl < 3 && !hit; nl++)
+            for (uint32_t nr = 0; nr < 3 && !hit; nr++) {
+                const BloomProbe b2 = bloom_probe(ctx_key(w, l2 & ctx_lmask(nl), r2 & ctx_rmask(nr), nl * 3 + nr),
+                                                  h.ctx_mul, CTX_PK);
+                hit = (ctxb[b2.block] & b2.mask) == b2.mask;
+            }
+        if (hit) { if ((size_t)k < cap && out) out[k] = p; k++; }
     }
     return k;
 }

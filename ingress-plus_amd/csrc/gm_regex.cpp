@@ -371,11 +371,18 @@ struct NfaBuilder {
 };
 
 // ---------------------------------------------------------------- factors
+// Follow set of a string set: the folded bytes that can come right after any of its strings
+// (none = unknown).  The WAF scan probes only even offsets, and keys a 4-byte string at odd
+// offsets through the windows one byte left or right of it (gm_compile.cpp choose_keys): with a
+// known follow set the right-hand family has |follow| members instead of 128.
+struct Follow { CSet set; bool ok = false; };
 struct FI {
     bool exact_ok = false;
     std::vector<std::string> exact;
     std::vector<std::string> best;     // best OR-set found anywhere inside (empty = none)
+    Follow best_follow;
     std::vector<std::string> prefix = {""};   // every match starts with one of these (folded)
+    Follow prefix_follow;
 };
 
 bool small_set(const std::vector<std::string> &v) {
@@ -405,6 +412,59 @@ void uniq(std::vector<std::string> &v) { std::sort(v.begin(), v.end()); v.erase(
 void take_best(std::vector<std::string> &best, const std::vector<std::string> &cand) {
     if (score_len(cand) > 0 && better(cand, best)) best = cand;
 }
+void take_best(std::vector<std::string> &best, Follow &bf, const std::vector<std::string> &cand, const Follow &cf) {
+    if (score_len(cand) > 0 && better(cand, best)) { best = cand; bf = cf; }
+}
+
+// FIRST set of a node (ASCII-folded: the factors are matched caseless) and whether it can match
+// the empty string.  Used to extend 4-byte factors by the byte that must follow them: the WAF
+// scan probes only even offsets, which a >= 5-byte key covers with two windows
+// (gm_compile.cpp add_lit), while a 4-byte key needs 128 one-byte variants.
+struct First { CSet set; bool nullable = true; };
+First first_of(const std::vector<Node> &N, int n) {
+    const Node &x = N[n];
+    First r;
+    switch (x.k) {
+    case Node::EMPTY: case Node::BOL: case Node::EOL: return r;
+    case Node::SET:
+        for (int c = 0; c < 256; c++) if (x.set[c]) r.set[(c >= 'A' && c <= 'Z') ? c | 0x20 : c] = true;
+        r.nullable = false;
+        return r;
+    case Node::CAT:
+        for (int k : x.kids) {
+            First g = first_of(N, k);
+            r.set |= g.set;
+            if (!g.nullable) { r.nullable = false; break; }
+        }
+        return r;
+    case Node::ALT:
+        r.nullable = false;
+        for (int k : x.kids) { First g = first_of(N, k); r.set |= g.set; if (g.nullable) r.nullable = true; }
+        return r;
+    case Node::REP: {
+        First g = first_of(N, x.kids[0]);
+        r.set = g.set;
+        r.nullable = x.mn == 0 || g.nullable;
+        return r;
+    }
+    }
+    return r;
+}
+// FIRST of the sequence kids[i..] of a CAT; nullable = the whole rest can be empty
+First first_seq(const std::vector<Node> &N, const std::vector<int> &kids, size_t i) {
+    First r;
+    for (; i < kids.size(); i++) {
+        First g = first_of(N, kids[i]);
+        r.set |= g.set;
+        if (!g.nullable) { r.nullable = false; return r; }
+    }
+    return r;
+}
+Follow follow_of(const First &f) {
+    Follow r;
+    if (!f.nullable && f.set.any()) { r.set = f.set; r.ok = true; }
+    return r;
+}
 
 FI factors(const std::vector<Node> &N, int n) {
     const Node &x = N[n];
@@ -428,8 +488,9 @@ FI factors(const std::vector<Node> &N, int n) {
         bool cur_ok = true, all_exact = true;
         std::vector<FI> gs;
         for (int k : x.kids) gs.push_back(factors(N, k));
-        for (const FI &g : gs) {
-            take_best(r.best, g.best);
+        for (size_t gi = 0; gi < gs.size(); gi++) {
+            const FI &g = gs[gi];
+            take_best(r.best, r.best_follow, g.best, g.best_follow);
             if (g.exact_ok && cur_ok && cur.size() * g.exact.size() <= 16) {
                 std::vector<std::string> nx;
                 for (auto &a : cur) for (auto &b : g.exact) nx.push_back(a + b);
@@ -437,52 +498,65 @@ FI factors(const std::vector<Node> &N, int n) {
                 bool too_long = false; for (auto &s : nx) if (s.size() > 32) too_long = true;
                 if (!too_long) { cur = nx; continue; }
             }
-            // chain breaks here
+            // chain breaks here: cur is followed by FIRST(kids[gi..])
             all_exact = false;
-            take_best(r.best, cur);
+            take_best(r.best, r.best_follow, cur, follow_of(first_seq(N, x.kids, gi)));
             if (g.exact_ok) { cur = g.exact; cur_ok = true; }
             else { cur = {""}; cur_ok = true; }
         }
-        take_best(r.best, cur);
+        take_best(r.best, r.best_follow, cur, Follow{});
         if (all_exact) { r.exact_ok = true; r.exact = cur; }
         std::vector<std::string> pre = {""};
-        for (const FI &g : gs) {
+        Follow pf;   // follow set of pre
+        for (size_t gi = 0; gi < gs.size(); gi++) {
+            const FI &g = gs[gi];
             if (g.exact_ok) {
                 auto nx = cross(pre, g.exact);
                 if (small_set(nx)) { pre = nx; continue; }
+                pf = follow_of(first_seq(N, x.kids, gi));
                 break;
             }
             auto nx = cross(pre, g.prefix);
-            if (small_set(nx)) pre = nx;
+            if (small_set(nx) && g.prefix != std::vector<std::string>{""}) { pre = nx; pf = g.prefix_follow; }
+            else pf = follow_of(first_seq(N, x.kids, gi));
             break;
         }
+        r.prefix_follow = pf;
         r.prefix = pre;
         return r;
     }
     case Node::ALT: {
         bool all_exact = true, all_req = true;
         std::vector<std::string> ex, un, pu;
+        Follow uf, pf;   // unions of the kids' follow sets (unknown if any kid's is)
+        uf.ok = pf.ok = true;
         for (int k : x.kids) {
             FI g = factors(N, k);
             pu.insert(pu.end(), g.prefix.begin(), g.prefix.end());
+            pf.ok = pf.ok && g.prefix_follow.ok; pf.set |= g.prefix_follow.set;
             if (g.exact_ok) ex.insert(ex.end(), g.exact.begin(), g.exact.end()); else all_exact = false;
             std::vector<std::string> b = g.best;
-            if (g.exact_ok) take_best(b, g.exact);
+            Follow bf = g.best_follow;
+            if (g.exact_ok) take_best(b, bf, g.exact, Follow{});
+            uf.ok = uf.ok && bf.ok; uf.set |= bf.set;
             if (score_len(b) <= 0) all_req = false; else un.insert(un.end(), b.begin(), b.end());
         }
         uniq(ex); uniq(un);
         if (all_exact && ex.size() <= 16) { r.exact_ok = true; r.exact = ex; }
-        if (all_req) r.best = un;
+        if (all_req) { r.best = un; if (uf.ok) r.best_follow = uf; }
         uniq(pu);
         r.prefix = small_set(pu) ? pu : std::vector<std::string>{""};
+        if (small_set(pu) && pf.ok) r.prefix_follow = pf;
         return r;
     }
     case Node::REP: {
         FI g = factors(N, x.kids[0]);
         if (x.mn >= 1) {
             r.prefix = g.prefix;
+            r.prefix_follow = g.exact_ok ? Follow{} : g.prefix_follow;
             r.best = g.best;
-            if (g.exact_ok) take_best(r.best, g.exact);
+            r.best_follow = g.best_follow;
+            if (g.exact_ok) take_best(r.best, r.best_follow, g.exact, Follow{});
             if (x.mn == x.mx && g.exact_ok) {
                 std::vector<std::string> cur = {""};
                 bool ok = true;
@@ -639,12 +713,19 @@ RegexInfo compile_regex(const std::string &pattern, bool caseless, int max_state
 
     FI fi = factors(P.nodes, root);
     std::vector<std::string> best = fi.best;
-    if (fi.exact_ok) take_best(best, fi.exact);
-    if (score_len(best) > 0) { out.factors = best; out.min_factor = score_len(best); }
+    Follow bf = fi.best_follow;
+    if (fi.exact_ok) take_best(best, bf, fi.exact, Follow{});
+    if (score_len(best) > 0) {
+        out.factors = best; out.min_factor = score_len(best);
+        out.factor_follow = bf.set; out.has_factor_follow = bf.ok;
+    }
     bool has_bol = false;
     for (auto &nd : P.nodes) if (nd.k == Node::BOL) has_bol = true;
+    // prefix mode needs >= 4-byte prefixes (verified by an anchored DFA that dies within a few
+    // bytes -- far cheaper than a factor job's search over the whole zone, so it always wins)
     if (!has_bol && score_len(fi.prefix) >= 4 && build(false, out.anchored)) {
         out.prefix = fi.prefix;
+        out.prefix_follow = fi.prefix_follow.set; out.has_prefix_follow = fi.prefix_follow.ok;
         out.prefix_mode = true;
     }
     out.status = RX_OK;

@@ -8,6 +8,7 @@
 // (SURVEY.md §8 A8).
 #pragma once
 #include <stdint.h>
+#include <bitset>
 #include <string>
 #include <vector>
 
@@ -36,6 +37,10 @@ struct RegexInfo {
     bool prefix_mode = false;
     std::vector<std::string> prefix;
     Dfa anchored;
+    // folded bytes that can follow a factor / prefix string (has_* false = unknown): the WAF key
+    // chooser keys a 4-byte string at odd offsets on "its last three bytes + a follow byte"
+    std::bitset<256> factor_follow, prefix_follow;
+    bool has_factor_follow = false, has_prefix_follow = false;
 };
 
 RegexInfo compile_regex(const std::string &pattern, bool caseless, int max_states = 8192);

@@ -148,7 +148,8 @@ struct DLit {
     uint16_t len;
     uint8_t  flags;          // LIT_*
     uint8_t  zones;          // bit0 uri, bit1 args, bit2 hdrs, bit3 body
-    uint16_t key_off;        // offset of the 4-byte key window inside the pattern (rarest window)
+    int16_t  key_off;        // offset of the 4-byte key window inside the pattern; -1 = the window
+                             // starts one byte before the pattern (4-byte patterns, gm_compile.cpp)
     uint16_t pad;
 };
 enum : uint32_t { RXM_TRIGGER = 0, RXM_ALWAYS = 1, RXM_PREFIX = 2 };
@@ -175,7 +176,7 @@ struct TabHeader {
     uint32_t bloom_log2;     // BLOOM_LOG2 the image was built for
     uint32_t bloom_mul;      // Bloom hash multiplier (chosen per generation, see gm_compile.cpp)
     uint32_t bloom_pk;       // packed shifts per probe (K = 2 * bloom_pk)
-    uint32_t pad_end;
+    uint32_t ctx_mul;        // stage-2 context filter multiplier (waf_b, see ctx_key)
 };
 
 struct GTab {                // device pointers, built on host from the image base
@@ -188,7 +189,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const uint8_t *bytes; const uint32_t *waf_a; const uint32_t *waf_b;
     const DLitBucket *lit_buckets; const DLit *lits; const DSigRegex *sig_regex; const uint32_t *always;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
-    uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk;
+    uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
     uint32_t gen;
 };
 
@@ -215,6 +216,21 @@ __host__ __device__ inline BloomProbe bloom_probe(uint32_t w, uint32_t mul, uint
     uint32_t m = 0;
     for (uint32_t q = 0; q < pk; q++) m |= pk_bits(hi >> (4 * q));
     return BloomProbe{lo >> (32 - BLOOM_LOG2), m};
+}
+// Stage-2 context filter (waf_b, same size as the scan Bloom filter; staged into LDS by
+// k_waf_verify).  A scan candidate window w at arena offset p survives only if waf_b holds w
+// together with the folded bytes around it that its pattern fixes: up to two on the left
+// (l2 = A[p-2] | A[p-1] << 8) and two on the right (r2 = A[p+4] | A[p+5] << 8).  Each key entry
+// inserts one shape (nl, nr = bytes its pattern has on each side, 0..2); a window is probed with
+// all nine shapes.  Bytes outside the arena read as the fold of 0 (0x20).
+constexpr uint32_t CTX_PK = 3;
+constexpr uint32_t CTX_MUL_DEFAULT = 0x7FEB352Du;
+__host__ __device__ inline uint32_t ctx_lmask(uint32_t nl) { return nl == 0 ? 0u : nl == 1 ? 0xFF00u : 0xFFFFu; }
+__host__ __device__ inline uint32_t ctx_rmask(uint32_t nr) { return nr == 0 ? 0u : nr == 1 ? 0x00FFu : 0xFFFFu; }
+__host__ __device__ inline uint32_t ctx_key(uint32_t w, uint32_t l2, uint32_t r2, uint32_t shape) {
+    uint32_t c = (l2 * 0x9E3779B1u) ^ (r2 * 0x85EBCA77u) ^ ((shape + 1u) * 0xC2B2AE3Du);
+    c ^= c >> 15;
+    return w ^ c;
 }
 __host__ __device__ inline uint32_t lit_bucket_hash(uint32_t w) { uint32_t h = w * 0xC2B2AE3Du; return h ^ (h >> 16); }
 // Prefilter fold: OR 0x20 into every byte.  Maps A-Z onto a-z (so case-insensitive keys match)

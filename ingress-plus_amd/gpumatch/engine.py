@@ -32,12 +32,14 @@ STATS_FIELDS64 = ["table_bytes", "lds_bytes_scan", "last_candidates", "last_pair
 
 
 STATS_FIELDS_MS = ["last_ms_route", "last_ms_scan", "last_ms_verify", "last_ms_tail"]
+STATS_FIELDS_WAF = ["n_waf_keys", "bloom_pk", "bloom_fp_ppm", "last_ctx_pass", "last_jobs", "reserved0"]
 GM_CREATE_PROFILE = 0x2
 
 
 class GmStats(ctypes.Structure):
     _fields_ = ([(f, ctypes.c_uint32) for f in STATS_FIELDS] + [(f, ctypes.c_uint64) for f in STATS_FIELDS64] +
-                [(f, ctypes.c_float) for f in STATS_FIELDS_MS])
+                [(f, ctypes.c_float) for f in STATS_FIELDS_MS] +
+                [(f, ctypes.c_uint32) for f in STATS_FIELDS_WAF])
 
 
 class GmBatch(ctypes.Structure):
@@ -117,7 +119,7 @@ class Engine:
     def stats(self) -> dict:
         s = GmStats()
         self._chk(lib().gm_stats(self.h, ctypes.byref(s)))
-        return {f: getattr(s, f) for f in STATS_FIELDS + STATS_FIELDS64 + STATS_FIELDS_MS}
+        return {f: getattr(s, f) for f in STATS_FIELDS + STATS_FIELDS64 + STATS_FIELDS_MS + STATS_FIELDS_WAF}
 
     def match_ptr(self, reqs_ptr, arena_ptr, arena_len, n, out_ptr, hits_ptr, hit_cap, stream=0, host=False):
         b = GmBatch(reqs_ptr, arena_ptr, arena_len, n, GM_BATCH_HOST if host else 0)
@@ -146,6 +148,17 @@ class Engine:
         s = stream if stream is not None else torch.cuda.current_stream()
         self.match_ptr(reqs_t.data_ptr(), arena_t.data_ptr(), arena_len, reqs_t.numel() // 64, out_t.data_ptr(),
                        hits_t.data_ptr(), hits_t.numel(), s.cuda_stream)
+
+    def debug_status(self) -> np.ndarray:
+        """The last batch's device status words (gm_waf.inc: counts and profiling counters)."""
+        out = np.zeros(128, dtype=np.uint32)
+        L = lib()
+        L.gm_debug_status.restype = ctypes.c_int
+        L.gm_debug_status.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        rc = L.gm_debug_status(self.h, out.ctypes.data, 128)
+        if rc < 0:
+            self._chk(rc)
+        return out
 
     def counters(self) -> np.ndarray:
         n = self.stats()["n_counters"]

@@ -31,6 +31,16 @@ DEF_KERNEL(k_bfe, "v_bfe_u32 %0, %0, %1, 5")
 DEF_KERNEL(k_bitop3, "v_bitop3_b32 %0, %0, %1, %0 bitop3:0x6c")
 DEF_KERNEL(k_alignbyte, "v_alignbyte_b32 %0, %0, %1, 1")
 DEF_KERNEL(k_perm, "v_perm_b32 %0, %0, %1, %1")
+DEF_KERNEL(k_pk_mul16, "v_pk_mul_lo_u16 %0, %0, %1")
+DEF_KERNEL(k_pk_lshl16, "v_pk_lshlrev_b16 %0, %0, %1")
+DEF_KERNEL(k_min3, "v_min3_u32 %0, %0, %1, %0")
+DEF_KERNEL(k_dot4, "v_dot4_u32_u8 %0, %0, %1, %0")
+DEF_KERNEL(k_lshl_add, "v_lshl_add_u32 %0, %0, 3, %1")
+DEF_KERNEL(k_and_or, "v_and_or_b32 %0, %0, %1, %0")
+DEF_KERNEL(k_bfi, "v_bfi_b32 %0, %1, %0, %1")
+DEF_KERNEL(k_lshr, "v_lshrrev_b32 %0, 7, %0")
+DEF_KERNEL(k_mad_u24, "v_mad_u32_u24 %0, %0, %1, %1")
+DEF_KERNEL(k_pk_mad16, "v_pk_mad_u16 %0, %0, %1, %1")
 
 __global__ void k_mad64(uint32_t *out, uint32_t seed) {
     uint64_t x[CHAINS];
@@ -84,7 +94,10 @@ int main() {
         {"v_mul_lo_u32", k_mul_lo}, {"v_mul_hi_u32", k_mul_hi}, {"v_mul_u32_u24", k_mul_u24},
         {"v_mul_hi_u32_u24", k_mul_hi_u24}, {"v_xor_b32", k_xor}, {"v_lshl_or_b32", k_lshl_or},
         {"v_bfe_u32", k_bfe}, {"v_bitop3_b32", k_bitop3}, {"v_alignbyte_b32", k_alignbyte},
-        {"v_perm_b32", k_perm}, {"v_mad_u64_u32", k_mad64}};
+        {"v_perm_b32", k_perm}, {"v_mad_u64_u32", k_mad64},
+        {"v_pk_mul_lo_u16", k_pk_mul16}, {"v_pk_lshlrev_b16", k_pk_lshl16}, {"v_min3_u32", k_min3},
+        {"v_dot4_u32_u8", k_dot4}, {"v_lshl_add_u32", k_lshl_add}, {"v_and_or_b32", k_and_or},
+        {"v_bfi_b32", k_bfi}, {"v_lshrrev_b32", k_lshr}, {"v_mad_u32_u24", k_mad_u24}, {"v_pk_mad_u16", k_pk_mad16}};
     for (auto &k : ks) {
         hipLaunchKernelGGL(k.f, dim3(blocks), dim3(threads), 0, 0, d, 1u);
         (void)hipEventRecord(a);

@@ -118,6 +118,43 @@ def test_waf_scan_every_alignment(eng):
     assert (exp["n_hits"] == 1).sum() == len(items)
 
 
+def test_waf_zone_boundaries(eng):
+    """Patterns at the first and last byte of every zone, at both arena parities (the stride-2
+    scan keys 4-byte patterns on windows that begin a byte before or end a byte after them, i.e.
+    possibly in the neighbouring zone or request)."""
+    rules = [sigs.Rule("lit", True, "uahb", b"/zq9"), sigs.Rule("lit", False, "ahb", b"kx7w"),
+             sigs.Rule("re", False, "uahb", r"(k7fo|0ovr|gizw3)[a-z0-9]+--"),
+             sigs.Rule("re", True, "ahb", r"qvxj\s*\(\d+\)"), sigs.Rule("lit", True, "ahb", b"jjqqz")]
+    b = workloads.c4_blob(sigs.SigSet(rules))
+    rng = np.random.Generator(np.random.PCG64(11))
+    toks = [b"kx7w", b"k7foab--", b"QVXJ(12)", b"jjqqz", b"0ovr9--"]
+    items = []
+    for i in range(4000):
+        t = toks[i % len(toks)]
+        pad = b"a" * int(rng.integers(0, 7))
+        where = (i // len(toks)) % 6
+        it = {"host": "cafe.example.com", "uri": "/tea/zq9" + "b" * int(rng.integers(0, 5)), "https": True}
+        if where == 0:
+            it["args"] = (t + pad).decode()
+        elif where == 1:
+            it["args"] = (pad + t).decode()
+        elif where == 2:
+            it["headers"] = [(t.decode(), "v" + pad.decode())]
+        elif where == 3:
+            it["body"] = t + pad
+            it["args"] = pad.decode()
+        elif where == 4:
+            it["body"] = pad + t
+        else:
+            it["uri"] = "/tea" + pad.decode() + "/zq9"
+            it["args"] = (t + pad).decode()
+        items.append(it)
+    reqs, arena = records.from_dicts(items)
+    got, gh, exp, eh = run_both(eng, b, reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "zone-boundaries")
+    assert (exp["n_hits"] >= 2).sum() > 3000
+
+
 def test_e2e_kats_on_gpu(eng):
     adv = golden("advanced_routing.json")
     for case in adv["cases"]:

@@ -123,28 +123,29 @@ def test_c4_signature_set_compiles():
     assert s["n_sig_regex_always"] == 0
 
 
-def _prefilter(e, arena):
+def _prefilter(e, arena, stage2=False):
     L = ctypes.CDLL(engine.LIB_PATH)
-    L.gm_debug_waf_prefilter.restype = ctypes.c_int64
-    L.gm_debug_waf_prefilter.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
-                                         ctypes.c_size_t]
+    f = L.gm_debug_waf_prefilter2 if stage2 else L.gm_debug_waf_prefilter
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
     a = np.ascontiguousarray(arena)
-    n = L.gm_debug_waf_prefilter(e.h, a.ctypes.data, a.size, None, 0)
+    n = f(e.h, a.ctypes.data, a.size, None, 0)
     out = np.zeros(max(n, 1), np.uint64)
-    L.gm_debug_waf_prefilter(e.h, a.ctypes.data, a.size, out.ctypes.data, n)
+    f(e.h, a.ctypes.data, a.size, out.ctypes.data, n)
     return out[:n]
 
 
-def test_prefilter_covers_every_literal_occurrence():
-    """Host restatement of the scan kernel's candidate rule: every occurrence of every literal
-    (any case for nocase rules) yields a candidate inside the occurrence, and the false-positive
-    rate on the C4 traffic stays small."""
+@pytest.mark.parametrize("stage2", [False, True])
+def test_prefilter_covers_every_literal_occurrence(stage2):
+    """Host restatement of the scan kernel's candidate rule (and of k_waf_verify's stage-2
+    context filter): every occurrence of every literal (any case for nocase rules) yields a
+    candidate inside the occurrence, and the false-positive rate on the C4 traffic stays small."""
     from gpumatch import records
     ss = workloads.c4_sigset(800, 200)
     e = engine.Engine(compile_only=True)
     e.load(workloads.c4_blob(ss), 3)
     reqs, arena = records.gen_c4(3000, ss, plant_rate=0.3)
-    cand = np.sort(_prefilter(e, arena))
+    cand = np.sort(_prefilter(e, arena, stage2))
     a = bytes(arena)
     al = a.lower()
     checked = 0
@@ -155,9 +156,12 @@ def test_prefilter_covers_every_literal_occurrence():
         hay, needle = (al, pat.lower()) if r.nocase else (a, pat)
         start = hay.find(needle)
         while start >= 0:
-            k = np.searchsorted(cand, start)
-            assert k < len(cand) and cand[k] <= start + len(pat) - 4, (pat, start)
+            # stride-2 scan: the candidate is an even offset in [start - 1, start + len - 4]
+            # (4-byte literals: [start - 1, start + 1], the one-byte-extended key families)
+            k = np.searchsorted(cand, start - 1)
+            assert k < len(cand) and cand[k] <= start + max(len(pat) - 4, 1), (pat, start)
+            assert cand[k] % 2 == 0
             checked += 1
             start = hay.find(needle, start + 1)
     assert checked > 200
-    assert len(cand) < len(a) * 2e-3
+    assert len(cand) < len(a) * (5e-4 if stage2 else 2e-3)
