@@ -55,7 +55,8 @@ def main():
     # ---- generation: C4 signature set on the cafe Ingress, wallarm mode block
     t0 = time.time()
     ss = workloads.c4_sigset()
-    gblob = workloads.c4_blob(ss, "block")
+    # benign traffic sample (disjoint seed) for the prefilter's key / hash choice (GM_ENTRY_SAMPLE)
+    gblob = workloads.c4_blob(ss, "block", sample=workloads.c4_sample(ss))
     eng = engine.Engine(local, profile=True)
     eng.load(gblob, 1)
     st = eng.stats()

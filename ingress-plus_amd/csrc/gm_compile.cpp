@@ -672,15 +672,57 @@ const char *kBackground =
     "navigate same-origin cors upgrade-insecure-requests x-forwarded-for x-request x-trace-id "
     "if-none-match etag utf-8 charset boundary multipart form-data urlencoded";
 
+// Standard request header lines as they sit in a header block (CRLF-separated): every request
+// carries a dozen of them, so their folded 4-grams ("\r\nUs" -> "-*us") are the most frequent
+// windows a scan sees and must not test positive in the prefilter.
+const char *kHeaderLines[] = {
+    "Host: ", "User-Agent: Mozilla/5.0 (Windows NT 10.0; Win64; x64) AppleWebKit/537.36 (KHTML, like Gecko)",
+    "Accept: text/html,application/xhtml+xml,application/xml;q=0.9,image/webp,*/*;q=0.8",
+    "Accept-Language: en-US,en;q=0.9", "Accept-Encoding: gzip, deflate, br", "Connection: keep-alive",
+    "Referer: https://www.", "Cache-Control: no-cache, max-age=0", "Upgrade-Insecure-Requests: 1",
+    "X-Forwarded-For: ", "X-Forwarded-Proto: https", "X-Real-IP: ", "X-Request-ID: ", "X-Requested-With: ",
+    "Sec-Fetch-Mode: navigate", "Sec-Fetch-Site: same-origin", "Sec-Fetch-Dest: document", "DNT: 1",
+    "Pragma: no-cache", "Origin: https://", "Content-Type: application/json", "Content-Length: ",
+    "Authorization: Bearer ", "If-None-Match: W/\"", "If-Modified-Since: ", "Cookie: session=",
+    "X-Client-Version: ", "X-Trace-Id: ", "X-Request-Start: t="};
+// separators words meet in URIs, query strings, JSON, form data and text
+const char *kSeps[] = {" ", "\n", "\r\n", "_", "-", "/", ":", "=", "&", ".", ",", "\"", "\": \"", ", ", ". "};
+
+// folded 4-gram -> relative weight (header-line grams 16, word/separator grams by word rank)
+const std::unordered_map<uint32_t, double> &background_weights() {
+    static std::unordered_map<uint32_t, double> g = [] {
+        std::unordered_map<uint32_t, double> m;
+        auto add = [&](const std::string &t, double wt) {
+            for (size_t i = 0; i + 4 <= t.size(); i++) {
+                uint32_t w;
+                memcpy(&w, t.data() + i, 4);
+                double &x = m[fold4(w)];
+                x = std::max(x, wt);
+            }
+        };
+        add(std::string(kBackground), 0.05);
+        std::vector<std::string> words;
+        {
+            std::string t(kBackground), cur;
+            for (char ch : t) { if (ch == ' ') { if (!cur.empty()) words.push_back(cur); cur.clear(); } else cur += ch; }
+            if (!cur.empty()) words.push_back(cur);
+        }
+        // kBackground lists the English words by frequency: Zipf weights by rank
+        for (size_t r = 0; r < words.size(); r++)
+            for (const char *a : kSeps)
+                for (const char *b : kSeps) add(std::string(a) + words[r] + b, 50.0 / (double)(r + 10));
+        std::string hb;
+        for (const char *h : kHeaderLines) hb += std::string("\r\n") + h + "\r\n";
+        add(hb, 16.0);
+        return m;
+    }();
+    return g;
+}
+
 const std::set<uint32_t> &background_grams() {
     static std::set<uint32_t> g = [] {
         std::set<uint32_t> s;
-        std::string t(kBackground);
-        for (size_t i = 0; i + 4 <= t.size(); i++) {
-            uint32_t w = (uint8_t)t[i] | (uint32_t)(uint8_t)t[i + 1] << 8 | (uint32_t)(uint8_t)t[i + 2] << 16 |
-                         (uint32_t)(uint8_t)t[i + 3] << 24;
-            s.insert(fold4(w));
-        }
+        for (auto &kv : background_weights()) s.insert(kv.first);
         return s;
     }();
     return g;
@@ -782,10 +824,14 @@ KeyChoice choose_keys(const std::string &pat, const KeyModel &M, std::unordered_
         cl += M.cost(z | (w << 8));
         if (ys[z]) cr += M.cost((w >> 8) | (z << 24));
     }
+    // every key also costs prefilter precision (Bloom load): a right-hand family restricted by a
+    // follow set of at most 32 bytes wins unless it is far costlier in benign traffic
+    const size_t nr = ys.count();
+    const bool left = nr <= 32 ? cl * 8 < cr : cl <= cr;
     r.keys.push_back({w, 0});
     for (uint32_t z = 0; z < 256; z++) {
         if ((z | 0x20u) != z) continue;
-        if (cl <= cr) r.keys.push_back({z | (w << 8), -1});
+        if (left) r.keys.push_back({z | (w << 8), -1});
         else if (ys[z]) r.keys.push_back({(w >> 8) | (z << 24), 1});
     }
     return r;
@@ -799,6 +845,24 @@ const uint32_t kBloomMuls[] = {0x9E3779B1u, 0x85EBCA77u, 0xC2B2AE3Du, 0x27D4EB2F
                                0xFD7046C5u, 0xB55A4F09u, 0x7FEB352Du, 0x846CA68Bu, 0x2C1B3C6Du, 0x297A2D39u,
                                0xE6546B64u | 1u, 0x1B873593u, 0xCC9E2D51u, 0x5BD1E995u};
 
+// the 16 fixed multipliers plus 48 more odd ones from a fixed-seed splitmix sequence
+const std::vector<uint32_t> &bloom_mul_candidates() {
+    static std::vector<uint32_t> v = [] {
+        std::vector<uint32_t> r(std::begin(kBloomMuls), std::end(kBloomMuls));
+        uint64_t x = 0x243F6A8885A308D3ull;
+        while (r.size() < 64) {
+            x += 0x9E3779B97F4A7C15ull;
+            uint64_t z = x;
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            z ^= z >> 31;
+            r.push_back((uint32_t)z | 1u);
+        }
+        return r;
+    }();
+    return v;
+}
+
 struct BloomChoice { uint32_t mul = 0; double fp = 0; };   // fp: weighted false positives per window
 BloomChoice choose_bloom_mul(const std::vector<uint32_t> &keys, uint32_t pk, const KeyModel &M,
                              std::vector<uint32_t> &filter) {
@@ -807,10 +871,10 @@ BloomChoice choose_bloom_mul(const std::vector<uint32_t> &keys, uint32_t pk, con
     if (M.n > 0) {
         for (auto &kv : M.cnt) if (!kset.count(kv.first)) test.push_back({kv.first, kv.second / M.n});
     } else {
-        for (uint32_t g : background_grams()) if (!kset.count(g)) test.push_back({g, 1.0 / 65536});
+        for (auto &kv : background_weights()) if (!kset.count(kv.first)) test.push_back({kv.first, kv.second / 65536});
     }
     BloomChoice best{kBloomMuls[0], 1e300};
-    for (uint32_t mul : kBloomMuls) {
+    for (uint32_t mul : bloom_mul_candidates()) {
         std::fill(filter.begin(), filter.end(), 0u);
         for (uint32_t k : keys) { const BloomProbe b = bloom_probe(k, mul, pk); filter[b.block] |= b.mask; }
         double fp = 0;
@@ -1135,8 +1199,9 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     for (const LitE &e : lits) {
         const int k = e.lit.key_off, L = (int)e.bytes.size();
         auto cb = [&](int i) { return (uint32_t)(uint8_t)e.bytes[i] | 0x20u; };
-        const uint32_t nl = k <= 0 ? 0u : (uint32_t)std::min(2, k);
-        const uint32_t nr = (uint32_t)std::max(0, std::min(2, L - (k + 4)));
+        uint32_t nl = k <= 0 ? 0u : (uint32_t)std::min(2, k);
+        uint32_t nr = (uint32_t)std::max(0, std::min(2, L - (k + 4)));
+        ctx_canon(nl, nr);
         const uint32_t l2 = (nl >= 2 ? cb(k - 2) : 0u) | (nl >= 1 ? cb(k - 1) << 8 : 0u);
         const uint32_t r2 = (nr >= 1 ? cb(k + 4) : 0u) | (nr >= 2 ? cb(k + 5) << 8 : 0u);
         const BloomProbe b = bloom_probe(ctx_key(e.key, l2, r2, nl * 3 + nr), CTX_MUL_DEFAULT, CTX_PK);
@@ -1155,7 +1220,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         buckets.back().second.second++;
     }
     // probes per window: pk = 2 or 3 (K = 4 or 6 bits), whichever minimises scan + verify cost:
-    // pk = 3 costs ~17 % more scan VALU per probe; a false positive costs ~700 probes of verify
+    // pk = 3 costs ~20 % more scan time per probe (measured: 4.2 -> 5.9 ms on C4); a false
+    // positive costs ~20 probes' worth (its 32-byte record and the stage-2 context test)
     uint32_t bloom_pk = BLOOM_PK_DEFAULT, bloom_mul = kBloomMuls[0];
     if (!keys.empty()) {
         int forced = 0;
@@ -1165,7 +1231,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         if (!forced) {
             std::vector<uint32_t> f3(BLOOM_WORDS, 0);
             BloomChoice b3 = choose_bloom_mul(keys, 3, KM, f3);
-            if (0.17 + 700.0 * b3.fp < 700.0 * b.fp) { b = b3; bloom_pk = 3; waf_a.swap(f3); }
+            if (0.2 + 20.0 * b3.fp < 20.0 * b.fp) { b = b3; bloom_pk = 3; waf_a.swap(f3); }
         }
         bloom_mul = b.mul;
         st.bloom_fp_ppm = (uint32_t)std::min(1e9, b.fp * 1e6);

@@ -875,6 +875,8 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
         if (c->scan_depth == 1) k_waf_scan<2, 1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 2) k_waf_scan<2, 2><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 6) k_waf_scan<2, 6><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else if (c->scan_depth == 101) k_waf_scan<2, 4, 1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else if (c->scan_depth == 102) k_waf_scan<2, 4, 2><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
     } else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
     HIPCHK(c, hipGetLastError());
@@ -1121,12 +1123,12 @@ extern "C" int64_t gm_debug_waf_prefilter2(gm_ctx *c, const uint8_t *A, size_t l
         const int64_t q = (int64_t)p;
         const uint32_t l2 = fb(q - 2) | fb(q - 1) << 8, r2 = fb(q + 4) | fb(q + 5) << 8;
         bool hit = false;
-        for (uint32_t nl = 0; nl < 3 && !hit; nl++)
-            for (uint32_t nr = 0; nr < 3 && !hit; nr++) {
-                const BloomProbe b2 = bloom_probe(ctx_key(w, l2 & ctx_lmask(nl), r2 & ctx_rmask(nr), nl * 3 + nr),
-                                                  h.ctx_mul, CTX_PK);
-                hit = (ctxb[b2.block] & b2.mask) == b2.mask;
-            }
+        for (int i = 0; i < CTX_SHAPES && !hit; i++) {
+            const uint32_t nl = ctx_shape_nl(i), nr = ctx_shape_nr(i);
+            const BloomProbe b2 = bloom_probe(ctx_key(w, l2 & ctx_lmask(nl), r2 & ctx_rmask(nr), nl * 3 + nr),
+                                              h.ctx_mul, CTX_PK);
+            hit = (ctxb[b2.block] & b2.mask) == b2.mask;
+        }
         if (hit) { if ((size_t)k < cap && out) out[k] = p; k++; }
     }
     return k;

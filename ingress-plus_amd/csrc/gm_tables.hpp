@@ -218,15 +218,26 @@ __host__ __device__ inline BloomProbe bloom_probe(uint32_t w, uint32_t mul, uint
     return BloomProbe{lo >> (32 - BLOOM_LOG2), m};
 }
 // Stage-2 context filter (waf_b, same size as the scan Bloom filter; staged into LDS by
-// k_waf_verify).  A scan candidate window w at arena offset p survives only if waf_b holds w
+// k_waf_ctx).  A scan candidate window w at arena offset p survives only if waf_b holds w
 // together with the folded bytes around it that its pattern fixes: up to two on the left
 // (l2 = A[p-2] | A[p-1] << 8) and two on the right (r2 = A[p+4] | A[p+5] << 8).  Each key entry
-// inserts one shape (nl, nr = bytes its pattern has on each side, 0..2); a window is probed with
-// all nine shapes.  Bytes outside the arena read as the fold of 0 (0x20).
+// inserts one shape (nl, nr = context bytes used on each side): the bytes its pattern has,
+// canonicalised to one of the CTX_SHAPES shapes (ctx_canon); a window is probed with all of
+// them.  Bytes outside the arena read as the fold of 0 (0x20).
 constexpr uint32_t CTX_PK = 3;
 constexpr uint32_t CTX_MUL_DEFAULT = 0x7FEB352Du;
 __host__ __device__ inline uint32_t ctx_lmask(uint32_t nl) { return nl == 0 ? 0u : nl == 1 ? 0xFF00u : 0xFFFFu; }
 __host__ __device__ inline uint32_t ctx_rmask(uint32_t nr) { return nr == 0 ? 0u : nr == 1 ? 0x00FFu : 0xFFFFu; }
+// the probed shapes, as nl * 3 + nr: (2,2) (1,1) (1,0) (0,1) (0,0)
+constexpr int CTX_SHAPES = 5;
+__host__ __device__ inline uint32_t ctx_shape_nl(int i) { return i == 0 ? 2u : i <= 2 ? 1u : 0u; }
+__host__ __device__ inline uint32_t ctx_shape_nr(int i) { return i == 0 ? 2u : (i == 1 || i == 3) ? 1u : 0u; }
+// the largest probed shape within the context (nl, nr) a pattern has
+__host__ __device__ inline void ctx_canon(uint32_t &nl, uint32_t &nr) {
+    if (nl == 2 && nr == 2) return;
+    if (nl >= 1 && nr >= 1) { nl = nr = 1; return; }
+    nl = nl ? 1u : 0u; nr = nr ? 1u : 0u;
+}
 __host__ __device__ inline uint32_t ctx_key(uint32_t w, uint32_t l2, uint32_t r2, uint32_t shape) {
     uint32_t c = (l2 * 0x9E3779B1u) ^ (r2 * 0x85EBCA77u) ^ ((shape + 1u) * 0xC2B2AE3Du);
     c ^= c >> 15;

@@ -11,14 +11,18 @@ from __future__ import annotations
 import struct
 
 MAGIC = 0x31424D47
-ENTRY_MAIN, ENTRY_CONFD, ENTRY_SIGS = 1, 2, 3
+ENTRY_MAIN, ENTRY_CONFD, ENTRY_SIGS, ENTRY_SAMPLE = 1, 2, 3, 4
 
 
 def _b(x):
     return x.encode() if isinstance(x, str) else bytes(x)
 
 
-def make_blob(main: str | bytes | None, confd: dict, sigs_text: str | bytes | None = None) -> bytes:
+def make_blob(main: str | bytes | None, confd: dict, sigs_text: str | bytes | None = None,
+              sample: bytes | None = None) -> bytes:
+    """``sample``: optional benign traffic bytes (GM_ENTRY_SAMPLE) -- the compiler uses them only to
+    choose the WAF prefilter's key windows and hash multiplier; matching results never depend
+    on it."""
     entries = []
     if main is not None:
         entries.append((ENTRY_MAIN, b"nginx.conf", _b(main)))
@@ -26,6 +30,8 @@ def make_blob(main: str | bytes | None, confd: dict, sigs_text: str | bytes | No
         entries.append((ENTRY_CONFD, _b(name) + b".conf", _b(confd[name])))
     if sigs_text is not None:
         entries.append((ENTRY_SIGS, b"signatures", _b(sigs_text)))
+    if sample is not None:
+        entries.append((ENTRY_SAMPLE, b"sample", _b(sample)))
     out = [struct.pack("<II", MAGIC, len(entries))]
     for kind, name, data in entries:
         out.append(struct.pack("<III", kind, len(name), len(data)))

@@ -76,13 +76,26 @@ def c2_blob() -> bytes:
     return blob.make_blob(confgen.render_main(), files)
 
 
-def c4_blob(sigset: sigs.SigSet, mode: str = "block") -> bytes:
+def c4_sample(sigset: sigs.SigSet, n: int = 2000, seed: int = records.SEED_BASE + 33) -> bytes:
+    """A benign traffic sample for the WAF prefilter tuning (GM_ENTRY_SAMPLE): C4 requests from a
+    seed disjoint from every pool the tests and the bench match (a deployment samples its own
+    recent traffic the same way); the zone bytes only."""
+    reqs, arena = records.gen_c4(n, sigset, seed=seed, plant_rate=0.0, pool_mb=2)
+    parts = []
+    for r in reqs:
+        b = int(r["base"])
+        z = int(r["uri_len"]) + int(r["args_len"]) + int(r["hdr_len"]) + int(r["body_len"])
+        parts.append(arena[b:b + z].tobytes())
+    return b"".join(parts)
+
+
+def c4_blob(sigset: sigs.SigSet, mode: str = "block", sample: bytes | None = None) -> bytes:
     base = confgen.default_config_params()
     base["MainEnableWallarm"] = True
     ing = copy.deepcopy(CAFE_INGRESS)
     ing["metadata"]["annotations"] = {"wallarm.com/mode": mode}
     files = confgen.ingress_files([ing], base=base, secrets=("cafe-secret",))
-    return blob.make_blob(confgen.render_main(base), files, sigset.to_text())
+    return blob.make_blob(confgen.render_main(base), files, sigset.to_text(), sample)
 
 
 def c5_blob(n_hosts: int = 1000, seed: int = records.SEED_BASE + 4) -> bytes:

@@ -492,6 +492,7 @@ orc_ctx *orc_create(const void *blob, size_t len, uint32_t gen) {
         memcpy(&kind, b + off, 4); memcpy(&nl, b + off + 4, 4); memcpy(&dl, b + off + 8, 4); off += 12;
         const char *data = (const char *)b + off + nl; off += nl + dl;
         if (kind == GM_ENTRY_SIGS) { sigt = data; sign = (int)dl; continue; }
+        if (kind == GM_ENTRY_SAMPLE) continue;   /* traffic sample: tunes the GPU prefilter only */
         dir_t *root = calloc(1, sizeof(dir_t));
         lexer L = {data, (int)dl, 0, malloc(dl + 1)};
         if (parse_block(&L, root, 0) < 0) { seterr("config parse error", NULL); return NULL; }

@@ -30,7 +30,7 @@ def main():
     from oracle_py import Oracle
 
     ss = workloads.c4_sigset()
-    blob = workloads.c4_blob(ss, "block")
+    blob = workloads.c4_blob(ss, "block", sample=workloads.c4_sample(ss))   # as bench.py
     reqs, arena = records.gen_c4(args.pool, ss, seed=records.SEED_BASE + 3)
     m = args.oracle_n or len(reqs)
     e = engine.Engine(0)

@@ -58,10 +58,14 @@ def test_c4_waf_parity_small_set(eng, mode):
         assert len(eh) == 0
 
 
-def test_c4_waf_parity_10k_rules(eng):
+@pytest.mark.parametrize("sample", [False, True])
+def test_c4_waf_parity_10k_rules(eng, sample):
+    """The bench's rule set, with and without a traffic sample in the generation (the sample
+    only steers the prefilter's key choice; verdicts must not depend on it)."""
     ss = workloads.c4_sigset()
     reqs, arena = records.gen_c4(6_000, ss, plant_rate=0.05)
-    got, gh, exp, eh = run_both(eng, workloads.c4_blob(ss), reqs, arena)
+    smp = workloads.c4_sample(ss, 500) if sample else None
+    got, gh, exp, eh = run_both(eng, workloads.c4_blob(ss, sample=smp), reqs, arena)
     assert_verdicts_equal(got, exp, gh, eh, "C4-10k")
     assert (exp["action"] == 6).sum() > 100
 
