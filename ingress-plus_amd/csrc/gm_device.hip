@@ -621,7 +621,10 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
 constexpr int ROUTE_BLOCK = 256;
 constexpr uint32_t LDS_HIST_MAX = 2048;
 
-__global__ __launch_bounds__(ROUTE_BLOCK) void k_route(const gm_req *__restrict__ reqs, uint32_t n,
+// WPE: waves per SIMD the register allocation targets (beside the scan's workgroup, a CU has
+// room for route waves only when they are small)
+template <int WPE>
+__global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_route(const gm_req *__restrict__ reqs, uint32_t n,
                                                        const uint8_t *__restrict__ A, uint64_t arena_len,
                                                        GTab t, gm_verdict *__restrict__ out,
                                                        unsigned long long *__restrict__ counters,
@@ -705,11 +708,18 @@ struct gm_ctx {
     ncclComm_t comm = nullptr;
     uint64_t last_candidates = 0, last_pairs = 0, last_hits = 0, last_ctx_pass = 0, last_jobs = 0;
     hipEvent_t ev[5] = {};
+    hipEvent_t ev_route[2] = {};   // GM_CREATE_PROFILE: route kernel on the side stream
+    // side stream: k_route runs beside the WAF scan (independent inputs) and joins before the
+    // exact check, which needs its blk2rec map
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool ev_pending = false;
     int ev_used = 0;
     float last_ms[4] = {0, 0, 0, 0};
+    bool route_side = false;   // last batch ran k_route on the side stream
     int cu_count = 256;
     int scan_depth = SCAN_DEPTH;   // chunks in flight per scan wave (GM_SCAN_DEPTH tuning knob)
+    int route_wpe = 3;             // k_route register target, waves per SIMD (GM_ROUTE_WPE tuning knob)
     std::mutex mu;
 };
 
@@ -751,12 +761,20 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
             c->cu_count = cus;
         if (const char *ev = getenv("GM_SCAN_DEPTH")) c->scan_depth = atoi(ev);
+        if (const char *ev = getenv("GM_ROUTE_WPE")) c->route_wpe = atoi(ev);
         if (hipMalloc((void **)&c->d_status, STATUS_WORDS * 4) != hipSuccess ||
             hipHostMalloc((void **)&c->h_status, STATUS_WORDS * 4, hipHostMallocDefault) != hipSuccess) {
             t_err = "status alloc failed"; delete c; return nullptr;
         }
-        if (flags & GM_CREATE_PROFILE)
+        if (flags & GM_CREATE_PROFILE) {
             for (auto &e : c->ev) (void)hipEventCreate(&e);
+            for (auto &e : c->ev_route) (void)hipEventCreate(&e);
+        }
+        if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+            t_err = "stream/event create failed"; delete c; return nullptr;
+        }
     }
     return c;
 }
@@ -775,6 +793,10 @@ void gm_destroy(gm_ctx *c) {
         if (c->h_status) (void)hipHostFree(c->h_status);
         if (c->comm) ncclCommDestroy(c->comm);
         for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
+        for (auto &e : c->ev_route) if (e) (void)hipEventDestroy(e);
+        if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+        if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+        if (c->side) (void)hipStreamDestroy(c->side);
     }
     delete c->gen;
     delete c;
@@ -839,18 +861,43 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
         return GM_OK;
     };
     c->ev_used = 0;
+    c->route_side = false;
     HIPCHK(c, hipMemsetAsync(c->d_status, 0, STATUS_WORDS * 4, s));
     if (mark(0)) return GM_E_HIP;
-    {
-        uint32_t blocks = std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK, (uint32_t)c->cu_count * 8);
-        if (blocks == 0) blocks = 1;
-        k_route<<<blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, c->d_counters,
-                                                waf ? c->d_blk2rec : nullptr, nblk);
-        HIPCHK(c, hipGetLastError());
-    }
-    if (mark(1)) return GM_E_HIP;
+    const uint32_t route_blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
+                                                                           (uint32_t)c->cu_count * 8));
     c->last_candidates = c->last_pairs = c->last_hits = c->last_ctx_pass = c->last_jobs = 0;
-    if (!waf || n == 0) return GM_OK;
+    if (!waf || n == 0) {
+        k_route<3><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, c->d_counters, nullptr, nblk);
+        HIPCHK(c, hipGetLastError());
+        return mark(1) ? GM_E_HIP : GM_OK;
+    }
+    // fork: k_route on the side stream, overlapping the WAF scan and context filter (the scan is
+    // HBM/VALU-bound with one 1024-thread workgroup per CU; route waves fit beside it).  The
+    // route launch is issued after the scan's, so the scan's workgroups claim the CUs first.
+    HIPCHK(c, hipEventRecord(c->ev_fork, s));
+    HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    auto launch_route = [&]() -> int {
+        if (prof) HIPCHK(c, hipEventRecord(c->ev_route[0], c->side));
+        if (c->route_wpe == 5)
+            k_route<5><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
+                                                                  c->d_blk2rec, nblk);
+        else if (c->route_wpe == 6)
+            k_route<6><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
+                                                                  c->d_blk2rec, nblk);
+        else if (c->route_wpe == 4)
+            k_route<4><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
+                                                                  c->d_blk2rec, nblk);
+        else
+            k_route<3><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
+                                                                  c->d_blk2rec, nblk);
+        HIPCHK(c, hipGetLastError());
+        if (prof) HIPCHK(c, hipEventRecord(c->ev_route[1], c->side));
+        HIPCHK(c, hipEventRecord(c->ev_join, c->side));
+        c->route_side = true;
+        return GM_OK;
+    };
+    if (mark(1)) return GM_E_HIP;
 
     // candidate records: 32 B (4 x u64) each, room for one per 64 arena bytes (a lane with a
     // candidate window in every 4th 16-byte slice) -- overflow is reported, never truncated
@@ -880,11 +927,13 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
         else k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
     } else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
     HIPCHK(c, hipGetLastError());
+    if ((e = launch_route())) return e;
     if (mark(2)) return GM_E_HIP;
     const uint32_t bcap = (uint32_t)std::min<size_t>(c->cap_surv / scan_blocks, 0xFFFFFFFFu);
     k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, c->d_ccnt, W, t, c->d_surv, bcap, c->d_ccnt + W,
                                                 c->d_status);
     HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipStreamWaitEvent(s, c->ev_join, 0));   // join: verdicts and blk2rec are written
     constexpr uint32_t EXACT_SUB = 8;
     k_waf_exact<<<scan_blocks * EXACT_SUB, 256, 0, s>>>(A, alen, reqs, n, c->d_blk2rec, t, c->d_surv, bcap,
                                                          c->d_ccnt + W, EXACT_SUB, c->d_pairs, (uint32_t)c->cap_pairs,
@@ -983,6 +1032,8 @@ int gm_sync(gm_ctx *c, void *stream) {
             c->last_ms[k] = 0;
             if (k + 1 < c->ev_used) (void)hipEventElapsedTime(&c->last_ms[k], c->ev[k], c->ev[k + 1]);
         }
+        // overlapped route: its own time on the side stream (the scan's stage starts at the fork)
+        if (c->route_side) (void)hipEventElapsedTime(&c->last_ms[0], c->ev_route[0], c->ev_route[1]);
         c->ev_pending = false;
     }
     if (c->h_status[3]) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded");
