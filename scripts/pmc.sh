@@ -3,6 +3,7 @@
 # only -- never combined with sys/runtime traces).  Output: gpurun_out/pmc_${TAG}_<pass>/.
 #   pass hbm: FETCH_SIZE, WRITE_SIZE is a separate pass (TCC slots)  -> roofline.traffic
 #   pass sq : instruction mix and wave stall cycles of the scan / route / verify kernels
+#   pass lds: LDS bank / address conflicts and unaligned stalls (the LDS Bloom probes)
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 TAG=${TAG:-r1}
@@ -10,7 +11,7 @@ ARGS="--steps 2 --warmup 1 --no-cpu ${BENCH_ARGS}"
 cd /tmp && export TMPDIR=/tmp
 run() {
   local name=$1; shift
-  timeout -k 10 600 rocprofv3 --kernel-trace --pmc "$@" --kernel-include-regex 'k_(waf|route|pairs)' \
+  timeout -s KILL 240 rocprofv3 --kernel-trace --pmc "$@" --kernel-include-regex 'k_(waf|route|pairs)' \
     -d "$GRAFT_REPO_ROOT/gpurun_out/pmc_${TAG}_${name}" -o run --output-format csv \
     -- python "$GRAFT_REPO_ROOT/bench.py" $ARGS > "$GRAFT_REPO_ROOT/gpurun_out/pmc_${TAG}_${name}.log" 2>&1
   local rc=$?
@@ -19,7 +20,8 @@ run() {
 }
 run fetch FETCH_SIZE &&
 run write WRITE_SIZE &&
-run sq SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU
+run sq SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SALU &&
+run lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_LDS SQ_WAVE_CYCLES
 rc=$?
 # per-kernel summary (FETCH_SIZE is in KiB; on gfx950 it counts half the bytes of wide streaming
 # reads -- MI355X_MICROARCH.md, HBM section -- so the scan's HBM bytes = 2 x FETCH_SIZE x 1024)

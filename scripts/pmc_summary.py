@@ -9,7 +9,7 @@ import sys
 
 out_dir, tag = sys.argv[1], sys.argv[2]
 res = collections.defaultdict(dict)
-for p in ("fetch", "write", "sq"):
+for p in ("fetch", "write", "sq", "lds"):
     f = os.path.join(out_dir, f"pmc_{tag}_{p}", "run_counter_collection.csv")
     if not os.path.exists(f):
         continue
@@ -25,5 +25,8 @@ summary = {"tag": tag, "kernels": res}
 scan = res.get("k_waf_scan", {})
 if "FETCH_SIZE" in scan:
     summary["k_waf_scan_hbm_read_bytes_per_launch"] = 2.0 * scan["FETCH_SIZE"] * 1024
+if "SQ_LDS_BANK_CONFLICT" in scan and scan.get("SQ_LDS_IDX_ACTIVE"):
+    # extra LDS cycles from bank conflicts per LDS-active cycle (the scan's Bloom probes)
+    summary["k_waf_scan_lds_bank_conflict_rate"] = scan["SQ_LDS_BANK_CONFLICT"] / scan["SQ_LDS_IDX_ACTIVE"]
 json.dump(summary, open(os.path.join(out_dir, f"pmc_{tag}_summary.json"), "w"), indent=1)
 print(json.dumps({k: v for k, v in summary.items() if k != "kernels"}))
