@@ -1104,6 +1104,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             } else dl.kind = LK_NONE;
 
             if (L.kind == PFX || L.kind == NOREGEX || L.kind == EXACT) {
+                D.trie_depth = std::max<uint32_t>(D.trie_depth, (uint32_t)L.path.size());
                 uint32_t nd = walk(D.trie_root, L.path);
                 int32_t &slot = (L.kind == EXACT) ? nodes[nd].exact_loc : nodes[nd].prefix_loc;
                 if (slot >= 0) st.n_rejected_other++;   // duplicate location: nginx refuses; keep first
@@ -1128,11 +1129,11 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     for (auto &nd : nodes) if (nd.prefix_loc >= 0 || nd.exact_loc >= 0) nd.ar_loc = -1;
 
     uint32_t ecap = pow2_at_least(edge_list.size() * 2 + 1);
-    std::vector<DEdge> edges(ecap, DEdge{0, 0});
+    std::vector<DEdge> edges(ecap, DEdge{0, 0, -1, 0});
     for (auto &e : edge_list) {
         uint32_t i = edge_hash(e.first) & (ecap - 1);
         while (edges[i].key) i = (i + 1) & (ecap - 1);
-        edges[i] = DEdge{e.first, e.second};
+        edges[i] = DEdge{e.first, e.second, nodes[e.second].prefix_loc, 0};
     }
 
     // ---- signatures

@@ -373,6 +373,28 @@ __device__ __forceinline__ void load_span32(const uint8_t *A, uint64_t off, uint
     }
 }
 
+// load_span32 restricted to the aligned 16-byte blocks that hold [off, off + nbytes) (nbytes <=
+// 32): bytes past them read as 0.  Each skipped block is one random HBM transaction saved.
+__device__ __forceinline__ void load_span_n(const uint8_t *A, uint64_t off, uint64_t lim, uint32_t nbytes,
+                                            uint32_t (&w)[8]) {
+    const uint64_t a = off & ~15ull;
+    const uint32_t r = (uint32_t)(off & 15), nb = (r + nbytes + 15) >> 4;
+    uint32_t d[12];
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+        uint4 q = make_uint4(0, 0, 0, 0);
+        if ((uint32_t)b < nb && a + 16 * b < lim) q = *reinterpret_cast<const uint4 *>(A + a + 16 * b);
+        d[4 * b] = q.x; d[4 * b + 1] = q.y; d[4 * b + 2] = q.z; d[4 * b + 3] = q.w;
+    }
+    const uint32_t qd = r >> 2, sh = r & 3;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint32_t lo = qd == 0 ? d[k] : qd == 1 ? d[k + 1] : qd == 2 ? d[k + 2] : d[k + 3];
+        const uint32_t hi = qd == 0 ? d[k + 1] : qd == 1 ? d[k + 2] : qd == 2 ? d[k + 3] : d[k + 4];
+        w[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    }
+}
+
 __device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[8], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xFF; }
 
 // Host of <= 32 bytes held in registers: validate_host + exact-name probe (the common case).
@@ -513,7 +535,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
         int hl;
         if (r.host_len <= 32) {
             uint32_t hw[8];
-            load_span32(A, f_host, alen, hw);
+            load_span_n(A, f_host, alen, r.host_len, hw);
             hl = host_fast(hw, r.host_len, t, pi, s);
         } else {
             hl = validate_host(A + f_host, r.host_len);
@@ -542,13 +564,12 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
     // The first 32 URI bytes come from registers (a window shifted one dword per 4 bytes).
     const uint8_t *u = A + f_uri;
     uint32_t uw[8];
-    load_span32(A, f_uri, alen, uw);
+    // only the bytes the walk can read: it stops at the server's deepest location name
+    load_span_n(A, f_uri, alen, min(min(r.uri_len, S.trie_depth + 1u), 32u), uw);
     uint32_t node = S.trie_root;
-    int32_t best = -1;
+    int32_t best = t.nodes[node].prefix_loc;
     uint32_t i = 0;
     for (;; i++) {
-        const DNode nd = t.nodes[node];
-        if (nd.prefix_loc >= 0) best = nd.prefix_loc;
         if (i == r.uri_len) break;
         uint32_t b;
         if (i < 32) {
@@ -564,13 +585,15 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
         }
         const uint32_t key = node * 256u + b + 1u;
         uint32_t slot = edge_hash(key) & t.edges_mask, child = GM_NONE;
+        int32_t cpref = -1;
         for (;; slot = (slot + 1) & t.edges_mask) {
             const DEdge e = t.edges[slot];
             if (e.key == 0) break;
-            if (e.key == key) { child = e.child; break; }
+            if (e.key == key) { child = e.child; cpref = e.child_prefix; break; }
         }
         if (child == GM_NONE) break;
         node = child;
+        if (cpref >= 0) best = cpref;
     }
     int32_t loc = -1;
     if (i == r.uri_len) {
@@ -674,6 +697,20 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
     }
 }
 
+// blk2rec alone (k_waf_exact's record lookup), when k_route runs after the scan
+__global__ __launch_bounds__(256) void k_blk2rec(const gm_req *__restrict__ reqs, uint32_t n, uint64_t arena_len,
+                                                 uint32_t *__restrict__ blk2rec, uint32_t nblk) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        // blocks whose start lies in [base_i, base_{i+1}) belong to record i
+        const uint64_t b0 = (i == 0) ? 0 : reqs[i].base;
+        const uint64_t b1 = (i + 1 < n) ? reqs[i + 1].base : arena_len;
+        const uint64_t k0 = (b0 + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
+        uint64_t k1 = (b1 + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
+        if (i + 1 == n) k1 = nblk;
+        for (uint64_t k = k0; k < k1 && k < nblk; k++) blk2rec[k] = i;
+    }
+}
+
 #include "gm_waf.inc"
 
 }  // namespace
@@ -712,7 +749,8 @@ struct gm_ctx {
     // side stream: k_route runs beside the WAF scan (independent inputs) and joins before the
     // exact check, which needs its blk2rec map
     hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_blk = nullptr, ev_scan = nullptr;
+    int route_mode = 0;            // 0: route beside the scan, 1: after it (GM_ROUTE_MODE tuning knob)
     bool ev_pending = false;
     int ev_used = 0;
     float last_ms[4] = {0, 0, 0, 0};
@@ -762,6 +800,7 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
             c->cu_count = cus;
         if (const char *ev = getenv("GM_SCAN_DEPTH")) c->scan_depth = atoi(ev);
         if (const char *ev = getenv("GM_ROUTE_WPE")) c->route_wpe = atoi(ev);
+        if (const char *ev = getenv("GM_ROUTE_MODE")) c->route_mode = atoi(ev);
         if (hipMalloc((void **)&c->d_status, STATUS_WORDS * 4) != hipSuccess ||
             hipHostMalloc((void **)&c->h_status, STATUS_WORDS * 4, hipHostMallocDefault) != hipSuccess) {
             t_err = "status alloc failed"; delete c; return nullptr;
@@ -772,7 +811,9 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
         }
         if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+            hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_blk, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming) != hipSuccess) {
             t_err = "stream/event create failed"; delete c; return nullptr;
         }
     }
@@ -796,6 +837,8 @@ void gm_destroy(gm_ctx *c) {
         for (auto &e : c->ev_route) if (e) (void)hipEventDestroy(e);
         if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
         if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+        if (c->ev_blk) (void)hipEventDestroy(c->ev_blk);
+        if (c->ev_scan) (void)hipEventDestroy(c->ev_scan);
         if (c->side) (void)hipStreamDestroy(c->side);
     }
     delete c->gen;
@@ -872,25 +915,38 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
         HIPCHK(c, hipGetLastError());
         return mark(1) ? GM_E_HIP : GM_OK;
     }
-    // fork: k_route on the side stream, overlapping the WAF scan and context filter (the scan is
-    // HBM/VALU-bound with one 1024-thread workgroup per CU; route waves fit beside it).  The
-    // route launch is issued after the scan's, so the scan's workgroups claim the CUs first.
+    // fork: k_route on the side stream.  route_mode 0: beside the WAF scan (its waves fit
+    // beside the scan's one workgroup per CU; the route launch is issued after the scan's, so
+    // the scan claims the CUs first).  route_mode 1: after the scan, beside the context filter
+    // and the exact check (latency-bound kernels), with blk2rec from k_blk2rec beside the scan.
     HIPCHK(c, hipEventRecord(c->ev_fork, s));
     HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    const bool late = c->route_mode == 1;
+    if (late) {
+        k_blk2rec<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 4)), 256, 0,
+                    c->side>>>(reqs, n, alen, c->d_blk2rec, nblk);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(c->ev_blk, c->side));
+    }
     auto launch_route = [&]() -> int {
+        if (late) {
+            HIPCHK(c, hipEventRecord(c->ev_scan, s));
+            HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_scan, 0));
+        }
+        uint32_t *b2r = late ? nullptr : c->d_blk2rec;
         if (prof) HIPCHK(c, hipEventRecord(c->ev_route[0], c->side));
         if (c->route_wpe == 5)
             k_route<5><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
-                                                                  c->d_blk2rec, nblk);
+                                                                  b2r, nblk);
         else if (c->route_wpe == 6)
             k_route<6><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
-                                                                  c->d_blk2rec, nblk);
+                                                                  b2r, nblk);
         else if (c->route_wpe == 4)
             k_route<4><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
-                                                                  c->d_blk2rec, nblk);
+                                                                  b2r, nblk);
         else
             k_route<3><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
-                                                                  c->d_blk2rec, nblk);
+                                                                  b2r, nblk);
         HIPCHK(c, hipGetLastError());
         if (prof) HIPCHK(c, hipEventRecord(c->ev_route[1], c->side));
         HIPCHK(c, hipEventRecord(c->ev_join, c->side));
@@ -924,6 +980,7 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
         else if (c->scan_depth == 6) k_waf_scan<2, 6><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 101) k_waf_scan<2, 4, 1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 102) k_waf_scan<2, 4, 2><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else if (c->scan_depth == 103) k_waf_scan<2, 4, 3><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
     } else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
     HIPCHK(c, hipGetLastError());
@@ -933,12 +990,14 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
     k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, c->d_ccnt, W, t, c->d_surv, bcap, c->d_ccnt + W,
                                                 c->d_status);
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipStreamWaitEvent(s, c->ev_join, 0));   // join: verdicts and blk2rec are written
+    // blk2rec must be written before the exact check; the route's verdicts before the pairs
+    HIPCHK(c, hipStreamWaitEvent(s, late ? c->ev_blk : c->ev_join, 0));
     constexpr uint32_t EXACT_SUB = 8;
     k_waf_exact<<<scan_blocks * EXACT_SUB, 256, 0, s>>>(A, alen, reqs, n, c->d_blk2rec, t, c->d_surv, bcap,
                                                          c->d_ccnt + W, EXACT_SUB, c->d_pairs, (uint32_t)c->cap_pairs,
                                                          c->d_jobs, (uint32_t)c->cap_jobs, c->d_status);
     HIPCHK(c, hipGetLastError());
+    if (late) HIPCHK(c, hipStreamWaitEvent(s, c->ev_join, 0));   // join
     if (mark(3)) return GM_E_HIP;
     HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, STATUS_WORDS * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));

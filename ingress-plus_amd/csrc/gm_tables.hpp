@@ -44,7 +44,8 @@ struct DServer {
     uint32_t first_if, n_if; // server rewrite-phase `if (...) { return }` list (DServerIf)
     uint32_t first_rloc, n_rloc;  // regex locations (DRegexLoc), config order
     uint32_t waf_mode;
-    uint32_t pad[2];
+    uint32_t trie_depth;     // longest exact / prefix location name: URI bytes the trie walk reads
+    uint32_t pad;
 };
 struct DServerIf {
     uint32_t op;             // SIF_*
@@ -63,7 +64,9 @@ struct DNode {
     int32_t ar_loc;          // auto_redirect target: location named <this>/ (only if nothing ends here)
     uint32_t pad;
 };
-struct DEdge { uint32_t key; uint32_t child; };   // key = node*256 + byte + 1, 0 = empty
+// key = node*256 + byte + 1 (0 = empty); child_prefix = the child's prefix_loc, so the walk reads
+// one 16-byte edge per URI byte instead of an edge and then the child node
+struct DEdge { uint32_t key; uint32_t child; int32_t child_prefix; uint32_t pad; };
 
 // ---- locations -------------------------------------------------------------------------
 enum : uint8_t { LK_PROXY = 0, LK_RETURN = 1, LK_IRL_SPLIT = 2, LK_IRL_RULES = 3, LK_UNSUPPORTED = 4,
