@@ -651,7 +651,10 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
                                                        const uint8_t *__restrict__ A, uint64_t arena_len,
                                                        GTab t, gm_verdict *__restrict__ out,
                                                        unsigned long long *__restrict__ counters,
-                                                       uint32_t *__restrict__ blk2rec, uint32_t nblk) {
+                                                       uint32_t *__restrict__ blk2rec, uint32_t nblk, int prio) {
+    // beside the WAF scan: issue priority over the scan's waves, so the route's short
+    // latency-bound waves finish early instead of stretching past the scan (GM_ROUTE_PRIO)
+    if (prio) __builtin_amdgcn_s_setprio(2);
     __shared__ uint32_t hist[LDS_HIST_MAX];
     const bool use_hist = t.n_locs <= LDS_HIST_MAX;
     if (use_hist) for (uint32_t k = threadIdx.x; k < t.n_locs; k += blockDim.x) hist[k] = 0;
@@ -750,6 +753,7 @@ struct gm_ctx {
     // exact check, which needs its blk2rec map
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_blk = nullptr, ev_scan = nullptr;
+    int route_prio = 1;            // k_route beside the scan at raised issue priority (GM_ROUTE_PRIO)
     int route_mode = 0;            // 0: route beside the scan, 1: after it (GM_ROUTE_MODE tuning knob)
     bool ev_pending = false;
     int ev_used = 0;
@@ -757,7 +761,7 @@ struct gm_ctx {
     bool route_side = false;   // last batch ran k_route on the side stream
     int cu_count = 256;
     int scan_depth = SCAN_DEPTH;   // chunks in flight per scan wave (GM_SCAN_DEPTH tuning knob)
-    int route_wpe = 3;             // k_route register target, waves per SIMD (GM_ROUTE_WPE tuning knob)
+    int route_wpe = 5;             // k_route register target, waves per SIMD (GM_ROUTE_WPE tuning knob)
     std::mutex mu;
 };
 
@@ -801,6 +805,7 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
         if (const char *ev = getenv("GM_SCAN_DEPTH")) c->scan_depth = atoi(ev);
         if (const char *ev = getenv("GM_ROUTE_WPE")) c->route_wpe = atoi(ev);
         if (const char *ev = getenv("GM_ROUTE_MODE")) c->route_mode = atoi(ev);
+        if (const char *ev = getenv("GM_ROUTE_PRIO")) c->route_prio = atoi(ev);
         if (hipMalloc((void **)&c->d_status, STATUS_WORDS * 4) != hipSuccess ||
             hipHostMalloc((void **)&c->h_status, STATUS_WORDS * 4, hipHostMallocDefault) != hipSuccess) {
             t_err = "status alloc failed"; delete c; return nullptr;
@@ -911,7 +916,7 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
                                                                            (uint32_t)c->cu_count * 8));
     c->last_candidates = c->last_pairs = c->last_hits = c->last_ctx_pass = c->last_jobs = 0;
     if (!waf || n == 0) {
-        k_route<3><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, c->d_counters, nullptr, nblk);
+        k_route<3><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, c->d_counters, nullptr, nblk, 0);
         HIPCHK(c, hipGetLastError());
         return mark(1) ? GM_E_HIP : GM_OK;
     }
@@ -937,16 +942,16 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
         if (prof) HIPCHK(c, hipEventRecord(c->ev_route[0], c->side));
         if (c->route_wpe == 5)
             k_route<5><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
-                                                                  b2r, nblk);
+                                                                  b2r, nblk, late ? 0 : c->route_prio);
         else if (c->route_wpe == 6)
             k_route<6><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
-                                                                  b2r, nblk);
+                                                                  b2r, nblk, late ? 0 : c->route_prio);
         else if (c->route_wpe == 4)
             k_route<4><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
-                                                                  b2r, nblk);
+                                                                  b2r, nblk, late ? 0 : c->route_prio);
         else
             k_route<3><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
-                                                                  b2r, nblk);
+                                                                  b2r, nblk, late ? 0 : c->route_prio);
         HIPCHK(c, hipGetLastError());
         if (prof) HIPCHK(c, hipEventRecord(c->ev_route[1], c->side));
         HIPCHK(c, hipEventRecord(c->ev_join, c->side));
@@ -980,6 +985,8 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
         else if (c->scan_depth == 6) k_waf_scan<2, 6><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 101) k_waf_scan<2, 4, 1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 102) k_waf_scan<2, 4, 2><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else if (c->scan_depth == 104) k_waf_scan<2, 4, 4><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else if (c->scan_depth == 105) k_waf_scan<1, 4, 1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 103) k_waf_scan<2, 4, 3><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
     } else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
