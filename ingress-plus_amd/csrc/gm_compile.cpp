@@ -365,13 +365,14 @@ struct Compiler {
     }
 
     // regex -> dfa id, or -1 (counted)
-    int regex(const std::string &pat, bool ci, Dfa *keep = nullptr) {
+    int regex(const std::string &pat, bool ci, Dfa *keep = nullptr, std::vector<std::string> *factors = nullptr) {
         RegexInfo ri = compile_regex(pat, ci);
         if (ri.status != RX_OK) {
             if (ri.status == RX_PCRE_ONLY) st.n_rejected_pcre++; else st.n_rejected_other++;
             return -1;
         }
         if (keep) *keep = ri.dfa;
+        if (factors) { factors->clear(); if (ri.min_factor >= 4) *factors = ri.factors; }
         return add_dfa(ri.dfa);
     }
 
@@ -1017,6 +1018,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     std::vector<DServer> dservers(M.servers.size());
     std::vector<DServerIf> sifs;
     std::vector<DRegexLoc> rlocs;
+    std::vector<std::vector<std::string>> rloc_factors;   // parallel to rlocs: >= 4-byte factors
     auto new_node = [&]() { nodes.push_back(DNode{-1, -1, -1, 0}); return (uint32_t)nodes.size() - 1; };
     auto walk = [&](uint32_t root, const std::string &p) {
         uint32_t cur = root;
@@ -1110,12 +1112,18 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 if (slot >= 0) st.n_rejected_other++;   // duplicate location: nginx refuses; keep first
                 else slot = lid;
             } else if (L.kind == RX || L.kind == RXI) {
-                int d = C.regex(L.path, L.kind == RXI);
-                if (d >= 0) rlocs.push_back(DRegexLoc{(uint32_t)d, (uint32_t)lid});
-                else dl.kind = LK_UNSUPPORTED;
+                // a rejected regex stays in config order with dfa GM_NONE: a URI that reaches it
+                // (no earlier regex matched) gets GM_ACT_UNSUPPORTED -- nginx's answer would
+                // depend on PCRE, so the request is the data plane's to defer
+                std::vector<std::string> fac;
+                int d = C.regex(L.path, L.kind == RXI, nullptr, &fac);
+                if (d < 0) dl.kind = LK_UNSUPPORTED;
+                rlocs.push_back(DRegexLoc{d >= 0 ? (uint32_t)d : GM_NONE, (uint32_t)lid});
+                rloc_factors.push_back(std::move(fac));
             }
         }
         D.n_rloc = (uint32_t)rlocs.size() - D.first_rloc;
+        D.rk_on = D.n_rloc > RLOC_SEQ_MAX;
         // auto_redirect: location "<p>/" with proxy_pass -> node for "<p>" if nothing ends there
         for (int lid : S.locs) {
             Loc &L = M.locs[lid];
@@ -1134,6 +1142,49 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         uint32_t i = edge_hash(e.first) & (ecap - 1);
         while (edges[i].key) i = (i + 1) & (ecap - 1);
         edges[i] = DEdge{e.first, e.second, nodes[e.second].prefix_loc, 0};
+    }
+
+    // ---- regex-location factor prefilter (servers with rk_on).  Each regex is keyed on one
+    // folded 4-byte window per factor (every match contains one of its factors); the window is
+    // the one shared by the fewest regexes so far, preferring windows that span a '/' (a path
+    // segment boundary: rarer in URIs than a window inside one word).
+    std::map<std::pair<uint32_t, uint32_t>, std::vector<uint32_t>> rk_lists;   // (server, key) -> k
+    std::vector<uint32_t> rk_ids;
+    for (auto &S : M.servers) {
+        DServer &D = dservers[S.id];
+        if (!D.rk_on) continue;
+        std::vector<uint32_t> alw;
+        std::map<uint32_t, uint32_t> use;
+        for (uint32_t k = 0; k < D.n_rloc; k++) {
+            const DRegexLoc &rl = rlocs[D.first_rloc + k];
+            const auto &fac = rloc_factors[D.first_rloc + k];
+            if (rl.dfa == GM_NONE || fac.empty()) { alw.push_back(k); continue; }
+            std::set<uint32_t> keys;
+            for (const std::string &f : fac) {
+                uint32_t best = 0; int best_cost = INT32_MAX;
+                for (size_t o = 0; o + 4 <= f.size(); o++) {
+                    uint32_t w = 0;
+                    for (int b = 0; b < 4; b++) w |= (uint32_t)(uint8_t)f[o + b] << (8 * b);
+                    w = fold4(w);
+                    bool span = f[o + 1] == '/' || f[o + 2] == '/' || f[o + 3] == '/';
+                    int cost = 2 * (int)use[w] + (span ? 0 : 1);
+                    if (cost < best_cost) { best_cost = cost; best = w; }
+                }
+                keys.insert(best);
+            }
+            for (uint32_t w : keys) { use[w]++; rk_lists[{(uint32_t)S.id, w}].push_back(k); }
+        }
+        D.first_ralw = (uint32_t)rk_ids.size(); D.n_ralw = (uint32_t)alw.size();
+        rk_ids.insert(rk_ids.end(), alw.begin(), alw.end());
+    }
+    const uint32_t rkcap = pow2_at_least(rk_lists.size() * 2 + 1);
+    std::vector<DRlocKey> rk(rkcap, DRlocKey{0, 0, 0, 0});
+    for (auto &kv : rk_lists) {
+        const uint32_t sv = kv.first.first, w = kv.first.second;
+        uint32_t i = rk_hash(w, sv) & (rkcap - 1);
+        while (rk[i].key) i = (i + 1) & (rkcap - 1);
+        rk[i] = DRlocKey{w, (uint32_t)rk_ids.size(), (uint32_t)kv.second.size(), sv};
+        rk_ids.insert(rk_ids.end(), kv.second.begin(), kv.second.end());   // ascending: pushed in k order
     }
 
     // ---- signatures
@@ -1280,6 +1331,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_waf_a = I.put(waf_a); h.off_waf_b = I.put(waf_b);
     h.off_lit_buckets = I.put(ltab); h.off_lits = I.put(dlits); h.off_sig_regex = I.put(sregex);
     h.off_always = I.put(always);
+    h.n_rk_cap = rkcap; h.n_rk_ids = (uint32_t)rk_ids.size();
+    h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids);
     C.bytes.resize(C.bytes.size() + 64, 0);   // slack: vector compares may over-read
     h.off_bytes = I.put(C.bytes);
     I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
@@ -1323,6 +1376,9 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.lits = (const DLit *)(b + h.off_lits);
     t.sig_regex = (const DSigRegex *)(b + h.off_sig_regex);
     t.always = (const uint32_t *)(b + h.off_always);
+    t.rk = (const DRlocKey *)(b + h.off_rk);
+    t.rk_ids = (const uint32_t *)(b + h.off_rk_ids);
+    t.rk_mask = h.n_rk_cap - 1;
     t.n_ports = h.n_ports;
     t.names_mask = h.n_names_cap - 1; t.wild_head_mask = h.n_wild_head_cap - 1; t.wild_tail_mask = h.n_wild_tail_cap - 1;
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;

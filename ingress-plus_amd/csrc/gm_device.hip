@@ -288,6 +288,66 @@ __device__ bool dfa_run_bytes(const GTab &t, uint32_t dfa_id, const uint8_t *p, 
     return r;
 }
 
+// Regex locations of a large server: the first regex in config
+// order that matches `u`, behind the factor prefilter (gm_tables.hpp RLOC_SEQ_MAX).  One pass
+// over the URI's folded 4-byte windows collects the RK_K smallest candidate indices >= lo
+// (sorted in registers); they run in order, merged with the server's always list; if all RK_K
+// fail the next pass collects the candidates after them.  Rejected (PCRE-only) regexes are in the
+// always list with dfa GM_NONE and "match" when reached.  Out of line: the route fast path
+// keeps its registers.
+constexpr int RK_K = 8;
+__device__ __noinline__ int32_t rloc_prefiltered(const GTab &t, const DServer &S, uint32_t sid, const uint8_t *u,
+                                                 uint32_t ulen) {
+    auto run = [&](uint32_t k) -> bool {
+        const DRegexLoc rl = t.rlocs[S.first_rloc + k];
+        return rl.dfa == GM_NONE || dfa_run_bytes(t, rl.dfa, u, ulen);
+    };
+    uint32_t lo = 0, ai = 0;
+    for (;;) {
+        uint32_t c[RK_K];
+#pragma unroll
+        for (int j = 0; j < RK_K; j++) c[j] = GM_NONE;
+        uint32_t w = 0;
+        for (uint32_t i = 0; i < ulen; i++) {
+            w = (w >> 8) | ((uint32_t)u[i] << 24);
+            if (i < 3) continue;
+            const uint32_t key = fold4(w);
+            for (uint32_t b = rk_hash(key, sid) & t.rk_mask;; b = (b + 1) & t.rk_mask) {
+                const DRlocKey e = t.rk[b];
+                if (e.key == 0) break;
+                if (e.key != key || e.server != sid) continue;
+                for (uint32_t q = 0; q < e.count; q++) {
+                    const uint32_t k = t.rk_ids[e.first + q];
+                    if (k < lo) continue;
+                    if (k >= c[RK_K - 1]) break;   // ascending lists
+                    bool dup = false;
+#pragma unroll
+                    for (int j = 0; j < RK_K; j++) dup |= c[j] == k;
+                    if (dup) continue;
+                    c[RK_K - 1] = k;
+#pragma unroll
+                    for (int j = RK_K - 1; j > 0; j--)
+                        if (c[j] < c[j - 1]) { const uint32_t x = c[j]; c[j] = c[j - 1]; c[j - 1] = x; }
+                }
+                break;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < RK_K; j++) {
+            const uint32_t k = c[j];
+            while (ai < S.n_ralw) {
+                const uint32_t a = t.rk_ids[S.first_ralw + ai];
+                if (a >= k) break;
+                ai++;
+                if (run(a)) return (int32_t)t.rlocs[S.first_rloc + a].loc;
+            }
+            if (k == GM_NONE) return -1;
+            if (run(k)) return (int32_t)t.rlocs[S.first_rloc + k].loc;
+        }
+        lo = c[RK_K - 1] + 1;
+    }
+}
+
 __device__ uint32_t murmur2_val(const Val &v, uint8_t *buf, bool &ok) {
     // gather to a contiguous lane-private buffer (values here are <= 64 bytes: $request_id)
     uint32_t n = v.total;
@@ -604,10 +664,12 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
     if (loc < 0) {
         if (best >= 0 && t.locs[best].noregex) loc = best;
         else {
-            for (uint32_t k = 0; k < S.n_rloc && loc < 0; k++) {
-                const DRegexLoc rl = t.rlocs[S.first_rloc + k];
-                if (dfa_run_bytes(t, rl.dfa, u, r.uri_len)) loc = (int32_t)rl.loc;
-            }
+            if (S.rk_on) loc = rloc_prefiltered(t, S, sid, u, r.uri_len);
+            else
+                for (uint32_t k = 0; k < S.n_rloc && loc < 0; k++) {
+                    const DRegexLoc rl = t.rlocs[S.first_rloc + k];
+                    if (rl.dfa == GM_NONE || dfa_run_bytes(t, rl.dfa, u, r.uri_len)) loc = (int32_t)rl.loc;
+                }
             if (loc < 0) loc = best;
         }
     }
@@ -761,6 +823,11 @@ struct gm_ctx {
     bool route_side = false;   // last batch ran k_route on the side stream
     int cu_count = 256;
     int scan_depth = SCAN_DEPTH;   // chunks in flight per scan wave (GM_SCAN_DEPTH tuning knob)
+    // scan records staged in LDS and written in whole slices (1) or stored directly (0): staging
+    // makes the scan 0.7 ms shorter per 10M C4 requests, but k_route beside it then gets fewer
+    // issue slots and finishes later than the scan -- direct stores stay the default until
+    // the route's critical path is shorter (GM_SCAN_STAGE tuning knob)
+    int scan_stage = 0;
     int route_wpe = 5;             // k_route register target, waves per SIMD (GM_ROUTE_WPE tuning knob)
     std::mutex mu;
 };
@@ -803,6 +870,7 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
             c->cu_count = cus;
         if (const char *ev = getenv("GM_SCAN_DEPTH")) c->scan_depth = atoi(ev);
+        if (const char *ev = getenv("GM_SCAN_STAGE")) c->scan_stage = atoi(ev);
         if (const char *ev = getenv("GM_ROUTE_WPE")) c->route_wpe = atoi(ev);
         if (const char *ev = getenv("GM_ROUTE_MODE")) c->route_mode = atoi(ev);
         if (const char *ev = getenv("GM_ROUTE_PRIO")) c->route_prio = atoi(ev);
@@ -982,13 +1050,19 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
     else if (t.bloom_pk == 2) {
         if (c->scan_depth == 1) k_waf_scan<2, 1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 2) k_waf_scan<2, 2><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else if (c->scan_depth == 106) k_waf_scan<2, 4, 6><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else if (c->scan_depth == 8) k_waf_scan<2, 8><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else if (c->scan_depth == 108) k_waf_scan<2, 8, 2><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else if (c->scan_depth == 110) k_waf_scan<2, 4, 5><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else if (c->scan_depth == 111) k_waf_scan<2, 8, 5><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 6) k_waf_scan<2, 6><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 101) k_waf_scan<2, 4, 1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 102) k_waf_scan<2, 4, 2><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 104) k_waf_scan<2, 4, 4><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 105) k_waf_scan<1, 4, 1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
         else if (c->scan_depth == 103) k_waf_scan<2, 4, 3><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else if (c->scan_stage) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+        else k_waf_scan<2, SCAN_DEPTH, 6><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
     } else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
     HIPCHK(c, hipGetLastError());
     if ((e = launch_route())) return e;

@@ -45,8 +45,17 @@ struct DServer {
     uint32_t first_rloc, n_rloc;  // regex locations (DRegexLoc), config order
     uint32_t waf_mode;
     uint32_t trie_depth;     // longest exact / prefix location name: URI bytes the trie walk reads
+    uint32_t rk_on;          // regex locations behind the factor prefilter (n_rloc > RLOC_SEQ_MAX)
+    uint32_t first_ralw, n_ralw;  // rk_ids slice: regex locations evaluated for every URI (no
+                                  // >= 4-byte factor, or PCRE-only), ascending
     uint32_t pad;
 };
+// A server with more regex locations than this evaluates them behind a factor prefilter: every
+// match of regex k contains one of its factors, so k is a candidate only if one of its key
+// windows (a folded 4-byte window of a factor) occurs in the URI.  Candidates run in config
+// order, merged with the always list; the first match wins (ngx_http_core_find_location).
+constexpr uint32_t RLOC_SEQ_MAX = 8;
+struct DRlocKey { uint32_t key; uint32_t first, count; uint32_t server; };   // key 0 = empty slot
 struct DServerIf {
     uint32_t op;             // SIF_*
     uint32_t src;            // DSrc index (variable), unused for SIF_RETURN
@@ -180,6 +189,8 @@ struct TabHeader {
     uint32_t bloom_mul;      // Bloom hash multiplier (chosen per generation, see gm_compile.cpp)
     uint32_t bloom_pk;       // packed shifts per probe (K = 2 * bloom_pk)
     uint32_t ctx_mul;        // stage-2 context filter multiplier (waf_b, see ctx_key)
+    uint32_t n_rk_cap, n_rk_ids;   // regex-location prefilter: key table (pow2) and id lists
+    uint64_t off_rk, off_rk_ids;
 };
 
 struct GTab {                // device pointers, built on host from the image base
@@ -191,6 +202,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const DDfa *dfas; const uint16_t *dfa_trans; const uint8_t *dfa_acc; const uint8_t *dfa_cls;
     const uint8_t *bytes; const uint32_t *waf_a; const uint32_t *waf_b;
     const DLitBucket *lit_buckets; const DLit *lits; const DSigRegex *sig_regex; const uint32_t *always;
+    const DRlocKey *rk; const uint32_t *rk_ids; uint32_t rk_mask;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
     uint32_t gen;
@@ -247,6 +259,7 @@ __host__ __device__ inline uint32_t ctx_key(uint32_t w, uint32_t l2, uint32_t r2
     return w ^ c;
 }
 __host__ __device__ inline uint32_t lit_bucket_hash(uint32_t w) { uint32_t h = w * 0xC2B2AE3Du; return h ^ (h >> 16); }
+__host__ __device__ inline uint32_t rk_hash(uint32_t w, uint32_t server) { return lit_bucket_hash(w ^ (server * 0x9E3779B9u)); }
 // Prefilter fold: OR 0x20 into every byte.  Maps A-Z onto a-z (so case-insensitive keys match)
 // and merges a few other byte pairs (0x40/0x60, 0x00-0x1F/0x20-0x3F, ...); the merge only adds
 // prefilter candidates -- k_waf_verify compares the literal bytes exactly (lc() for nocase).

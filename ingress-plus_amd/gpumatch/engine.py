@@ -15,7 +15,7 @@ import numpy as np
 from .records import REQ_DTYPE, VERDICT_DTYPE
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(HERE), "libgpumatch.so")
+LIB_PATH = os.environ.get("GM_LIB") or os.path.join(os.path.dirname(HERE), "libgpumatch.so")
 
 GM_OK = 0
 GM_E_OVERFLOW = -4

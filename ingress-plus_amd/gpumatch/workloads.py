@@ -167,3 +167,155 @@ def algorithmic_bytes(reqs: np.ndarray, config: str) -> int:
         return hdr + int(reqs["host_len"].sum() + reqs["uri_len"].sum() + reqs["args_len"].sum() +
                          reqs["hdr_len"].sum() + reqs["method_len"].sum()) + 16 * n
     return hdr + int(reqs["uri_len"].sum())
+
+
+# --------------------------------------------------------------------------- C3 regex locations
+
+C3_HOST = "regex.example.com"
+_C3_WORDS = ("api", "v1", "v2", "v3", "users", "items", "shop", "cart", "img", "static", "blog", "post",
+             "search", "admin", "login", "docs", "files", "media", "video", "feed", "news", "order",
+             "account", "profile", "catalog", "product", "assets", "report", "export", "tags",
+             "comments", "upload", "download", "health", "status", "metrics", "session", "user",
+             "group", "team", "project", "build", "release", "config", "settings", "page", "wiki")
+_C3_EXT = ("json", "xml", "php", "html", "png", "jpg", "css", "js", "txt", "csv")
+# PCRE-only constructs (rejected at compile time and counted)
+_C3_PCRE_ONLY = ("(?=/)", "(?!x)", "(?<=/)", "(\\w+)/\\1", "[a-z]++", "(?>ab|a)", "\\Kz")
+
+
+def c3_regexes(n: int = 1000, seed: int = records.SEED_BASE + 2):
+    """C3: ``n`` regex locations from the RE2-compatible grammar of SURVEY.md §8(d): literal
+    segments, ``[a-z0-9]+``, ``\\d{1,4}``, alternations of <= 4, optional groups, 70 % ``^``
+    anchored; 20 % ``~*`` (caseless); 5 % carry a PCRE-only construct.  Returns
+    ``[(pattern, caseless, pcre_only, segments, anchored, dollar)]``; ``segments`` is the sampler's
+    view of the pattern (``c3_uri``)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    W = _C3_WORDS
+    out, seen = [], set()
+    while len(out) < n:
+        segs = []
+        for _ in range(int(rng.integers(2, 6))):
+            r = rng.random()
+            if r < 0.45:
+                segs.append(("lit", "/" + W[rng.integers(len(W))]))
+            elif r < 0.6:
+                segs.append(("cls", "/"))
+            elif r < 0.72:
+                segs.append(("dig", "/" if rng.random() < 0.6 else "-"))
+            elif r < 0.87:
+                k = int(rng.integers(2, 5))
+                segs.append(("alt", tuple(sorted(set("/" + W[i] for i in rng.choice(len(W), k, replace=False))))))
+            else:
+                segs.append(("opt", "/" + W[rng.integers(len(W))]))
+        if rng.random() < 0.3:
+            segs.append(("ext", tuple(sorted(set(_C3_EXT[i] for i in rng.choice(len(_C3_EXT), int(rng.integers(1, 4)),
+                                                                               replace=False))))))
+        anchored = rng.random() < 0.7
+        dollar = rng.random() < 0.5
+        caseless = rng.random() < 0.2
+        pcre_only = rng.random() < 0.05
+        body = []
+        for kind, v in segs:
+            if kind == "lit":
+                body.append(v)
+            elif kind == "cls":
+                body.append(v + "[a-z0-9]+")
+            elif kind == "dig":
+                body.append(v + "\\d{1,4}")
+            elif kind == "alt":
+                body.append("(" + "|".join(v) + ")")
+            elif kind == "opt":
+                body.append("(" + v + ")?")
+            else:
+                body.append("\\.(" + "|".join(v) + ")")
+        if pcre_only:
+            body.insert(int(rng.integers(0, len(body) + 1)), _C3_PCRE_ONLY[rng.integers(len(_C3_PCRE_ONLY))])
+        pat = ("^" if anchored else "") + "".join(body) + ("$" if dollar else "")
+        if pat in seen:
+            continue
+        seen.add(pat)
+        out.append((pat, caseless, pcre_only, tuple(segs), anchored, dollar))
+    return out
+
+
+def c3_conf(regexes) -> str:
+    """nginx.conf text of the C3 server: ``location ~ / ~*`` blocks in config order (regex
+    locations come from custom templates / snippets), plus prefix locations."""
+    ups = "".join(f"  upstream c3-u{k} {{ server 10.3.0.{k + 1}:80; }}\n" for k in range(8))
+    locs = []
+    for i, (pat, ci, *_r) in enumerate(regexes):
+        locs.append(f'    location {"~*" if ci else "~"} "{pat}" {{ proxy_pass http://c3-u{i % 8}; }}\n')
+    return ("http {\n" + ups + "  server {\n    listen 80 default_server;\n"
+            f"    server_name {C3_HOST};\n"
+            "    location / { proxy_pass http://c3-u0; }\n"
+            "    location ^~ /static/fixed/ { proxy_pass http://c3-u1; }\n"
+            "    location = /exact { return 204; }\n" + "".join(locs) + "  }\n}\n")
+
+
+def c3_blob(regexes=None) -> bytes:
+    return blob.make_blob(c3_conf(regexes if regexes is not None else c3_regexes()), {})
+
+
+_C3_ALNUM = "abcdefghijklmnopqrstuvwxyz0123456789"
+
+
+def _c3_word(rng):
+    return "".join(rng.choices(_C3_ALNUM, k=rng.randint(1, 8)))
+
+
+def c3_uri(rng, regexes, crafted: bool) -> str:
+    """One synthetic URI of 32-256 bytes (``rng`` a ``random.Random``): a string generated from a
+    random regex of the set (``crafted``) or a random path of vocabulary words and alphanumeric
+    segments."""
+    W = _C3_WORDS
+    target = rng.randint(32, 256)
+    if not crafted:
+        s = ""
+        while len(s) < target:
+            r = rng.random()
+            s += "/" + (rng.choice(W) if r < 0.5 else str(rng.randrange(99999)) if r < 0.65 else _c3_word(rng))
+        if rng.random() < 0.2:
+            s += "." + rng.choice(_C3_EXT)
+        return s[:256]
+    pat, ci, pcre_only, segs, anchored, dollar = rng.choice(regexes)
+    body = ""
+    for kind, v in segs:
+        if kind == "lit":
+            body += v
+        elif kind == "cls":
+            body += v + _c3_word(rng)
+        elif kind == "dig":
+            body += v + str(rng.randrange(10 ** rng.randint(1, 4)))
+        elif kind == "alt":
+            body += rng.choice(v)
+        elif kind == "opt":
+            body += v if rng.random() < 0.5 else ""
+        else:
+            body += "." + rng.choice(v)
+    if ci and rng.random() < 0.5:
+        body = "".join(ch.upper() if rng.random() < 0.3 else ch for ch in body)
+    pre = suf = ""
+    room = max(0, target - len(body))
+    if not anchored:
+        k = rng.randint(0, room)
+        while len(pre) < k:
+            pre += "/" + rng.choice(W)
+        room = max(0, target - len(body) - len(pre))
+    if not dollar:
+        while len(suf) < room:
+            suf += "/" + _c3_word(rng)
+    return (pre + body + suf)[:256] or "/"
+
+
+def gen_c3(n: int, regexes=None, seed: int = records.SEED_BASE + 2, pool: int = 100_000):
+    """C3 requests: host regex.example.com, URIs 32-256 B, 40 % crafted to hit a regex location.
+    A pool of ``min(n, pool)`` distinct URIs is generated and indexed (vectorised for 10M)."""
+    regexes = regexes if regexes is not None else c3_regexes()
+    import random
+    rnd = random.Random(seed)
+    m = min(n, pool)
+    uris = [c3_uri(rnd, regexes, rnd.random() < 0.4) for _ in range(m)]
+    idx = np.arange(n) if n <= m else np.random.Generator(np.random.PCG64(seed)).integers(0, m, n)
+    fields = {"uri": [records.choice_seg(uris, idx)],
+              "host": [records.const_seg(C3_HOST, n)],
+              "method": [records.const_seg("GET", n)]}
+    return records.build(n, fields, np.full(n, 80), np.zeros(n, dtype=np.int64))
