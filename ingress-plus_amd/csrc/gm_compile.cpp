@@ -322,6 +322,62 @@ struct Image {
     }
 };
 
+// A superset of a PCRE-only regex in the RE2 subset, or "" when there is none here: lookaround
+// groups dropped, atomic groups made plain, possessive quantifiers made greedy, \K dropped,
+// backreferences widened to (?:.|\n)*.  Every subject the original matches, the relaxed
+// pattern matches too, so a regex location whose relaxed DFA does not match a URI is skipped
+// exactly; one that matches is deferred (GM_ACT_UNSUPPORTED).  Restated in oracle/gm_oracle.c
+// (orc_relax).
+static std::string relax_pcre_only(const std::string &p) {
+    std::string o;
+    const size_t n = p.size();
+    bool cls = false;
+    for (size_t i = 0; i < n; i++) {
+        const char ch = p[i];
+        if (ch == '\\' && i + 1 < n) {
+            const char e = p[i + 1];
+            if (!cls && e >= '1' && e <= '9') { o += "(?:.|\\n)*"; i++; continue; }
+            if (!cls && e == 'K') { i++; continue; }
+            if (!cls && (e == 'g' || e == 'k')) return "";
+            o += ch; o += e; i++;
+            continue;
+        }
+        if (cls) { o += ch; if (ch == ']') cls = false; continue; }
+        if (ch == '[') {
+            cls = true; o += ch;
+            if (i + 1 < n && p[i + 1] == '^') o += p[++i];
+            if (i + 1 < n && p[i + 1] == ']') o += p[++i];
+            continue;
+        }
+        if (ch == '(' && i + 2 < n && p[i + 1] == '?') {
+            const char a = p[i + 2];
+            const bool look = a == '=' || a == '!' || (a == '<' && i + 3 < n && (p[i + 3] == '=' || p[i + 3] == '!'));
+            if (look) {   // skip to the matching ')'
+                int depth = 0;
+                bool c2 = false;
+                size_t j = i;
+                for (; j < n; j++) {
+                    if (p[j] == '\\') { j++; continue; }
+                    if (c2) { if (p[j] == ']') c2 = false; continue; }
+                    if (p[j] == '[') { c2 = true; if (j + 1 < n && p[j + 1] == '^') j++; if (j + 1 < n && p[j + 1] == ']') j++; continue; }
+                    if (p[j] == '(') depth++;
+                    else if (p[j] == ')' && --depth == 0) break;
+                }
+                if (j >= n) return "";
+                i = j;
+                if (i + 1 < n && (p[i + 1] == '*' || p[i + 1] == '+' || p[i + 1] == '?' || p[i + 1] == '{')) return "";
+                continue;
+            }
+            if (a == '>') { o += "(?:"; i += 2; continue; }
+            if (a == 'R' || a == '(' || a == 'C' || a == 'P' || a == '&' || a == '|' || (a >= '0' && a <= '9')) return "";
+        }
+        if ((ch == '*' || ch == '+' || ch == '?' || ch == '}') && i + 1 < n && p[i + 1] == '+' &&
+            !(ch == '?' && i > 0 && p[i - 1] == '(')) { o += ch; i++; continue; }
+        o += ch;
+    }
+    return o;
+}
+
 uint32_t pow2_at_least(size_t n) { uint32_t c = 16; while (c < n) c <<= 1; return c; }
 
 struct Compiler {
@@ -365,9 +421,20 @@ struct Compiler {
     }
 
     // regex -> dfa id, or -1 (counted)
-    int regex(const std::string &pat, bool ci, Dfa *keep = nullptr, std::vector<std::string> *factors = nullptr) {
+    // superset: for a PCRE-only pattern, compile relax_pcre_only(pat) instead (still counted as
+    // rejected) and report it through *superset
+    int regex(const std::string &pat, bool ci, Dfa *keep = nullptr, std::vector<std::string> *factors = nullptr,
+              bool *superset = nullptr) {
         RegexInfo ri = compile_regex(pat, ci);
-        if (ri.status != RX_OK) {
+        if (superset) *superset = false;
+        if (ri.status == RX_PCRE_ONLY && superset) {
+            st.n_rejected_pcre++;
+            const std::string rp = relax_pcre_only(pat);
+            if (rp.empty()) return -1;
+            ri = compile_regex(rp, ci);
+            if (ri.status != RX_OK) return -1;
+            *superset = true;
+        } else if (ri.status != RX_OK) {
             if (ri.status == RX_PCRE_ONLY) st.n_rejected_pcre++; else st.n_rejected_other++;
             return -1;
         }
@@ -1112,12 +1179,14 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 if (slot >= 0) st.n_rejected_other++;   // duplicate location: nginx refuses; keep first
                 else slot = lid;
             } else if (L.kind == RX || L.kind == RXI) {
-                // a rejected regex stays in config order with dfa GM_NONE: a URI that reaches it
-                // (no earlier regex matched) gets GM_ACT_UNSUPPORTED -- nginx's answer would
-                // depend on PCRE, so the request is the data plane's to defer
+                // a rejected (PCRE-only) regex stays in config order with the DFA of a superset
+                // pattern (relax_pcre_only), or dfa GM_NONE when there is none: a URI that
+                // reaches it and matches the superset gets GM_ACT_UNSUPPORTED -- nginx's answer
+                // depends on PCRE there, so the request is the data plane's to defer
                 std::vector<std::string> fac;
-                int d = C.regex(L.path, L.kind == RXI, nullptr, &fac);
-                if (d < 0) dl.kind = LK_UNSUPPORTED;
+                bool sup = false;
+                int d = C.regex(L.path, L.kind == RXI, nullptr, &fac, &sup);
+                if (d < 0 || sup) dl.kind = LK_UNSUPPORTED;   // sup: the DFA is a superset
                 rlocs.push_back(DRegexLoc{d >= 0 ? (uint32_t)d : GM_NONE, (uint32_t)lid});
                 rloc_factors.push_back(std::move(fac));
             }

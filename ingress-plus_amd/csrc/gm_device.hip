@@ -348,6 +348,18 @@ __device__ __noinline__ int32_t rloc_prefiltered(const GTab &t, const DServer &S
     }
 }
 
+// The regex-location step of ngx_http_core_find_location: the first regex location in config
+// order whose DFA matches the URI (-1: none).  Out of line, like the other rarely taken steps.
+__device__ __noinline__ int32_t rloc_first_match(const GTab &t, const DServer &S, uint32_t sid, const uint8_t *u,
+                                                 uint32_t ulen) {
+    if (S.rk_on) return rloc_prefiltered(t, S, sid, u, ulen);
+    for (uint32_t k = 0; k < S.n_rloc; k++) {
+        const DRegexLoc rl = t.rlocs[S.first_rloc + k];
+        if (rl.dfa == GM_NONE || dfa_run_bytes(t, rl.dfa, u, ulen)) return (int32_t)rl.loc;
+    }
+    return -1;
+}
+
 __device__ uint32_t murmur2_val(const Val &v, uint8_t *buf, bool &ok) {
     // gather to a contiguous lane-private buffer (values here are <= 64 bytes: $request_id)
     uint32_t n = v.total;
@@ -664,12 +676,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
     if (loc < 0) {
         if (best >= 0 && t.locs[best].noregex) loc = best;
         else {
-            if (S.rk_on) loc = rloc_prefiltered(t, S, sid, u, r.uri_len);
-            else
-                for (uint32_t k = 0; k < S.n_rloc && loc < 0; k++) {
-                    const DRegexLoc rl = t.rlocs[S.first_rloc + k];
-                    if (rl.dfa == GM_NONE || dfa_run_bytes(t, rl.dfa, u, r.uri_len)) loc = (int32_t)rl.loc;
-                }
+            loc = rloc_first_match(t, S, sid, u, r.uri_len);
             if (loc < 0) loc = best;
         }
     }
@@ -1323,4 +1330,20 @@ extern "C" int64_t gm_debug_waf_prefilter2(gm_ctx *c, const uint8_t *A, size_t l
         if (hit) { if ((size_t)k < cap && out) out[k] = p; k++; }
     }
     return k;
+}
+
+// Server `sid` of the current generation as u32 words (DServer), followed by its regex
+// locations (dfa, loc) pairs; returns the number of words written.
+extern "C" int gm_debug_server(gm_ctx *c, uint32_t sid, uint32_t *out, size_t cap) {
+    if (!c || !c->gen || !out) return -1;
+    const TabHeader &h = c->gen->hdr;
+    if (sid >= h.n_servers) return -1;
+    const uint8_t *b = c->gen->host_image.data();
+    const DServer S = reinterpret_cast<const DServer *>(b + h.off_servers)[sid];
+    const DRegexLoc *rl = reinterpret_cast<const DRegexLoc *>(b + h.off_rlocs);
+    size_t k = 0;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(&S);
+    for (size_t i = 0; i < sizeof(DServer) / 4 && k < cap; i++) out[k++] = w[i];
+    for (uint32_t i = 0; i < S.n_rloc && k + 2 <= cap; i++) { out[k++] = rl[S.first_rloc + i].dfa; out[k++] = rl[S.first_rloc + i].loc; }
+    return (int)k;
 }

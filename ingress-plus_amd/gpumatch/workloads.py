@@ -192,8 +192,11 @@ def c3_regexes(n: int = 1000, seed: int = records.SEED_BASE + 2):
     W = _C3_WORDS
     out, seen = [], set()
     while len(out) < n:
+        anchored = rng.random() < 0.7
         segs = []
-        for _ in range(int(rng.integers(2, 6))):
+        # unanchored patterns get >= 3 segments, every pattern >= 1 literal segment: a pattern
+        # like "(/a|/b)" alone would match most URIs and end every search at once
+        for _ in range(int(rng.integers(2 if anchored else 3, 6))):
             r = rng.random()
             if r < 0.45:
                 segs.append(("lit", "/" + W[rng.integers(len(W))]))
@@ -206,10 +209,11 @@ def c3_regexes(n: int = 1000, seed: int = records.SEED_BASE + 2):
                 segs.append(("alt", tuple(sorted(set("/" + W[i] for i in rng.choice(len(W), k, replace=False))))))
             else:
                 segs.append(("opt", "/" + W[rng.integers(len(W))]))
+        if not any(k == "lit" for k, _ in segs):
+            segs[int(rng.integers(len(segs)))] = ("lit", "/" + W[rng.integers(len(W))])
         if rng.random() < 0.3:
             segs.append(("ext", tuple(sorted(set(_C3_EXT[i] for i in rng.choice(len(_C3_EXT), int(rng.integers(1, 4)),
                                                                                replace=False))))))
-        anchored = rng.random() < 0.7
         dollar = rng.random() < 0.5
         caseless = rng.random() < 0.2
         pcre_only = rng.random() < 0.05

@@ -162,6 +162,8 @@ typedef struct {
     int has_return; int ret_code;
     char *err418;             /* error_page 418 = <complex value> */
     int waf_mode;
+    int pcre_only;            /* regex location the engine rejects (orc_pcre_only) */
+    pcre *relaxed;            /* its superset pattern (orc_relax), NULL = none */
 } loc_t;
 
 typedef struct { char *var; int op; char *val; pcre *re; int code; char *text; int is_return_only; } sif_t;
@@ -206,6 +208,92 @@ static pcre *re_compile(const char *pat, int caseless) {
     const char *e; int eo;
     pcre *r = pcre_compile(pat, caseless ? PCRE_CASELESS : 0, &e, &eo, NULL);
     return r;
+}
+
+/* PCRE-only syntax, restated from the engine's contract (rejected at compile
+ * time and counted): backreferences \1-\9 \g \k, \K, lookaround (?= (?! (?<= (?<!, atomic (?>,
+ * recursion / conditionals / callouts / named groups (?R (?( (?C (?P (?& (?| (?<digit>,
+ * possessive quantifiers *+ ++ ?+ }+.  A request that reaches such a regex location (no earlier
+ * regex matched) is GM_ACT_UNSUPPORTED: nginx's answer depends on PCRE, the engine defers it. */
+int orc_pcre_only(const char *p) {
+    size_t n = strlen(p);
+    int in_cls = 0;
+    for (size_t i = 0; i < n; i++) {
+        char ch = p[i];
+        if (ch == '\\' && i + 1 < n) {
+            char e = p[i + 1];
+            if (!in_cls && ((e >= '1' && e <= '9') || e == 'g' || e == 'k' || e == 'K')) return 1;
+            i++;
+            continue;
+        }
+        if (in_cls) { if (ch == ']') in_cls = 0; continue; }
+        if (ch == '[') { in_cls = 1; if (i + 1 < n && p[i + 1] == '^') i++; if (i + 1 < n && p[i + 1] == ']') i++; continue; }
+        if (ch == '(' && i + 2 < n && p[i + 1] == '?') {
+            char a = p[i + 2];
+            if (a == '=' || a == '!' || a == '>' || a == 'R' || a == '(' || a == 'C' || a == 'P' || a == '&' ||
+                a == '|' || (a >= '0' && a <= '9')) return 1;
+            if (a == '<' && i + 3 < n && (p[i + 3] == '=' || p[i + 3] == '!')) return 1;
+            continue;
+        }
+        if ((ch == '*' || ch == '+' || ch == '?' || ch == '}') && i + 1 < n && p[i + 1] == '+') {
+            if (ch == '?' && i > 0 && p[i - 1] == '(') continue;
+            return 1;
+        }
+    }
+    return 0;
+}
+
+/* The engine's superset of a PCRE-only pattern (gm_compile.cpp relax_pcre_only, restated):
+ * lookaround groups dropped, (?> -> (?:, possessive -> greedy, \K dropped, backreferences ->
+ * (?:.|\n)*.  Returns a malloc'd string, or NULL when the engine has no superset. */
+char *orc_relax(const char *p) {
+    size_t n = strlen(p), k = 0;
+    char *o = malloc(n * 10 + 16);
+    int cls = 0;
+    for (size_t i = 0; i < n; i++) {
+        char ch = p[i];
+        if (ch == '\\' && i + 1 < n) {
+            char e = p[i + 1];
+            if (!cls && e >= '1' && e <= '9') { memcpy(o + k, "(?:.|\\n)*", 9); k += 9; i++; continue; }
+            if (!cls && e == 'K') { i++; continue; }
+            if (!cls && (e == 'g' || e == 'k')) { free(o); return NULL; }
+            o[k++] = ch; o[k++] = e; i++;
+            continue;
+        }
+        if (cls) { o[k++] = ch; if (ch == ']') cls = 0; continue; }
+        if (ch == '[') {
+            cls = 1; o[k++] = ch;
+            if (i + 1 < n && p[i + 1] == '^') o[k++] = p[++i];
+            if (i + 1 < n && p[i + 1] == ']') o[k++] = p[++i];
+            continue;
+        }
+        if (ch == '(' && i + 2 < n && p[i + 1] == '?') {
+            char a = p[i + 2];
+            int look = a == '=' || a == '!' || (a == '<' && i + 3 < n && (p[i + 3] == '=' || p[i + 3] == '!'));
+            if (look) {
+                int depth = 0, c2 = 0;
+                size_t j = i;
+                for (; j < n; j++) {
+                    if (p[j] == '\\') { j++; continue; }
+                    if (c2) { if (p[j] == ']') c2 = 0; continue; }
+                    if (p[j] == '[') { c2 = 1; if (j + 1 < n && p[j + 1] == '^') j++; if (j + 1 < n && p[j + 1] == ']') j++; continue; }
+                    if (p[j] == '(') depth++;
+                    else if (p[j] == ')' && --depth == 0) break;
+                }
+                if (j >= n) { free(o); return NULL; }
+                i = j;
+                if (i + 1 < n && (p[i + 1] == '*' || p[i + 1] == '+' || p[i + 1] == '?' || p[i + 1] == '{')) { free(o); return NULL; }
+                continue;
+            }
+            if (a == '>') { memcpy(o + k, "(?:", 3); k += 3; i += 2; continue; }
+            if (a == 'R' || a == '(' || a == 'C' || a == 'P' || a == '&' || a == '|' || (a >= '0' && a <= '9')) { free(o); return NULL; }
+        }
+        if ((ch == '*' || ch == '+' || ch == '?' || ch == '}') && i + 1 < n && p[i + 1] == '+' &&
+            !(ch == '?' && i > 0 && p[i - 1] == '(')) { o[k++] = ch; i++; continue; }
+        o[k++] = ch;
+    }
+    o[k] = 0;
+    return o;
 }
 
 static int cmp_str(const void *a, const void *b) { return strcmp(*(char *const *)a, *(char *const *)b); }
@@ -299,7 +387,14 @@ static void add_location(build_t *B, srv_t *S, dir_t *d, int srv_waf) {
         L.path = strdup(a1); L.plen = d->alen[1];
         L.kind = (L.plen && L.path[0] == '@') ? LK_NAMED : LK_PREFIX;
     }
-    if (L.kind == LK_REGEX || L.kind == LK_REGEX_I) L.re = re_compile(L.path, L.kind == LK_REGEX_I);
+    if (L.kind == LK_REGEX || L.kind == LK_REGEX_I) {
+        L.re = re_compile(L.path, L.kind == LK_REGEX_I);
+        L.pcre_only = orc_pcre_only(L.path);
+        if (L.pcre_only) {
+            char *rp = orc_relax(L.path);
+            if (rp) { L.relaxed = re_compile(rp, L.kind == LK_REGEX_I); free(rp); }
+        }
+    }
     for (int i = 0; i < d->nkids; i++) {
         dir_t *k = &d->kids[i];
         if (!k->nargs) continue;
@@ -906,6 +1001,10 @@ static int find_location(orc_ctx *c, srv_t *S, sv uri, int *auto301) {
         loc_t *L = &c->loc[S->locs[i]];
         if ((L->kind != LK_REGEX && L->kind != LK_REGEX_I) || !L->re) continue;
         int ov[30];
+        if (L->pcre_only) {   /* reached and its superset matches: deferred (GM_ACT_UNSUPPORTED) */
+            if (!L->relaxed || pcre_exec(L->relaxed, NULL, uri.p, uri.n, 0, 0, ov, 30) >= 0) return L->id;
+            continue;
+        }
         if (pcre_exec(L->re, NULL, uri.p, uri.n, 0, 0, ov, 30) >= 0) return L->id;
     }
     return best;
@@ -1007,6 +1106,7 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
     v->location_id = (uint32_t)lid;
     if (a301) { v->action = GM_ACT_AUTO_301; v->status = 301; return; }
     loc_t *L = &c->loc[lid];
+    if (L->pcre_only) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
     loc_t *F = L;   /* location that runs the content phase */
     if (L->has_return && L->ret_code == 418 && L->err418) {
         int pidx = -2, part = -2;

@@ -253,3 +253,31 @@ def test_empty_and_generation_swap(eng):
         eng.load(b"GMB1\x00", 10)
     v2, _ = eng.match_host(reqs, arena)
     assert np.array_equal(v1, v2)
+
+
+def test_c3_regex_locations_parity(eng):
+    """C3: 1k regex locations (factor prefilter path), URIs 32-256 B, 40 % crafted to hit;
+    PCRE-only locations reached in order give GM_ACT_UNSUPPORTED on both sides."""
+    regs = workloads.c3_regexes()
+    reqs, arena = workloads.gen_c3(50_000, regs)
+    got, gh, exp, eh = run_both(eng, workloads.c3_blob(regs), reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "c3")
+    hit = np.isin(got["location_id"], np.arange(3, len(regs) + 3))
+    assert 0.3 < hit.mean() < 0.99
+
+
+def test_regex_location_prefilter_edges(eng):
+    """More than RLOC_SEQ_MAX regex locations: > RK_K candidates sharing one key (rescan), the
+    always list (no 4-byte factor) interleaved in config order, caseless, PCRE-only reached."""
+    pats = [("~", f"^/api/v{i}/item$") for i in range(12)]          # 12 candidates on "/api"
+    pats += [("~", r"^/x\d"), ("~*", r"\.PHP$"), ("~", r"^/api/(?=v)"), ("~", r"/api/v11/"),
+             ("~", r"^/a"), ("~*", r"/API/Z")]
+    locs = "".join(f'    location {op} "{p}" {{ return 2{i:02d}; }}\n' for i, (op, p) in enumerate(pats))
+    conf = ("http {\n  server {\n    listen 80 default_server;\n    server_name e.example.com;\n"
+            "    location / { return 404; }\n" + locs + "  }\n}\n")
+    b = blob.make_blob(conf, {})
+    uris = [f"/api/v{i}/item" for i in range(12)] + ["/api/v11/item/", "/api/v11/x", "/api/w", "/x7",
+            "/y.php", "/y.PhP", "/a", "/b/api/z", "/b/API/z", "/api/v3/item/", "/", "", "/ap", "/API/v1/item"]
+    reqs, arena = records.from_dicts([{"host": "e.example.com", "uri": u} for u in uris])
+    got, gh, exp, eh = run_both(eng, b, reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "regex prefilter edges")

@@ -165,3 +165,20 @@ def test_prefilter_covers_every_literal_occurrence(stage2):
             start = hay.find(needle, start + 1)
     assert checked > 200
     assert len(cand) < len(a) * (5e-4 if stage2 else 2e-3)
+
+
+def test_c3_regex_locations_compile(eng):
+    """C3: 1k regex locations compile; the PCRE-only ones are rejected and
+    counted, and the oracle's restated PCRE-only rule agrees with the compiler on every one."""
+    import ctypes
+    from oracle_py import lib as oracle_lib
+    regs = workloads.c3_regexes()
+    eng.load(workloads.c3_blob(regs), 3)
+    s = eng.stats()
+    ol = oracle_lib()
+    ol.orc_pcre_only.restype = ctypes.c_int
+    ol.orc_pcre_only.argtypes = [ctypes.c_char_p]
+    flagged = [bool(ol.orc_pcre_only(p.encode())) for p, *_ in regs]
+    assert flagged == [r[2] for r in regs]
+    assert s["n_rejected_pcre"] == sum(flagged) > 0
+    assert s["n_locations"] == len(regs) + 3
