@@ -1205,6 +1205,36 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     // second pass: an ar_loc whose node later got a location is void
     for (auto &nd : nodes) if (nd.prefix_loc >= 0 || nd.exact_loc >= 0) nd.ar_loc = -1;
 
+    // small servers: the trie nodes that carry a location, as a flat list (DSmallLoc)
+    std::vector<DSmallLoc> smalls;
+    std::unordered_map<uint32_t, std::vector<std::pair<uint8_t, uint32_t>>> kids;
+    for (auto &kv : edge_map) kids[kv.first.first].push_back({kv.first.second, kv.second});
+    for (auto &S : M.servers) {
+        DServer &D = dservers[S.id];
+        if (D.trie_depth > 16) continue;
+        std::vector<std::pair<std::string, uint32_t>> todo{{"", D.trie_root}}, marked;
+        bool ok = true;
+        while (!todo.empty() && ok) {
+            auto [path, nd] = todo.back();
+            todo.pop_back();
+            const DNode &N = nodes[nd];
+            if (N.prefix_loc >= 0 || N.exact_loc >= 0 || N.ar_loc >= 0) marked.push_back({path, nd});
+            if (marked.size() > SMALL_LOCS_MAX) ok = false;
+            for (auto &c : kids[nd]) todo.push_back({path + (char)c.first, c.second});
+        }
+        if (!ok) continue;
+        D.sl_first = (uint32_t)smalls.size(); D.sl_n = (uint32_t)marked.size();
+        if (D.sl_n == 0) { D.sl_first = 0; continue; }   // no location at all: the walk finds none either
+        for (auto &m : marked) {
+            DSmallLoc e{};
+            memcpy(e.path, m.first.data(), m.first.size());
+            e.len = (uint32_t)m.first.size();
+            e.prefix_loc = nodes[m.second].prefix_loc; e.exact_loc = nodes[m.second].exact_loc;
+            e.ar_loc = nodes[m.second].ar_loc;
+            smalls.push_back(e);
+        }
+    }
+
     uint32_t ecap = pow2_at_least(edge_list.size() * 2 + 1);
     std::vector<DEdge> edges(ecap, DEdge{0, 0, -1, 0});
     for (auto &e : edge_list) {
@@ -1401,7 +1431,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_lit_buckets = I.put(ltab); h.off_lits = I.put(dlits); h.off_sig_regex = I.put(sregex);
     h.off_always = I.put(always);
     h.n_rk_cap = rkcap; h.n_rk_ids = (uint32_t)rk_ids.size();
-    h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids);
+    h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_small = I.put(smalls);
     C.bytes.resize(C.bytes.size() + 64, 0);   // slack: vector compares may over-read
     h.off_bytes = I.put(C.bytes);
     I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
@@ -1448,6 +1478,7 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.rk = (const DRlocKey *)(b + h.off_rk);
     t.rk_ids = (const uint32_t *)(b + h.off_rk_ids);
     t.rk_mask = h.n_rk_cap - 1;
+    t.small = (const DSmallLoc *)(b + h.off_small);
     t.n_ports = h.n_ports;
     t.names_mask = h.n_names_cap - 1; t.wild_head_mask = h.n_wild_head_cap - 1; t.wild_tail_mask = h.n_wild_tail_cap - 1;
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;

@@ -638,40 +638,64 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
     uint32_t uw[8];
     // only the bytes the walk can read: it stops at the server's deepest location name
     load_span_n(A, f_uri, alen, min(min(r.uri_len, S.trie_depth + 1u), 32u), uw);
-    uint32_t node = S.trie_root;
-    int32_t best = t.nodes[node].prefix_loc;
-    uint32_t i = 0;
-    for (;; i++) {
-        if (i == r.uri_len) break;
-        uint32_t b;
-        if (i < 32) {
-            b = uw[0] & 0xFF;
-            uw[0] >>= 8;
-            if ((i & 3) == 3) {
+    int32_t best = -1, fexact = -1, far = -1;
+    bool full = false;   // a location-trie node spells the whole URI
+    if (S.sl_n) {
+        // small server: compare the URI's first 16 bytes with every location-carrying node
+        uint32_t bestlen = 0;
+        for (uint32_t j = 0; j < S.sl_n; j++) {
+            const DSmallLoc E = t.small[S.sl_first + j];
+            if (E.len > r.uri_len) continue;
+            uint32_t diff = 0;
 #pragma unroll
-                for (int k = 0; k < 7; k++) uw[k] = uw[k + 1];
-                uw[7] = 0;
+            for (int k = 0; k < 4; k++) {
+                const int rem = (int)E.len - 4 * k;
+                const uint32_t m = rem >= 4 ? 0xFFFFFFFFu : rem > 0 ? (1u << (8 * rem)) - 1 : 0u;
+                diff |= (uw[k] ^ E.path[k]) & m;
             }
-        } else {
-            b = u[i];
+            if (diff) continue;
+            if (E.len == r.uri_len) { full = true; fexact = E.exact_loc; far = E.ar_loc; }
+            if (E.prefix_loc >= 0 && (best < 0 || E.len > bestlen)) { best = E.prefix_loc; bestlen = E.len; }
         }
-        const uint32_t key = node * 256u + b + 1u;
-        uint32_t slot = edge_hash(key) & t.edges_mask, child = GM_NONE;
-        int32_t cpref = -1;
-        for (;; slot = (slot + 1) & t.edges_mask) {
-            const DEdge e = t.edges[slot];
-            if (e.key == 0) break;
-            if (e.key == key) { child = e.child; cpref = e.child_prefix; break; }
+    } else {
+        uint32_t node = S.trie_root;
+        best = t.nodes[node].prefix_loc;
+        uint32_t i = 0;
+        for (;; i++) {
+            if (i == r.uri_len) break;
+            uint32_t b;
+            if (i < 32) {
+                b = uw[0] & 0xFF;
+                uw[0] >>= 8;
+                if ((i & 3) == 3) {
+    #pragma unroll
+                    for (int k = 0; k < 7; k++) uw[k] = uw[k + 1];
+                    uw[7] = 0;
+                }
+            } else {
+                b = u[i];
+            }
+            const uint32_t key = node * 256u + b + 1u;
+            uint32_t slot = edge_hash(key) & t.edges_mask, child = GM_NONE;
+            int32_t cpref = -1;
+            for (;; slot = (slot + 1) & t.edges_mask) {
+                const DEdge e = t.edges[slot];
+                if (e.key == 0) break;
+                if (e.key == key) { child = e.child; cpref = e.child_prefix; break; }
+            }
+            if (child == GM_NONE) break;
+            node = child;
+            if (cpref >= 0) best = cpref;
         }
-        if (child == GM_NONE) break;
-        node = child;
-        if (cpref >= 0) best = cpref;
+        if (i == r.uri_len) {
+            const DNode nd = t.nodes[node];
+            full = true; fexact = nd.exact_loc; far = nd.ar_loc;
+        }
     }
     int32_t loc = -1;
-    if (i == r.uri_len) {
-        const DNode nd = t.nodes[node];
-        if (nd.exact_loc >= 0) loc = nd.exact_loc;
-        else if (nd.ar_loc >= 0) { o.loc = (uint32_t)nd.ar_loc; o.action = GM_ACT_AUTO_301; o.status = 301; return; }
+    if (full) {
+        if (fexact >= 0) loc = fexact;
+        else if (far >= 0) { o.loc = (uint32_t)far; o.action = GM_ACT_AUTO_301; o.status = 301; return; }
     }
     if (loc < 0) {
         if (best >= 0 && t.locs[best].noregex) loc = best;
@@ -823,7 +847,8 @@ struct gm_ctx {
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_blk = nullptr, ev_scan = nullptr;
     int route_prio = 1;            // k_route beside the scan at raised issue priority (GM_ROUTE_PRIO)
-    int route_mode = 0;            // 0: route beside the scan, 1: after it (GM_ROUTE_MODE tuning knob)
+    int route_mode = 0;            // 0: route beside the scan, 1: after it, 2: split (GM_ROUTE_MODE tuning knob)
+    int route_split = 60;          // mode 2: percent of the requests routed beside the scan (GM_ROUTE_SPLIT)
     bool ev_pending = false;
     int ev_used = 0;
     float last_ms[4] = {0, 0, 0, 0};
@@ -880,6 +905,7 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
         if (const char *ev = getenv("GM_SCAN_STAGE")) c->scan_stage = atoi(ev);
         if (const char *ev = getenv("GM_ROUTE_WPE")) c->route_wpe = atoi(ev);
         if (const char *ev = getenv("GM_ROUTE_MODE")) c->route_mode = atoi(ev);
+        if (const char *ev = getenv("GM_ROUTE_SPLIT")) c->route_split = std::min(100, std::max(0, atoi(ev)));
         if (const char *ev = getenv("GM_ROUTE_PRIO")) c->route_prio = atoi(ev);
         if (hipMalloc((void **)&c->d_status, STATUS_WORDS * 4) != hipSuccess ||
             hipHostMalloc((void **)&c->h_status, STATUS_WORDS * 4, hipHostMallocDefault) != hipSuccess) {
@@ -1001,33 +1027,44 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
     // and the exact check (latency-bound kernels), with blk2rec from k_blk2rec beside the scan.
     HIPCHK(c, hipEventRecord(c->ev_fork, s));
     HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
-    const bool late = c->route_mode == 1;
+    // route_mode 0: k_route beside the scan; 1: after the scan, beside the context filter and the
+    // exact check; 2: split -- the first route_split % of the requests beside the scan, the rest
+    // after it (the scan with staged records is short enough that a whole route beside it ends
+    // later than the scan).  Modes 1 and 2 write blk2rec with k_blk2rec beside the scan.
+    const bool late = c->route_mode >= 1;
     if (late) {
         k_blk2rec<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 4)), 256, 0,
                     c->side>>>(reqs, n, alen, c->d_blk2rec, nblk);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipEventRecord(c->ev_blk, c->side));
     }
+    auto route_part = [&](uint32_t i0, uint32_t cnt, uint32_t *b2r, int prio) -> int {
+        if (cnt == 0) return GM_OK;
+        const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>((cnt + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
+                                                                     (uint32_t)c->cu_count * 8));
+        const gm_req *rq = reqs + i0;
+        gm_verdict *ov = out + i0;
+        if (c->route_wpe == 5)
+            k_route<5><<<nb, ROUTE_BLOCK, 0, c->side>>>(rq, cnt, A, alen, t, ov, c->d_counters, b2r, nblk, prio);
+        else if (c->route_wpe == 6)
+            k_route<6><<<nb, ROUTE_BLOCK, 0, c->side>>>(rq, cnt, A, alen, t, ov, c->d_counters, b2r, nblk, prio);
+        else if (c->route_wpe == 4)
+            k_route<4><<<nb, ROUTE_BLOCK, 0, c->side>>>(rq, cnt, A, alen, t, ov, c->d_counters, b2r, nblk, prio);
+        else
+            k_route<3><<<nb, ROUTE_BLOCK, 0, c->side>>>(rq, cnt, A, alen, t, ov, c->d_counters, b2r, nblk, prio);
+        HIPCHK(c, hipGetLastError());
+        return GM_OK;
+    };
     auto launch_route = [&]() -> int {
+        if (prof) HIPCHK(c, hipEventRecord(c->ev_route[0], c->side));
+        int e2;
+        const uint32_t n1 = c->route_mode == 2 ? (uint32_t)((uint64_t)n * (uint32_t)c->route_split / 100) : 0;
+        if (c->route_mode == 2 && (e2 = route_part(0, n1, nullptr, c->route_prio))) return e2;
         if (late) {
             HIPCHK(c, hipEventRecord(c->ev_scan, s));
             HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_scan, 0));
         }
-        uint32_t *b2r = late ? nullptr : c->d_blk2rec;
-        if (prof) HIPCHK(c, hipEventRecord(c->ev_route[0], c->side));
-        if (c->route_wpe == 5)
-            k_route<5><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
-                                                                  b2r, nblk, late ? 0 : c->route_prio);
-        else if (c->route_wpe == 6)
-            k_route<6><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
-                                                                  b2r, nblk, late ? 0 : c->route_prio);
-        else if (c->route_wpe == 4)
-            k_route<4><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
-                                                                  b2r, nblk, late ? 0 : c->route_prio);
-        else
-            k_route<3><<<route_blocks, ROUTE_BLOCK, 0, c->side>>>(reqs, n, A, alen, t, out, c->d_counters,
-                                                                  b2r, nblk, late ? 0 : c->route_prio);
-        HIPCHK(c, hipGetLastError());
+        if ((e2 = route_part(n1, n - n1, late ? nullptr : c->d_blk2rec, late ? 0 : c->route_prio))) return e2;
         if (prof) HIPCHK(c, hipEventRecord(c->ev_route[1], c->side));
         HIPCHK(c, hipEventRecord(c->ev_join, c->side));
         c->route_side = true;

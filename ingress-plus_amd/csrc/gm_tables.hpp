@@ -48,7 +48,17 @@ struct DServer {
     uint32_t rk_on;          // regex locations behind the factor prefilter (n_rloc > RLOC_SEQ_MAX)
     uint32_t first_ralw, n_ralw;  // rk_ids slice: regex locations evaluated for every URI (no
                                   // >= 4-byte factor, or PCRE-only), ascending
-    uint32_t pad;
+    uint32_t sl_first, sl_n;      // small-server location list (DSmallLoc), sl_n = 0: trie walk
+};
+// A server whose location names all fit 16 bytes and whose trie has at most SMALL_LOCS_MAX
+// nodes carrying a location gets those nodes as a flat list: the route compares the URI's
+// first 16 bytes (registers) with every entry -- independent loads instead of one dependent
+// edge probe per URI byte.  Same answers as the trie walk (exact, longest prefix, auto_redirect).
+constexpr uint32_t SMALL_LOCS_MAX = 8;
+struct DSmallLoc {
+    uint32_t path[4];        // name bytes, zero padded
+    uint32_t len;
+    int32_t prefix_loc, exact_loc, ar_loc;   // as DNode
 };
 // A server with more regex locations than this evaluates them behind a factor prefilter: every
 // match of regex k contains one of its factors, so k is a candidate only if one of its key
@@ -191,6 +201,7 @@ struct TabHeader {
     uint32_t ctx_mul;        // stage-2 context filter multiplier (waf_b, see ctx_key)
     uint32_t n_rk_cap, n_rk_ids;   // regex-location prefilter: key table (pow2) and id lists
     uint64_t off_rk, off_rk_ids;
+    uint64_t off_small;            // DSmallLoc lists
 };
 
 struct GTab {                // device pointers, built on host from the image base
@@ -202,7 +213,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const DDfa *dfas; const uint16_t *dfa_trans; const uint8_t *dfa_acc; const uint8_t *dfa_cls;
     const uint8_t *bytes; const uint32_t *waf_a; const uint32_t *waf_b;
     const DLitBucket *lit_buckets; const DLit *lits; const DSigRegex *sig_regex; const uint32_t *always;
-    const DRlocKey *rk; const uint32_t *rk_ids; uint32_t rk_mask;
+    const DRlocKey *rk; const uint32_t *rk_ids; uint32_t rk_mask; const DSmallLoc *small;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
     uint32_t gen;
