@@ -1247,7 +1247,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     // folded 4-byte window per factor (every match contains one of its factors); the window is
     // the one shared by the fewest regexes so far, preferring windows that span a '/' (a path
     // segment boundary: rarer in URIs than a window inside one word).
-    std::map<std::pair<uint32_t, uint32_t>, std::vector<uint32_t>> rk_lists;   // (server, key) -> k
+    std::map<std::pair<uint32_t, uint32_t>, std::vector<DRlocEnt>> rk_lists;   // (server, key) -> entries
+    std::vector<DRlocEnt> rk_ents;
     std::vector<uint32_t> rk_ids;
     for (auto &S : M.servers) {
         DServer &D = dservers[S.id];
@@ -1258,20 +1259,22 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             const DRegexLoc &rl = rlocs[D.first_rloc + k];
             const auto &fac = rloc_factors[D.first_rloc + k];
             if (rl.dfa == GM_NONE || fac.empty()) { alw.push_back(k); continue; }
-            std::set<uint32_t> keys;
+            std::vector<std::pair<uint32_t, DRlocEnt>> keys;   // a factor each (two may share a window)
             for (const std::string &f : fac) {
-                uint32_t best = 0; int best_cost = INT32_MAX;
+                uint32_t best = 0; int best_cost = INT32_MAX, best_o = 0;
                 for (size_t o = 0; o + 4 <= f.size(); o++) {
                     uint32_t w = 0;
                     for (int b = 0; b < 4; b++) w |= (uint32_t)(uint8_t)f[o + b] << (8 * b);
                     w = fold4(w);
                     bool span = f[o + 1] == '/' || f[o + 2] == '/' || f[o + 3] == '/';
                     int cost = 2 * (int)use[w] + (span ? 0 : 1);
-                    if (cost < best_cost) { best_cost = cost; best = w; }
+                    if (cost < best_cost) { best_cost = cost; best = w; best_o = (int)o; }
                 }
-                keys.insert(best);
+                std::string ff = f.substr(0, 0x7FFF);   // a prefix of a factor is a factor
+                for (char &ch : ff) ch = (char)((uint8_t)ch | 0x20);
+                keys.push_back({best, DRlocEnt{k, C.put_bytes(ff), (uint16_t)ff.size(), (int16_t)best_o}});
             }
-            for (uint32_t w : keys) { use[w]++; rk_lists[{(uint32_t)S.id, w}].push_back(k); }
+            for (auto &kv : keys) { use[kv.first]++; rk_lists[{(uint32_t)S.id, kv.first}].push_back(kv.second); }
         }
         D.first_ralw = (uint32_t)rk_ids.size(); D.n_ralw = (uint32_t)alw.size();
         rk_ids.insert(rk_ids.end(), alw.begin(), alw.end());
@@ -1282,8 +1285,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         const uint32_t sv = kv.first.first, w = kv.first.second;
         uint32_t i = rk_hash(w, sv) & (rkcap - 1);
         while (rk[i].key) i = (i + 1) & (rkcap - 1);
-        rk[i] = DRlocKey{w, (uint32_t)rk_ids.size(), (uint32_t)kv.second.size(), sv};
-        rk_ids.insert(rk_ids.end(), kv.second.begin(), kv.second.end());   // ascending: pushed in k order
+        rk[i] = DRlocKey{w, (uint32_t)rk_ents.size(), (uint32_t)kv.second.size(), sv};
+        rk_ents.insert(rk_ents.end(), kv.second.begin(), kv.second.end());   // ascending k: pushed in k order
     }
 
     // ---- signatures
@@ -1431,7 +1434,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_lit_buckets = I.put(ltab); h.off_lits = I.put(dlits); h.off_sig_regex = I.put(sregex);
     h.off_always = I.put(always);
     h.n_rk_cap = rkcap; h.n_rk_ids = (uint32_t)rk_ids.size();
-    h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_small = I.put(smalls);
+    h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_small = I.put(smalls); h.off_rk_ents = I.put(rk_ents);
     C.bytes.resize(C.bytes.size() + 64, 0);   // slack: vector compares may over-read
     h.off_bytes = I.put(C.bytes);
     I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
@@ -1479,6 +1482,7 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.rk_ids = (const uint32_t *)(b + h.off_rk_ids);
     t.rk_mask = h.n_rk_cap - 1;
     t.small = (const DSmallLoc *)(b + h.off_small);
+    t.rk_ents = (const DRlocEnt *)(b + h.off_rk_ents);
     t.n_ports = h.n_ports;
     t.names_mask = h.n_names_cap - 1; t.wild_head_mask = h.n_wild_head_cap - 1; t.wild_tail_mask = h.n_wild_tail_cap - 1;
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;

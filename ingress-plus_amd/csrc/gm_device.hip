@@ -317,9 +317,16 @@ __device__ __noinline__ int32_t rloc_prefiltered(const GTab &t, const DServer &S
                 if (e.key == 0) break;
                 if (e.key != key || e.server != sid) continue;
                 for (uint32_t q = 0; q < e.count; q++) {
-                    const uint32_t k = t.rk_ids[e.first + q];
+                    const DRlocEnt E = t.rk_ents[e.first + q];
+                    const uint32_t k = E.k;
                     if (k < lo) continue;
                     if (k >= c[RK_K - 1]) break;   // ascending lists
+                    // the whole folded factor at the window (a superset check: the DFA decides)
+                    const int st = (int)i - 3 - (int)E.key_off;
+                    if (st < 0 || (uint32_t)st + E.fac_len > ulen) continue;
+                    bool fok = true;
+                    for (uint32_t j = 0; j < E.fac_len && fok; j++) fok = (u[st + j] | 0x20u) == t.bytes[E.fac_off + j];
+                    if (!fok) continue;
                     bool dup = false;
 #pragma unroll
                     for (int j = 0; j < RK_K; j++) dup |= c[j] == k;

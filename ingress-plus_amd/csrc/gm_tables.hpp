@@ -65,7 +65,10 @@ struct DSmallLoc {
 // windows (a folded 4-byte window of a factor) occurs in the URI.  Candidates run in config
 // order, merged with the always list; the first match wins (ngx_http_core_find_location).
 constexpr uint32_t RLOC_SEQ_MAX = 8;
-struct DRlocKey { uint32_t key; uint32_t first, count; uint32_t server; };   // key 0 = empty slot
+struct DRlocKey { uint32_t key; uint32_t first, count; uint32_t server; };   // key 0 = empty slot; DRlocEnt slice
+// one keyed regex: the folded factor whose window the key is, checked in full at the window
+// before the regex becomes a candidate
+struct DRlocEnt { uint32_t k; uint32_t fac_off; uint16_t fac_len; int16_t key_off; };
 struct DServerIf {
     uint32_t op;             // SIF_*
     uint32_t src;            // DSrc index (variable), unused for SIF_RETURN
@@ -202,6 +205,7 @@ struct TabHeader {
     uint32_t n_rk_cap, n_rk_ids;   // regex-location prefilter: key table (pow2) and id lists
     uint64_t off_rk, off_rk_ids;
     uint64_t off_small;            // DSmallLoc lists
+    uint64_t off_rk_ents;          // DRlocEnt lists
 };
 
 struct GTab {                // device pointers, built on host from the image base
@@ -213,7 +217,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const DDfa *dfas; const uint16_t *dfa_trans; const uint8_t *dfa_acc; const uint8_t *dfa_cls;
     const uint8_t *bytes; const uint32_t *waf_a; const uint32_t *waf_b;
     const DLitBucket *lit_buckets; const DLit *lits; const DSigRegex *sig_regex; const uint32_t *always;
-    const DRlocKey *rk; const uint32_t *rk_ids; uint32_t rk_mask; const DSmallLoc *small;
+    const DRlocKey *rk; const uint32_t *rk_ids; uint32_t rk_mask; const DSmallLoc *small; const DRlocEnt *rk_ents;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
     uint32_t gen;
