@@ -90,17 +90,54 @@ __device__ void ctx_init(Ctx &c, const uint8_t *A, const Rec &r) {
     c.ruri = o; o += r.ruri_len; c.raddr = o;
 }
 
+// first position of byte `ch` in A[p, e), or e: aligned 16-byte loads, SWAR zero-byte test per
+// word (the lowest flagged byte of (x - 0x01..) & ~x & 0x80.. is always a true match); only
+// words wholly inside [p, e) are read
+__device__ uint64_t find_byte(const uint8_t *A, uint64_t p, uint64_t e, uint32_t ch) {
+    const uint32_t pat = ch * 0x01010101u;
+    while (p < e && (p & 15)) { if (A[p] == ch) return p; p++; }
+    for (; p + 16 <= e; p += 16) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(A + p);
+        const uint32_t w[4] = {q.x ^ pat, q.y ^ pat, q.z ^ pat, q.w ^ pat};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t z = (w[k] - 0x01010101u) & ~w[k] & 0x80808080u;
+            if (z) return p + 4 * k + (__builtin_ctz(z) >> 3);
+        }
+    }
+    for (; p < e; p++) if (A[p] == ch) return p;
+    return e;
+}
+
+// first position of either byte in A[p, e), or e (find_byte with two patterns: the lowest flag
+// of each SWAR mask is a true match, so the lowest flag of their union is the first match)
+__device__ uint64_t find_byte2(const uint8_t *A, uint64_t p, uint64_t e, uint32_t c1, uint32_t c2) {
+    const uint32_t p1 = c1 * 0x01010101u, p2 = c2 * 0x01010101u;
+    while (p < e && (p & 15)) { if (A[p] == c1 || A[p] == c2) return p; p++; }
+    for (; p + 16 <= e; p += 16) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(A + p);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t a = w[k] ^ p1, b = w[k] ^ p2;
+            const uint32_t z = ((a - 0x01010101u) & ~a & 0x80808080u) | ((b - 0x01010101u) & ~b & 0x80808080u);
+            if (z) return p + 4 * k + (__builtin_ctz(z) >> 3);
+        }
+    }
+    for (; p < e; p++) if (A[p] == c1 || A[p] == c2) return p;
+    return e;
+}
+
 // iterate "Name: value\r\n" lines; returns false at end
 struct HdrIt { uint64_t pos, end; };
 __device__ bool hdr_next(const uint8_t *A, HdrIt &it, uint64_t &ns, uint32_t &nl, uint64_t &vs, uint32_t &vl) {
     while (it.pos < it.end) {
-        uint64_t st = it.pos, e = st;
-        while (e < it.end && A[e] != '\n') e++;
+        uint64_t st = it.pos;
+        const uint64_t e = find_byte(A, st, it.end, '\n');
         it.pos = e + 1;
         uint64_t le = e;
         if (le > st && A[le - 1] == '\r') le--;
-        uint64_t c = st;
-        while (c < le && A[c] != ':') c++;
+        const uint64_t c = find_byte(A, st, le, ':');
         if (c >= le) continue;
         ns = st; nl = (uint32_t)(c - st);
         uint64_t v0 = c + 1;
@@ -206,13 +243,13 @@ __device__ void get_var(Ctx &c, const GTab &t, uint32_t src_id, Val &v) {
                     if (start < end && A[start] == '=') {
                         start++;
                         while (start < end && A[start] == ' ') start++;
-                        uint64_t last = start;
-                        while (last < end && A[last] != ';') last++;
+                        const uint64_t last = find_byte(A, start, end, ';');
                         v.add(A + start, (uint32_t)(last - start));
                         return;
                     }
                 }
-                while (start < end) { uint8_t ch = A[start++]; if (ch == ';' || ch == ',') break; }
+                start = find_byte2(A, start, end, ';', ',');
+                if (start < end) start++;
                 while (start < end && A[start] == ' ') start++;
             }
         }
@@ -220,18 +257,19 @@ __device__ void get_var(Ctx &c, const GTab &t, uint32_t src_id, Val &v) {
     }
     if (s.kind == SRC_ARG) {
         // ngx_http_arg
+        // the first occurrence of the name at an argument start ("&" or the beginning) followed
+        // by '=': only argument starts can qualify, so they are visited directly
         uint64_t a = c.args;
         uint32_t n = r.args_len, L = s.name_len;
-        for (uint32_t p = 0; p + L < n; p++) {
+        for (uint32_t p = 0; p + L < n;) {
             bool ok = true;
             for (uint32_t k = 0; ok && k < L; k++) if (lc(A[a + p + k]) != nm[k]) ok = false;
-            if (!ok) continue;
-            if ((p == 0 || A[a + p - 1] == '&') && A[a + p + L] == '=') {
-                uint32_t b = p + L + 1, e = b;
-                while (e < n && A[a + e] != '&') e++;
-                v.add(A + a + b, e - b);
+            const uint32_t amp = (uint32_t)(find_byte(A, a + p, a + n, '&') - a);
+            if (ok && A[a + p + L] == '=') {
+                v.add(A + a + p + L + 1, amp - (p + L + 1));
                 return;
             }
+            p = amp + 1;
         }
     }
 }
