@@ -597,16 +597,34 @@ __device__ __noinline__ uint8_t rules_generic(const uint8_t *A, const gm_req *rp
     Ctx c;
     ctx_init(c, A, r);
     Val v;
+    // header / cookie / argument values are looked up once per request, not once per condition
+    // that reads them (every match of a rules route repeats the route's conditions); variables
+    // are cheap and some share c.scratch, so they are not kept
+    constexpr int MEMO = 4;
+    Val memo[MEMO];
+    uint32_t msrc[MEMO];
+    int nmemo = 0;
     uint32_t bits = 0;
     for (uint32_t ch = 0; ch < R.n_chains; ch++) {
         int32_t nd = (int32_t)t.chain_heads[R.first_chain + ch];
         int guard = 0;
         while (nd >= 0 && guard++ < 64) {
             const DCond cd = t.conds[nd];
-            get_var(c, t, cd.src, v);
+            const Val *vp = nullptr;
+            for (int q = 0; q < nmemo; q++) if (msrc[q] == cd.src) vp = &memo[q];
+            if (!vp) {
+                if (nmemo < MEMO && t.srcs[cd.src].kind != SRC_VAR) {
+                    get_var(c, t, cd.src, memo[nmemo]);
+                    msrc[nmemo] = cd.src;
+                    vp = &memo[nmemo++];
+                } else {
+                    get_var(c, t, cd.src, v);
+                    vp = &v;
+                }
+            }
             bool m;
-            if (cd.is_regex) m = v.total > 0 && dfa_run_val(t, cd.dfa, v);
-            else m = val_eq(v, t.bytes + cd.key_off, cd.key_len, true);
+            if (cd.is_regex) m = vp->total > 0 && dfa_run_val(t, cd.dfa, *vp);
+            else m = val_eq(*vp, t.bytes + cd.key_off, cd.key_len, true);
             nd = m ? cd.next_true : cd.next_false;
         }
         if (nd == NEXT_1) bits |= 1u << ch;
