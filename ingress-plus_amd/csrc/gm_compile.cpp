@@ -412,7 +412,9 @@ struct Compiler {
         x.cls_off = (uint32_t)dfa_cls.size();
         x.n_states = (uint16_t)d.n_states; x.n_classes = (uint16_t)d.n_classes;
         x.flags = d.anchored_start ? DFA_ANCHOR_START : 0;
-        dfa_trans.insert(dfa_trans.end(), d.trans.begin(), d.trans.end());
+        // entries carry the target's accept flags in bits 14-15 (DFA_TRANS_STATE_MASK): the
+        // device step is one dependent load per byte, not a transition load then a flags load
+        for (uint16_t e : d.trans) dfa_trans.push_back((uint16_t)(e | (uint16_t)((d.acc[e] & 3u) << 14)));
         dfa_acc.insert(dfa_acc.end(), d.acc.begin(), d.acc.end());
         dfa_cls.insert(dfa_cls.end(), d.cls, d.cls + 256);
         dfas.push_back(x);

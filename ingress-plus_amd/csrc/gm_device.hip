@@ -291,18 +291,19 @@ __device__ bool dfa_run_val(const GTab &t, uint32_t dfa_id, const Val &v) {
     const DDfa d = t.dfas[dfa_id];
     const uint16_t *tr = t.dfa_trans + d.trans_off;
     const uint8_t *acc = t.dfa_acc + d.acc_off, *cls = t.dfa_cls + d.cls_off;
-    uint32_t st = 1;
-    if (acc[st] & 1) return true;
+    uint32_t st = 1, fl = acc[1];   // fl: accept flags of st (packed into the transitions)
+    if (fl & 1) return true;
     uint32_t pos = 0;
     for (int s = 0; s < v.cnt; s++)
         for (uint32_t i = 0; i < v.n[s]; i++, pos++) {
             uint8_t b = v.p[s][i];
-            if ((acc[st] & 2) && pos + 1 == v.total && b == '\n') return true;
-            st = tr[st * d.n_classes + cls[b]];
+            if ((fl & 2) && pos + 1 == v.total && b == '\n') return true;
+            const uint32_t e = tr[st * d.n_classes + cls[b]];
+            st = e & DFA_TRANS_STATE_MASK; fl = e >> 14;
             if (st == 0) return false;
-            if (acc[st] & 1) return true;
+            if (fl & 1) return true;
         }
-    return (acc[st] & 2) != 0;
+    return (fl & 2) != 0;
 }
 
 // `steps` (optional) accumulates the bytes consumed -- profiling counters of the WAF verify
@@ -310,18 +311,19 @@ __device__ bool dfa_run_bytes(const GTab &t, uint32_t dfa_id, const uint8_t *p, 
     const DDfa d = t.dfas[dfa_id];
     const uint16_t *tr = t.dfa_trans + d.trans_off;
     const uint8_t *acc = t.dfa_acc + d.acc_off, *cls = t.dfa_cls + d.cls_off;
-    uint32_t st = 1;
-    if (acc[st] & 1) return true;
+    uint32_t st = 1, fl = acc[1];   // fl: accept flags of st (packed into the transitions)
+    if (fl & 1) return true;
     uint32_t i = 0;
     bool r = false;
     for (; i < n; i++) {
         uint8_t b = p[i];
-        if ((acc[st] & 2) && i + 1 == n && b == '\n') { r = true; break; }
-        st = tr[st * d.n_classes + cls[b]];
+        if ((fl & 2) && i + 1 == n && b == '\n') { r = true; break; }
+        const uint32_t e = tr[st * d.n_classes + cls[b]];
+        st = e & DFA_TRANS_STATE_MASK; fl = e >> 14;
         if (st == 0) break;
-        if (acc[st] & 1) { r = true; break; }
+        if (fl & 1) { r = true; break; }
     }
-    if (i == n) r = (acc[st] & 2) != 0;
+    if (i == n) r = (fl & 2) != 0;
     if (steps) *steps += i;
     return r;
 }

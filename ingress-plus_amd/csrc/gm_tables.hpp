@@ -144,6 +144,9 @@ struct DPart { uint32_t bound; uint32_t star; uint32_t target; uint32_t pad; }; 
 
 // ---- DFAs (regex) ----------------------------------------------------------------------
 enum : uint32_t { DFA_ANCHOR_START = 1, DFA_ANCHOR_END = 2 };
+// dfa_trans entry = target state | accept flags of the target << 14 (states < 16384: the regex
+// compiler caps DFAs at 8192 states)
+constexpr uint32_t DFA_TRANS_STATE_MASK = 0x3FFFu;
 struct DDfa {
     uint32_t trans_off;      // uint16 [n_states][n_classes] into dfa_trans; state 0 = dead, 1 = start
     uint32_t acc_off;        // uint8 [n_states] accept flags into dfa_acc
