@@ -1283,8 +1283,11 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     }
     const uint32_t rkcap = pow2_at_least(rk_lists.size() * 2 + 1);
     std::vector<DRlocKey> rk(rkcap, DRlocKey{0, 0, 0, 0});
+    std::vector<uint32_t> rk_bloom(RK_BLOOM_WORDS, 0u);
     for (auto &kv : rk_lists) {
         const uint32_t sv = kv.first.first, w = kv.first.second;
+        const uint32_t bb = rk_bloom_bit(rk_hash(w, sv));
+        rk_bloom[bb >> 5] |= 1u << (bb & 31);
         uint32_t i = rk_hash(w, sv) & (rkcap - 1);
         while (rk[i].key) i = (i + 1) & (rkcap - 1);
         rk[i] = DRlocKey{w, (uint32_t)rk_ents.size(), (uint32_t)kv.second.size(), sv};
@@ -1435,8 +1438,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_waf_a = I.put(waf_a); h.off_waf_b = I.put(waf_b);
     h.off_lit_buckets = I.put(ltab); h.off_lits = I.put(dlits); h.off_sig_regex = I.put(sregex);
     h.off_always = I.put(always);
-    h.n_rk_cap = rkcap; h.n_rk_ids = (uint32_t)rk_ids.size();
-    h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_small = I.put(smalls); h.off_rk_ents = I.put(rk_ents);
+    h.n_rk_cap = rkcap; h.n_rk_ids = (uint32_t)rk_ids.size(); h.n_rk_ents_keys = (uint32_t)rk_lists.size();
+    h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_small = I.put(smalls); h.off_rk_ents = I.put(rk_ents); h.off_rk_bloom = I.put(rk_bloom);
     C.bytes.resize(C.bytes.size() + 64, 0);   // slack: vector compares may over-read
     h.off_bytes = I.put(C.bytes);
     I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
@@ -1485,6 +1488,8 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.rk_mask = h.n_rk_cap - 1;
     t.small = (const DSmallLoc *)(b + h.off_small);
     t.rk_ents = (const DRlocEnt *)(b + h.off_rk_ents);
+    t.rk_bloom = (const uint32_t *)(b + h.off_rk_bloom);
+    t.rk_keys = h.n_rk_ents_keys;
     t.n_ports = h.n_ports;
     t.names_mask = h.n_names_cap - 1; t.wild_head_mask = h.n_wild_head_cap - 1; t.wild_tail_mask = h.n_wild_tail_cap - 1;
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;

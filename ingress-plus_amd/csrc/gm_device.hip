@@ -315,10 +315,14 @@ __device__ bool dfa_run_bytes(const GTab &t, uint32_t dfa_id, const uint8_t *p, 
     if (fl & 1) return true;
     uint32_t i = 0;
     bool r = false;
+    // the next byte's class is loaded one step ahead: the only serial load per byte is the
+    // transition itself
+    uint32_t cn = n ? cls[p[0]] : 0u;
     for (; i < n; i++) {
-        uint8_t b = p[i];
-        if ((fl & 2) && i + 1 == n && b == '\n') { r = true; break; }
-        const uint32_t e = tr[st * d.n_classes + cls[b]];
+        const uint32_t cc = cn;
+        if (i + 1 < n) cn = cls[p[i + 1]];
+        else if ((fl & 2) && p[i] == '\n') { r = true; break; }   // $ before a final newline
+        const uint32_t e = tr[st * d.n_classes + cc];
         st = e & DFA_TRANS_STATE_MASK; fl = e >> 14;
         if (st == 0) break;
         if (fl & 1) { r = true; break; }
@@ -337,7 +341,7 @@ __device__ bool dfa_run_bytes(const GTab &t, uint32_t dfa_id, const uint8_t *p, 
 // keeps its registers.
 constexpr int RK_K = 8;
 __device__ __noinline__ int32_t rloc_prefiltered(const GTab &t, const DServer &S, uint32_t sid, const uint8_t *u,
-                                                 uint32_t ulen) {
+                                                 uint32_t ulen, const uint32_t *rkb) {
     auto run = [&](uint32_t k) -> bool {
         const DRegexLoc rl = t.rlocs[S.first_rloc + k];
         return rl.dfa == GM_NONE || dfa_run_bytes(t, rl.dfa, u, ulen);
@@ -352,7 +356,9 @@ __device__ __noinline__ int32_t rloc_prefiltered(const GTab &t, const DServer &S
             w = (w >> 8) | ((uint32_t)u[i] << 24);
             if (i < 3) continue;
             const uint32_t key = fold4(w);
-            for (uint32_t b = rk_hash(key, sid) & t.rk_mask;; b = (b + 1) & t.rk_mask) {
+            const uint32_t kh = rk_hash(key, sid), bb = rk_bloom_bit(kh);
+            if (rkb && !((rkb[bb >> 5] >> (bb & 31)) & 1u)) continue;   // LDS bit filter (k_route<, true>)
+            for (uint32_t b = kh & t.rk_mask;; b = (b + 1) & t.rk_mask) {
                 const DRlocKey e = t.rk[b];
                 if (e.key == 0) break;
                 if (e.key != key || e.server != sid) continue;
@@ -398,8 +404,8 @@ __device__ __noinline__ int32_t rloc_prefiltered(const GTab &t, const DServer &S
 // The regex-location step of ngx_http_core_find_location: the first regex location in config
 // order whose DFA matches the URI (-1: none).  Out of line, like the other rarely taken steps.
 __device__ __noinline__ int32_t rloc_first_match(const GTab &t, const DServer &S, uint32_t sid, const uint8_t *u,
-                                                 uint32_t ulen) {
-    if (S.rk_on) return rloc_prefiltered(t, S, sid, u, ulen);
+                                                 uint32_t ulen, const uint32_t *rkb) {
+    if (S.rk_on) return rloc_prefiltered(t, S, sid, u, ulen, rkb);
     for (uint32_t k = 0; k < S.n_rloc; k++) {
         const DRegexLoc rl = t.rlocs[S.first_rloc + k];
         if (rl.dfa == GM_NONE || dfa_run_bytes(t, rl.dfa, u, ulen)) return (int32_t)rl.loc;
@@ -653,7 +659,8 @@ __device__ __noinline__ uint32_t split_generic(const uint8_t *A, const gm_req *r
     return 0xFFu;
 }
 
-__device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const GTab &t, RouteOut &o) {
+__device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const GTab &t, RouteOut &o,
+                          const uint32_t *rkb) {
     o.server = GM_NONE; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0;
     o.action = GM_ACT_NO_LISTENER; o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF;
     const uint64_t f_uri = r.base, f_host = r.base + r.uri_len + r.args_len + r.hdr_len + r.body_len;
@@ -765,7 +772,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
     if (loc < 0) {
         if (best >= 0 && t.locs[best].noregex) loc = best;
         else {
-            loc = rloc_first_match(t, S, sid, u, r.uri_len);
+            loc = rloc_first_match(t, S, sid, u, r.uri_len, rkb);
             if (loc < 0) loc = best;
         }
     }
@@ -800,11 +807,14 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
 
 // ============================================================================ kernels
 constexpr int ROUTE_BLOCK = 256;
-constexpr uint32_t LDS_HIST_MAX = 2048;
+// per-block location histogram in LDS (generations with more locations count with wave-aggregated
+// global atomics): 2 KiB, so a route block fits beside the WAF scan's 128 KiB Bloom + 24 KiB of
+// record staging in the CU's 160 KiB
+constexpr uint32_t LDS_HIST_MAX = 512;
 
 // WPE: waves per SIMD the register allocation targets (beside the scan's workgroup, a CU has
 // room for route waves only when they are small)
-template <int WPE>
+template <int WPE, bool RK = false>
 __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_route(const gm_req *__restrict__ reqs, uint32_t n,
                                                        const uint8_t *__restrict__ A, uint64_t arena_len,
                                                        GTab t, gm_verdict *__restrict__ out,
@@ -816,11 +826,14 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
     __shared__ uint32_t hist[LDS_HIST_MAX];
     const bool use_hist = t.n_locs <= LDS_HIST_MAX;
     if (use_hist) for (uint32_t k = threadIdx.x; k < t.n_locs; k += blockDim.x) hist[k] = 0;
+    // RK: servers with many regex locations -- the prefilter's key bit filter in LDS
+    __shared__ uint32_t rkb[RK ? RK_BLOOM_WORDS : 1];
+    if (RK) for (uint32_t k = threadIdx.x; k < RK_BLOOM_WORDS; k += blockDim.x) rkb[k] = t.rk_bloom[k];
     __syncthreads();
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const Rec r = load_rec(reqs + i);
         RouteOut o;
-        route_one(A, arena_len, reqs + i, r, t, o);
+        route_one(A, arena_len, reqs + i, r, t, o, RK ? rkb : nullptr);
         uint4 w0, w1;
         w0.x = t.gen; w0.y = o.server; w0.z = o.loc; w0.w = o.ups;
         w1.x = (uint32_t)o.action | ((uint32_t)o.kind << 8) | ((uint32_t)o.bucket << 16) | ((uint32_t)o.match << 24);
@@ -1082,7 +1095,8 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
                                                                            (uint32_t)c->cu_count * 8));
     c->last_candidates = c->last_pairs = c->last_hits = c->last_ctx_pass = c->last_jobs = 0;
     if (!waf || n == 0) {
-        k_route<3><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, c->d_counters, nullptr, nblk, 0);
+        if (t.rk_keys) k_route<3, true><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, c->d_counters, nullptr, nblk, 0);
+        else k_route<3><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, c->d_counters, nullptr, nblk, 0);
         HIPCHK(c, hipGetLastError());
         return mark(1) ? GM_E_HIP : GM_OK;
     }
@@ -1109,7 +1123,9 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
                                                                      (uint32_t)c->cu_count * 8));
         const gm_req *rq = reqs + i0;
         gm_verdict *ov = out + i0;
-        if (c->route_wpe == 5)
+        if (t.rk_keys)
+            k_route<5, true><<<nb, ROUTE_BLOCK, 0, c->side>>>(rq, cnt, A, alen, t, ov, c->d_counters, b2r, nblk, prio);
+        else if (c->route_wpe == 5)
             k_route<5><<<nb, ROUTE_BLOCK, 0, c->side>>>(rq, cnt, A, alen, t, ov, c->d_counters, b2r, nblk, prio);
         else if (c->route_wpe == 6)
             k_route<6><<<nb, ROUTE_BLOCK, 0, c->side>>>(rq, cnt, A, alen, t, ov, c->d_counters, b2r, nblk, prio);

@@ -68,6 +68,10 @@ constexpr uint32_t RLOC_SEQ_MAX = 8;
 struct DRlocKey { uint32_t key; uint32_t first, count; uint32_t server; };   // key 0 = empty slot; DRlocEnt slice
 // one keyed regex: the folded factor whose window the key is, checked in full at the window
 // before the regex becomes a candidate
+// bit filter over the prefilter keys, staged into LDS by k_route: a URI window whose bit is
+// clear skips the key-table probe in L2
+constexpr uint32_t RK_BLOOM_WORDS = 1024;
+__host__ __device__ inline uint32_t rk_bloom_bit(uint32_t h) { return h >> 17; }   // 15 bits
 struct DRlocEnt { uint32_t k; uint32_t fac_off; uint16_t fac_len; int16_t key_off; };
 struct DServerIf {
     uint32_t op;             // SIF_*
@@ -206,9 +210,11 @@ struct TabHeader {
     uint32_t bloom_pk;       // packed shifts per probe (K = 2 * bloom_pk)
     uint32_t ctx_mul;        // stage-2 context filter multiplier (waf_b, see ctx_key)
     uint32_t n_rk_cap, n_rk_ids;   // regex-location prefilter: key table (pow2) and id lists
+    uint32_t n_rk_ents_keys, pad_rk;   // distinct (server, key) pairs
     uint64_t off_rk, off_rk_ids;
     uint64_t off_small;            // DSmallLoc lists
     uint64_t off_rk_ents;          // DRlocEnt lists
+    uint64_t off_rk_bloom;         // RK_BLOOM_WORDS: one bit per (server, key), top bits of rk_hash
 };
 
 struct GTab {                // device pointers, built on host from the image base
@@ -221,6 +227,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const uint8_t *bytes; const uint32_t *waf_a; const uint32_t *waf_b;
     const DLitBucket *lit_buckets; const DLit *lits; const DSigRegex *sig_regex; const uint32_t *always;
     const DRlocKey *rk; const uint32_t *rk_ids; uint32_t rk_mask; const DSmallLoc *small; const DRlocEnt *rk_ents;
+    const uint32_t *rk_bloom; uint32_t rk_keys;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
     uint32_t gen;
