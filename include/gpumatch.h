@@ -119,7 +119,9 @@ enum {
     GM_ACT_BAD_REQUEST  = 5,  /* invalid Host                                              */
     GM_ACT_BLOCK        = 6,  /* WAF block mode with >= 1 signature hit                    */
     GM_ACT_ERRPAGE      = 7,  /* error_page target empty (no split bucket) -> 302          */
-    GM_ACT_UNSUPPORTED  = 8,  /* location uses a construct the compiler rejected           */
+    GM_ACT_UNSUPPORTED  = 8,  /* location uses a construct the compiler rejected, or the   */
+                              /* regex search reached a PCRE-only regex location whose     */
+                              /* superset pattern matches: the data plane defers to nginx  */
     GM_ACT_NO_LISTENER  = 9   /* no server listens on the port / TLS on a plain port      */
 };
 
