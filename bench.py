@@ -191,8 +191,13 @@ def pmc_traffic():
     b = s.get("k_waf_scan_hbm_read_bytes_per_launch")
     if b is None:
         return {}
-    return {"traffic": b, "traffic_unit": "bytes/launch",
-            "traffic_source": os.path.relpath(files[-1], ROOT) + " (rocprofv3 --pmc FETCH_SIZE)"}
+    out = {"traffic": b, "traffic_unit": "bytes/launch",
+           "traffic_source": os.path.relpath(files[-1], ROOT) + " (rocprofv3 --pmc FETCH_SIZE)"}
+    # north_star: the LDS bank-conflict rate of the scan's Bloom probes, from the same passes
+    # (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE: conflict cycles per LDS-active cycle)
+    if s.get("k_waf_scan_lds_bank_conflict_rate") is not None:
+        out["lds_bank_conflict_rate"] = s["k_waf_scan_lds_bank_conflict_rate"]
+    return out
 
 
 def cpu_baseline(ss, gblob, preqs, parena, seconds):
