@@ -200,6 +200,16 @@ int         gm_comm_unique_id(void *out_128_bytes);
 int         gm_comm_init(gm_ctx *ctx, const void *nccl_unique_id, int nranks, int rank);
 int         gm_counters_allreduce(gm_ctx *ctx, void *stream);
 
+/* $uri normalisation of n raw request paths (nginx ngx_http_parse_complex_uri
+ * with merge_slashes on -- the step that turns the request line's path into the `$uri` every
+ * location rule matches, nginx.ingress.tmpl:96 `location {{Path}}`).  Path i is
+ * arena[off[i] .. off[i] + len[i]); '?' or '#' ends it.  The normalised bytes go to
+ * out[off[i] ..) (never longer than the input; out may equal arena) and out_len[i] = their
+ * length, or GM_NONE where nginx answers 400 (bad %-escape, NUL, ".." above the root).
+ * Device pointers; asynchronous on `stream`. */
+int         gm_normalize_uris(gm_ctx *ctx, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                              uint32_t n, uint8_t *out, uint32_t *out_len, void *stream);
+
 int         gm_stats(gm_ctx *ctx, gm_stats_t *out);
 const char *gm_last_error(gm_ctx *ctx);
 

@@ -1465,3 +1465,109 @@ extern "C" int gm_debug_server(gm_ctx *c, uint32_t sid, uint32_t *out, size_t ca
     for (uint32_t i = 0; i < S.n_rloc && k + 2 <= cap; i++) { out[k++] = rl[S.first_rloc + i].dfa; out[k++] = rl[S.first_rloc + i].loc; }
     return (int)k;
 }
+
+// ---------------------------------------------------------------------------------------------
+// $uri normalisation: nginx's ngx_http_parse_complex_uri with merge_slashes on,
+// restated as a byte state machine -- percent-decoding (a decoded byte re-enters the state that
+// saw its '%', so %2F acts as '/' and %2E as '.', except decoded '%', '#' and '?', which are
+// kept literally), merged slashes, "." and ".." segments; '?' or '#' ends the path; a bad escape,
+// a NUL or ".." above the root is a 400 (GM_NONE).  Lane per path; the output never outgrows
+// the input, so path i is written at its own arena offset.  Bound: HBM, algorithmic bytes per
+// path = its length read + its normalised length written + 16 B of (offset, length, out_len).
+namespace {
+enum : uint32_t { UN_USUAL, UN_SLASH, UN_DOT, UN_DOTDOT, UN_Q1, UN_Q2 };
+
+__device__ __forceinline__ int un_hex(uint32_t c) {
+    if (c - '0' < 10u) return (int)(c - '0');
+    c |= 0x20;
+    return c - 'a' < 6u ? (int)(c - 'a' + 10) : -1;
+}
+
+// out[0 .. u) holds "<...>/.."; drop it and the segment before it; false if that leaves the root
+__device__ __forceinline__ bool un_up(const uint8_t *out, uint32_t &u) {
+    if (u < 4) return false;
+    for (int64_t k = (int64_t)u - 4; k >= 0; k--)
+        if (out[k] == '/') { u = (uint32_t)k + 1; return true; }
+    return false;
+}
+
+// (no __restrict__: out may alias in -- the write position never passes the read position)
+__device__ uint32_t un_one(const uint8_t *in, uint32_t n, uint8_t *out) {
+    uint32_t st = UN_USUAL, qst = UN_USUAL, dec = 0, u = 0, i = 0, ch = 0;
+    bool again = false;
+    for (;;) {
+        if (!again) {
+            if (i >= n) break;
+            ch = in[i++];
+        }
+        again = false;
+        if (st == UN_Q1) {
+            const int v = un_hex(ch);
+            if (v < 0) return GM_NONE;
+            dec = (uint32_t)v; st = UN_Q2;
+            continue;
+        }
+        if (st == UN_Q2) {
+            const int v = un_hex(ch);
+            if (v < 0) return GM_NONE;
+            ch = dec << 4 | (uint32_t)v;
+            if (v < 10 ? (ch == '%' || ch == '#') : ch == '?') { out[u++] = (uint8_t)ch; st = UN_USUAL; continue; }
+            if (ch == 0) return GM_NONE;
+            st = qst; again = true;
+            continue;
+        }
+        if (ch == 0) return GM_NONE;
+        if (ch == '?' || ch == '#') break;
+        if (ch == '%') { qst = st; st = UN_Q1; continue; }
+        switch (st) {
+        case UN_USUAL:
+            out[u++] = (uint8_t)ch;
+            if (ch == '/') st = UN_SLASH;
+            break;
+        case UN_SLASH:
+            if (ch == '/') break;
+            out[u++] = (uint8_t)ch;
+            st = ch == '.' ? UN_DOT : UN_USUAL;
+            break;
+        case UN_DOT:
+            if (ch == '/') { u--; st = UN_SLASH; break; }
+            out[u++] = (uint8_t)ch;
+            st = ch == '.' ? UN_DOTDOT : UN_USUAL;
+            break;
+        default:   // UN_DOTDOT
+            if (ch == '/') {
+                if (!un_up(out, u)) return GM_NONE;
+                st = UN_SLASH;
+                break;
+            }
+            out[u++] = (uint8_t)ch;
+            st = UN_USUAL;
+            break;
+        }
+    }
+    if (st == UN_Q1 || st == UN_Q2) return GM_NONE;
+    if (st == UN_DOT) u--;
+    else if (st == UN_DOTDOT && !un_up(out, u)) return GM_NONE;
+    return u;
+}
+
+__global__ __launch_bounds__(256) void k_uri_normalize(const uint8_t *A, const uint64_t *__restrict__ off,
+                                                        const uint32_t *__restrict__ len, uint32_t n,
+                                                        uint8_t *out, uint32_t *__restrict__ out_len) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        out_len[i] = un_one(A + off[i], len[i], out + off[i]);
+}
+}  // namespace
+
+extern "C" int gm_normalize_uris(gm_ctx *c, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                                 uint32_t n, uint8_t *out, uint32_t *out_len, void *stream) {
+    if (!c) return fail(c, GM_E_INVAL, "null ctx");
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
+    if (n == 0) return GM_OK;
+    if (!arena || !off || !len || !out || !out_len) return fail(c, GM_E_INVAL, "null argument");
+    HIPCHK(c, hipSetDevice(c->dev));
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 16));
+    k_uri_normalize<<<blocks, 256, 0, (hipStream_t)stream>>>(arena, off, len, n, out, out_len);
+    HIPCHK(c, hipGetLastError());
+    return GM_OK;
+}

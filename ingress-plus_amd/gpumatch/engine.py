@@ -49,7 +49,7 @@ class GmBatch(ctypes.Structure):
 
 EXPORTS = ["gm_create", "gm_destroy", "gm_abi_version", "gm_load_generation", "gm_match_batch", "gm_sync",
            "gm_counters", "gm_counters_reset", "gm_comm_unique_id", "gm_comm_init", "gm_counters_allreduce",
-           "gm_stats", "gm_last_error"]
+           "gm_stats", "gm_last_error", "gm_normalize_uris"]
 
 _lib = None
 
@@ -74,6 +74,8 @@ def lib():
         L.gm_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         L.gm_counters_allreduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.gm_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(GmStats)]
+        L.gm_normalize_uris.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.gm_last_error.restype = ctypes.c_char_p
         L.gm_last_error.argtypes = [ctypes.c_void_p]
         _lib = L
@@ -141,6 +143,10 @@ class Engine:
         self.sync(0)
         total = self.stats()["last_hits"]
         return out, hits[:total]
+
+    def normalize_uris_ptr(self, arena_ptr, off_ptr, len_ptr, n, out_ptr, out_len_ptr, stream=0):
+        """gm_normalize_uris on device pointers (nginx $uri normalisation, include/gpumatch.h)."""
+        self._chk(lib().gm_normalize_uris(self.h, arena_ptr, off_ptr, len_ptr, n, out_ptr, out_len_ptr, stream))
 
     def match_torch(self, reqs_t, arena_t, arena_len: int, out_t, hits_t, stream=None):
         """Device tensors (torch.uint8 / structured views) -> verdicts in out_t (async)."""

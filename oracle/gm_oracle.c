@@ -1202,3 +1202,82 @@ int orc_pcre_match(const char *pat, int caseless, const char *subj, int n) {
     int m = pcre_exec(r, NULL, subj, n, 0, 0, ov, 30);
     return m >= 0 ? 1 : 0;
 }
+
+/* ------------------------------------------------------------------------------------------
+ * $uri normalisation oracle.  Restates nginx 1.17.3
+ * src/http/ngx_http_parse.c ngx_http_parse_complex_uri() with merge_slashes on (the nginx
+ * source is not in /root/reference; the reference renders `location {{Path}}`,
+ * nginx.ingress.tmpl:96, and nginx matches those paths against this normalised $uri).
+ * Parity unpinned: no reference test fixes these bytes; the hand vectors in tests/test_uri.py
+ * restate nginx's documented behaviour.  Returns the normalised length, or -1 (nginx 400).
+ * Test infrastructure only. */
+enum { ON_USUAL, ON_SLASH, ON_DOT, ON_DOTDOT, ON_Q1, ON_Q2 };
+
+static int on_hex(int c, int *v) {
+    if (c >= '0' && c <= '9') { *v = c - '0'; return 1; }
+    c |= 0x20;
+    if (c >= 'a' && c <= 'f') { *v = c - 'a' + 10; return 2; }
+    return 0;
+}
+
+/* "..": u points just past "/.."; back up over it and the previous segment (nginx u -= 4 loop) */
+static int on_up(const uint8_t *o, int64_t *u) {
+    int64_t k = *u - 4;
+    for (;;) {
+        if (k < 0) return 0;
+        if (o[k] == '/') { *u = k + 1; return 1; }
+        k--;
+    }
+}
+
+int64_t orc_normalize_uri(const uint8_t *p, uint32_t n, uint8_t *o) {
+    int state = ON_USUAL, quoted_state = ON_USUAL, hi = 0, v, kind;
+    int64_t u = 0;
+    uint32_t i = 0;
+    int ch;
+    while (i < n) {
+        ch = p[i++];
+    dispatch:
+        switch (state) {
+        case ON_Q1:
+            if (!on_hex(ch, &v)) return -1;
+            hi = v; state = ON_Q2;
+            continue;
+        case ON_Q2:
+            kind = on_hex(ch, &v);
+            if (!kind) return -1;
+            ch = hi * 16 + v;
+            if (kind == 1 && (ch == '%' || ch == '#')) { o[u++] = (uint8_t)ch; state = ON_USUAL; continue; }
+            if (kind == 1 && ch == 0) return -1;
+            if (kind == 2 && ch == '?') { o[u++] = (uint8_t)ch; state = ON_USUAL; continue; }
+            state = quoted_state;
+            goto dispatch;
+        default:
+            break;
+        }
+        if (ch == 0) return -1;
+        if (ch == '?' || ch == '#') goto done;
+        if (ch == '%') { quoted_state = state; state = ON_Q1; continue; }
+        if (state == ON_USUAL) {
+            o[u++] = (uint8_t)ch;
+            if (ch == '/') state = ON_SLASH;
+        } else if (state == ON_SLASH) {
+            if (ch == '/') continue;                 /* merge_slashes */
+            o[u++] = (uint8_t)ch;
+            state = ch == '.' ? ON_DOT : ON_USUAL;
+        } else if (state == ON_DOT) {
+            if (ch == '/') { u--; state = ON_SLASH; continue; }
+            o[u++] = (uint8_t)ch;
+            state = ch == '.' ? ON_DOTDOT : ON_USUAL;
+        } else {                                      /* ON_DOTDOT */
+            if (ch == '/') { if (!on_up(o, &u)) return -1; state = ON_SLASH; continue; }
+            o[u++] = (uint8_t)ch;
+            state = ON_USUAL;
+        }
+    }
+done:
+    if (state == ON_Q1 || state == ON_Q2) return -1;
+    if (state == ON_DOT) u--;
+    else if (state == ON_DOTDOT && !on_up(o, &u)) return -1;
+    return u;
+}
