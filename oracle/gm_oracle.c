@@ -1281,3 +1281,13 @@ done:
     else if (state == ON_DOTDOT && !on_up(o, &u)) return -1;
     return u;
 }
+
+/* batch form of orc_normalize_uri (CPU baseline of gm_normalize_uris, one thread); out_len[i] =
+ * 0xFFFFFFFF for a 400.  Test / baseline infrastructure only. */
+void orc_normalize_batch(const uint8_t *arena, const uint64_t *off, const uint32_t *len, uint32_t n,
+                         uint8_t *out, uint32_t *out_len) {
+    for (uint32_t i = 0; i < n; i++) {
+        int64_t r = orc_normalize_uri(arena + off[i], len[i], out + off[i]);
+        out_len[i] = r < 0 ? 0xFFFFFFFFu : (uint32_t)r;
+    }
+}

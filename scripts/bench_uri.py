@@ -52,12 +52,28 @@ def main(n_total=10_000_000, pool=200_000, steps=10, warmup=2):
     wall = time.perf_counter() - t0
     ms = e0.elapsed_time(e1) / steps
     olen = ol.cpu().numpy().view(np.uint32)
+    # CPU baseline: the oracle's batch restatement on one host thread over the first pool copy
+    import ctypes
+    from oracle_py import lib as orc_lib
+    L = orc_lib()
+    L.orc_normalize_batch.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_uint32] + [ctypes.c_void_p] * 2
+    cpu_out = np.empty(int(offs[pool - 1]) + int(lens[pool - 1]), np.uint8)
+    cpu_len = np.empty(pool, np.uint32)
+    reps_cpu, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < 3.0:
+        L.orc_normalize_batch(arena.ctypes.data, offs.ctypes.data, lens.ctypes.data, pool, cpu_out.ctypes.data,
+                              cpu_len.ctypes.data)
+        reps_cpu += 1
+    cpu_rate = reps_cpu * pool / (time.perf_counter() - t1)
+    assert np.array_equal(cpu_len, olen[:pool]), "GPU and CPU oracle disagree"
     out_bytes = int(olen[olen != 0xFFFFFFFF].astype(np.uint64).sum())
     algo = int(lens.astype(np.uint64).sum()) + out_bytes + 16 * n
     print(json.dumps({"metric": "paths/sec ($uri normalisation)", "value": n / (ms * 1e-3), "unit": "paths/s",
                       "ms_per_launch": ms, "paths": n, "mean_len": float(lens.mean()),
                       "algorithmic_GBps": algo / (ms * 1e-3) / 1e9, "hbm_frac": algo / (ms * 1e-3) / 8e12,
-                      "invalid_frac": float((olen == 0xFFFFFFFF).mean()), "wall_s": wall}))
+                      "invalid_frac": float((olen == 0xFFFFFFFF).mean()), "wall_s": wall,
+                      "cpu_baseline": {"value": cpu_rate, "unit": "paths/s", "cores": 1, "kind": "port",
+                                       "sample": f"{reps_cpu} passes over the {pool}-path pool (~3 s)"}}))
 
 
 if __name__ == "__main__":
