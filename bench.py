@@ -54,9 +54,8 @@ def main():
 
     # ---- generation: C4 signature set on the cafe Ingress, wallarm mode block
     t0 = time.time()
-    ss = workloads.c4_sigset()
     # benign traffic sample (disjoint seed) for the prefilter's key / hash choice (GM_ENTRY_SAMPLE)
-    gblob = workloads.c4_blob(ss, "block", sample=workloads.c4_sample(ss))
+    ss, gblob = workloads.c4_bench_generation()
     eng = engine.Engine(local, profile=True)
     eng.load(gblob, 1)
     st = eng.stats()
@@ -66,20 +65,14 @@ def main():
     # ---- synthetic requests: a P-request pool, replicated to R requests in HBM
     t0 = time.time()
     pool_n = min(args.pool, args.requests)
-    preqs, parena = records.gen_c4(pool_n, ss, seed=records.SEED_BASE + 3)
-    plen = (len(parena) + 15) & ~15
-    reps = (args.requests + pool_n - 1) // pool_n
+    preqs, parena = records.gen_c4(pool_n, ss, seed=workloads.C4_POOL_SEED)
     n = args.requests
+    reqs, plen, reps, arena_len = workloads.replicate_pool(preqs, len(parena), n)
     log(f"[rank {rank}] pool {pool_n} requests / {len(parena) / 1e9:.2f} GB generated in {time.time() - t0:.1f}s; "
         f"x{reps} -> {n} requests")
-    reqs = np.tile(preqs, reps)[:n]
-    reqs["base"] += (np.repeat(np.arange(reps, dtype=np.uint64), pool_n)[:n] * np.uint64(plen))
-    arena_len = int(reqs["base"][-1]) + int(sum(int(reqs[-1][f]) for f in
-                                                ("uri_len", "args_len", "hdr_len", "body_len", "host_len",
-                                                 "method_len", "ruri_len", "raddr_len")))
     dev = torch.device("cuda", local)
     d_pool = torch.from_numpy(np.ascontiguousarray(parena)).to(dev)
-    d_arena = torch.empty(reps * plen + 1024, dtype=torch.uint8, device=dev)
+    d_arena = torch.zeros(reps * plen + 1024, dtype=torch.uint8, device=dev)
     for k in range(reps):
         d_arena[k * plen:k * plen + len(parena)].copy_(d_pool)
     del d_pool
@@ -102,9 +95,9 @@ def main():
     def step():
         eng.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), arena_len, n, d_out.data_ptr(), d_hits.data_ptr(),
                       hit_cap, stream.cuda_stream)
-        eng.sync(stream.cuda_stream)
-        if world > 1:
+        if world > 1:   # job-wide counter totals (out of place: local counters stay cumulative)
             eng.counters_allreduce(stream.cuda_stream)
+        eng.sync(stream.cuda_stream)
 
     for w in range(args.warmup):
         step()
@@ -178,21 +171,32 @@ def main():
     print(json.dumps(result), flush=True)
 
 
+# The PMC summary of this bench's C4 scan (scripts/pmc.sh on the same tree; bumped with each
+# re-profile).  Selected by name -- never "the newest *pmc_summary.json", which may belong to
+# another kernel's profile.
+PMC_SUMMARY = "profiles/r2_pmc_summary.json"
+
+
 def pmc_traffic():
     """HBM read bytes per k_waf_scan launch from the committed PMC pass of this workload
     (scripts/pmc.sh: a separate `rocprofv3 --pmc FETCH_SIZE` run of this bench, FETCH_SIZE x 2 x
     1024 per the gfx950 correction in MI355X_MICROARCH.md).  Counters cannot be read from inside
     the timed run, so the value is the profiled one, named with its source file."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
-    if not files:
-        return {}
-    s = json.load(open(files[-1]))
+    path = os.path.join(ROOT, PMC_SUMMARY)
+    if not os.path.exists(path):
+        # fall back to the newest round's summary that carries the scan's bytes
+        import glob
+        cands = [p for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
+                 if "k_waf_scan_hbm_read_bytes_per_launch" in json.load(open(p))]
+        if not cands:
+            return {}
+        path = cands[-1]
+    s = json.load(open(path))
     b = s.get("k_waf_scan_hbm_read_bytes_per_launch")
     if b is None:
         return {}
     out = {"traffic": b, "traffic_unit": "bytes/launch",
-           "traffic_source": os.path.relpath(files[-1], ROOT) + " (rocprofv3 --pmc FETCH_SIZE)"}
+           "traffic_source": os.path.relpath(path, ROOT) + " (rocprofv3 --pmc FETCH_SIZE)"}
     # north_star: the LDS bank-conflict rate of the scan's Bloom probes, from the same passes
     # (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE: conflict cycles per LDS-active cycle)
     if s.get("k_waf_scan_lds_bank_conflict_rate") is not None:

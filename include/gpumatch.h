@@ -158,11 +158,11 @@ typedef struct gm_stats_t {
     uint64_t table_bytes;         /* device table bytes of the generation               */
     uint64_t lds_bytes_scan;      /* LDS bytes the WAF scan stage stages per workgroup  */
     uint64_t last_candidates;     /* WAF prefilter candidates in the last batch         */
-    uint64_t last_pairs;          /* (request, rule) hits before dedupe, last batch     */
+    uint64_t last_pairs;          /* unique (request, rule) hits of scanning requests   */
     uint64_t last_hits;           /* hit ids written, last batch                        */
-    /* GM_CREATE_PROFILE contexts: HIP-event times (ms) of the last batch's stages, on the
-     * caller's stream: route kernel, WAF scan kernel, verify kernel, and everything after it
-     * (regex confirm, sorts, hit emission, incl. the mid-batch host reads of counts). */
+    /* GM_CREATE_PROFILE contexts: HIP-event times (ms) of the last synced batch's stages: route
+     * kernel (side stream), WAF scan kernel, context filter + exact check, and everything after
+     * it (regex confirm, hit emission). */
     float    last_ms_route, last_ms_scan, last_ms_verify, last_ms_tail;
     /* WAF prefilter shape: key windows in the Bloom filter, probes per window (K = 2 * pk bits),
      * and the modelled false-positive weight per probed window (ppm) the compiler chose on. */
@@ -182,23 +182,37 @@ uint32_t    gm_abi_version(void);
  * live; rejected rules are counted (gm_stats), never returned as an error. */
 int         gm_load_generation(gm_ctx *ctx, const void *blob, size_t len, uint32_t gen);
 
-/* Classify a batch.  Asynchronous on `stream` (hipStream_t; NULL = legacy default stream);
- * out[i] receives the verdict of reqs[i]; the hit ids of request i are
- * hit_ids[out[i].first_hit_off .. + n_hits), ascending.  gm_sync() completes the batch and
- * reports capacity overflow. */
+/* Classify a batch.  Asynchronous on `stream` (hipStream_t; NULL = legacy default stream): the
+ * call enqueues every stage and returns without waiting for the device (no host round trip for
+ * intermediate counts -- they stay in device status words).  out[i] receives the verdict of
+ * reqs[i]; the hit ids of request i are hit_ids[out[i].first_hit_off .. + n_hits), ascending,
+ * requests in order.  gm_sync(ctx, stream) completes the stream's last batch and reports
+ * capacity overflow (GM_E_OVERFLOW: the batch's verdicts are void).
+ * Thread-safe per (ctx, stream) pair: each stream has its own scratch buffers, so batches on
+ * different streams may be enqueued from different threads and run concurrently.  A scratch
+ * buffer that a batch outgrows is replaced after its stream drains (the first large batches).
+ * Replaces the nginx worker's per-request classification (SURVEY.md §8 a): host/server
+ * (nginx.ingress.tmpl:53), location (nginx.ingress.tmpl:96), map / split_clients
+ * (nginx.virtualserver.tmpl:17-31), the Wallarm access phase (nginx.ingress.tmpl:12-29). */
 int         gm_match_batch(gm_ctx *ctx, const gm_batch *in, gm_verdict *out,
                            uint32_t *hit_ids, size_t hit_cap, void *stream);
 int         gm_sync(gm_ctx *ctx, void *stream);
 
-/* Per-location and per-signature hit counters, u64: [0, n_locations) locations,
- * [n_locations, n_locations + n_sigs) signatures (gm_stats_t.n_counters entries). */
+/* Per-location and per-signature hit counters of this device, u64, cumulative since the
+ * generation was loaded (or gm_counters_reset): [0, n_locations) locations,
+ * [n_locations, n_locations + n_sigs) signatures (gm_stats_t.n_counters entries).  The analogue
+ * of the reference's monotonic Prometheus counters (internal/metrics/collectors/manager.go:27-59). */
 int         gm_counters(gm_ctx *ctx, uint64_t *out, size_t n);
 int         gm_counters_reset(gm_ctx *ctx);
 
 /* Multi-GPU: ncclUniqueId (128 bytes) produced by rank 0 and shared by the caller. */
 int         gm_comm_unique_id(void *out_128_bytes);
 int         gm_comm_init(gm_ctx *ctx, const void *nccl_unique_id, int nranks, int rank);
+/* Sum of every rank's cumulative counters (RCCL all-reduce over xGMI, enqueued on `stream`),
+ * OUT OF PLACE: the local counters are untouched, so any number of calls give the true job
+ * totals.  gm_counters_global() reads the result of the last call. */
 int         gm_counters_allreduce(gm_ctx *ctx, void *stream);
+int         gm_counters_global(gm_ctx *ctx, uint64_t *out, size_t n);
 
 /* $uri normalisation of n raw request paths (nginx ngx_http_parse_complex_uri
  * with merge_slashes on -- the step that turns the request line's path into the `$uri` every
@@ -206,11 +220,13 @@ int         gm_counters_allreduce(gm_ctx *ctx, void *stream);
  * arena[off[i] .. off[i] + len[i]); '?' or '#' ends it.  The normalised bytes go to
  * out[off[i] ..) (never longer than the input; out may equal arena) and out_len[i] = their
  * length, or GM_NONE where nginx answers 400 (bad %-escape, NUL, ".." above the root).
- * Device pointers; asynchronous on `stream`. */
+ * Device pointers; asynchronous on `stream`; gm_sync(ctx, stream) completes it (the call clears
+ * the stream's batch status, so the sync reports no match-batch overflow). */
 int         gm_normalize_uris(gm_ctx *ctx, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                               uint32_t n, uint8_t *out, uint32_t *out_len, void *stream);
 
 int         gm_stats(gm_ctx *ctx, gm_stats_t *out);
+/* Message of the calling thread's last failing call (thread-local; ctx is not consulted). */
 const char *gm_last_error(gm_ctx *ctx);
 
 #ifdef __cplusplus

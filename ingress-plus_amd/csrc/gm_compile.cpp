@@ -188,7 +188,9 @@ struct Builder {
         for (const Dir &k : d.body) {
             if (k.a.empty()) continue;
             const std::string &n = k.a[0];
-            if (n == "proxy_pass" && k.a.size() == 2) {
+            // grpc_pass (nginx.org/grpc-services, version1/nginx.ingress.tmpl:154-158) proxies like
+            // proxy_pass, auto_redirect included (ngx_http_grpc_module sets clcf->auto_redirect)
+            if ((n == "proxy_pass" || n == "grpc_pass") && k.a.size() == 2) {
                 std::string u = k.a[1];
                 size_t p = u.find("://");
                 u = p == std::string::npos ? u : u.substr(p + 3);
@@ -258,6 +260,11 @@ struct Builder {
             } else if (n == "return" && k.a.size() >= 2) {
                 SIf f; f.ret_only = true;
                 f.code = isdigit((unsigned char)k.a[1][0]) ? atoi(k.a[1].c_str()) : 302;
+                S.ifs.push_back(f);
+            } else if (n == "rewrite") {
+                // server-level rewrite (server snippets): not compiled -- a request reaching it
+                // in the server rewrite phase defers to nginx (GM_ACT_UNSUPPORTED), counted
+                SIf f; f.var = "$uri"; f.op = -1;
                 S.ifs.push_back(f);
             } else if (n == "location" && k.block) {
                 location(S, k);

@@ -20,7 +20,10 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <vector>
 
@@ -819,7 +822,8 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
                                                        const uint8_t *__restrict__ A, uint64_t arena_len,
                                                        GTab t, gm_verdict *__restrict__ out,
                                                        unsigned long long *__restrict__ counters,
-                                                       uint32_t *__restrict__ blk2rec, uint32_t nblk, int prio) {
+                                                       uint32_t *__restrict__ blk2rec, uint32_t nblk,
+                                                       uint32_t *__restrict__ hcnt, int prio) {
     // beside the WAF scan: issue priority over the scan's waves, so the route's short
     // latency-bound waves finish early instead of stretching past the scan (GM_ROUTE_PRIO)
     if (prio) __builtin_amdgcn_s_setprio(2);
@@ -854,6 +858,10 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
             }
             todo &= ~same;
         }
+        if (hcnt) {   // the WAF stages' per-request hit counts start the batch at zero
+            hcnt[i] = 0;
+            if (i + 1 == n) hcnt[n] = 0;
+        }
         if (blk2rec) {
             // blocks whose start lies in [base_i, base_{i+1}) belong to record i
             uint64_t b0 = (i == 0) ? 0 : r.base;
@@ -871,82 +879,86 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
     }
 }
 
-// blk2rec alone (k_waf_exact's record lookup), when k_route runs after the scan
-__global__ __launch_bounds__(256) void k_blk2rec(const gm_req *__restrict__ reqs, uint32_t n, uint64_t arena_len,
-                                                 uint32_t *__restrict__ blk2rec, uint32_t nblk) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        // blocks whose start lies in [base_i, base_{i+1}) belong to record i
-        const uint64_t b0 = (i == 0) ? 0 : reqs[i].base;
-        const uint64_t b1 = (i + 1 < n) ? reqs[i + 1].base : arena_len;
-        const uint64_t k0 = (b0 + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
-        uint64_t k1 = (b1 + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
-        if (i + 1 == n) k1 = nblk;
-        for (uint64_t k = k0; k < k1 && k < nblk; k++) blk2rec[k] = i;
-    }
-}
-
 #include "gm_waf.inc"
 
 }  // namespace
 
 // ============================================================================ host runtime
+// A generation owns its device image and its counters (the counter space is the generation's
+// locations + signatures): gm_load_generation builds the next one beside the live one and swaps
+// under an exclusive lock; batches read `gen` under a shared lock for as long as they enqueue.
 struct Generation {
     uint8_t *d_image = nullptr;
+    unsigned long long *d_counters = nullptr;       // this device's cumulative counters
+    unsigned long long *d_counters_sum = nullptr;   // gm_counters_allreduce's out-of-place result
+    size_t n_counters = 0;
     TabHeader hdr{};
     GTab tab{};
     gm_stats_t stats{};
     std::vector<uint8_t> host_image;   // kept for host-side introspection (gpumatch_debug.h)
+    ~Generation() {
+        for (void *p : {(void *)d_image, (void *)d_counters, (void *)d_counters_sum})
+            if (p) (void)hipFree(p);
+    }
+};
+
+// Everything one batch writes, per (ctx, stream): batches on different streams never share a
+// buffer, so gm_match_batch is thread-safe per ctx + stream pair without a ctx-wide lock.
+struct Scratch {
+    hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;               // k_route beside the WAF scan
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev[5] = {}, ev_route[2] = {};  // GM_CREATE_PROFILE stage events
+    bool ev_pending = false, route_side = false;
+    int ev_used = 0;
+    uint32_t *d_status = nullptr, *h_status = nullptr;
+    uint32_t *d_blk2rec = nullptr; size_t cap_blk = 0;
+    unsigned long long *d_cand = nullptr; size_t cap_cand = 0;
+    unsigned long long *d_surv = nullptr; size_t cap_surv = 0;   // stage-2 survivors (arena offsets)
+    unsigned long long *d_pairs = nullptr; size_t cap_pairs = 0; // unique active (request, rule) pairs
+    unsigned long long *d_jobs = nullptr; size_t cap_jobs = 0;   // unique (request, regex, zone) jobs
+    unsigned long long *d_set = nullptr; size_t cap_set = 0;     // dedupe set (power of two)
+    uint32_t epoch = 0;                                          // dedupe epoch of the last batch
+    uint32_t *d_cnt = nullptr, *d_start = nullptr; size_t cap_cnt = 0, cap_start = 0;
+    uint32_t *d_ccnt = nullptr; size_t cap_ccnt = 0;
+    uint8_t *d_temp = nullptr; size_t cap_temp = 0;
+    uint8_t *d_stage = nullptr; size_t cap_stage = 0;            // GM_BATCH_HOST staging
+    ~Scratch() {
+        for (void *p : {(void *)d_status, (void *)d_blk2rec, (void *)d_cand, (void *)d_surv, (void *)d_pairs,
+                        (void *)d_jobs, (void *)d_set, (void *)d_cnt, (void *)d_start, (void *)d_ccnt,
+                        (void *)d_temp, (void *)d_stage})
+            if (p) (void)hipFree(p);
+        if (h_status) (void)hipHostFree(h_status);
+        for (auto &e : ev) if (e) (void)hipEventDestroy(e);
+        for (auto &e : ev_route) if (e) (void)hipEventDestroy(e);
+        if (ev_fork) (void)hipEventDestroy(ev_fork);
+        if (ev_join) (void)hipEventDestroy(ev_join);
+        if (side) (void)hipStreamDestroy(side);
+    }
 };
 
 struct gm_ctx {
     int dev = 0;
     uint32_t flags = 0;
-    Generation *gen = nullptr;
-    std::string err;
-    unsigned long long *d_counters = nullptr;
-    size_t n_counters = 0;
-    uint32_t *d_status = nullptr, *h_status = nullptr;
-    uint32_t *d_blk2rec = nullptr; size_t cap_blk = 0;
-    unsigned long long *d_cand = nullptr; size_t cap_cand = 0;
-    unsigned long long *d_surv = nullptr; size_t cap_surv = 0;   // stage-2 survivors (arena offsets)
-    unsigned long long *d_pairs = nullptr, *d_pairs2 = nullptr; size_t cap_pairs = 0;
-    unsigned long long *d_jobs = nullptr, *d_jobs2 = nullptr; size_t cap_jobs = 0;
-    uint32_t *d_keep = nullptr, *d_idx = nullptr; size_t cap_keep = 0, cap_idx = 0;
-    uint32_t *d_ccnt = nullptr; size_t cap_ccnt = 0;
-    uint8_t *d_temp = nullptr; size_t cap_temp = 0;
-    // host-staging (GM_BATCH_HOST)
-    uint8_t *d_stage = nullptr; size_t cap_stage = 0;
-    ncclComm_t comm = nullptr;
-    uint64_t last_candidates = 0, last_pairs = 0, last_hits = 0, last_ctx_pass = 0, last_jobs = 0;
-    hipEvent_t ev[5] = {};
-    hipEvent_t ev_route[2] = {};   // GM_CREATE_PROFILE: route kernel on the side stream
-    // side stream: k_route runs beside the WAF scan (independent inputs) and joins before the
-    // exact check, which needs its blk2rec map
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_blk = nullptr, ev_scan = nullptr;
-    int route_prio = 1;            // k_route beside the scan at raised issue priority (GM_ROUTE_PRIO)
-    int route_mode = 0;            // 0: route beside the scan, 1: after it, 2: split (GM_ROUTE_MODE tuning knob)
-    int route_split = 60;          // mode 2: percent of the requests routed beside the scan (GM_ROUTE_SPLIT)
-    bool ev_pending = false;
-    int ev_used = 0;
-    float last_ms[4] = {0, 0, 0, 0};
-    bool route_side = false;   // last batch ran k_route on the side stream
     int cu_count = 256;
-    int scan_depth = SCAN_DEPTH;   // chunks in flight per scan wave (GM_SCAN_DEPTH tuning knob)
-    // scan records staged in LDS and written in whole slices (1) or stored directly (0): staging
-    // makes the scan 0.7 ms shorter per 10M C4 requests, but k_route beside it then gets fewer
-    // issue slots and finishes later than the scan -- direct stores stay the default until
-    // the route's critical path is shorter (GM_SCAN_STAGE tuning knob)
-    int scan_stage = 0;
-    int route_wpe = 5;             // k_route register target, waves per SIMD (GM_ROUTE_WPE tuning knob)
-    std::mutex mu;
+    std::shared_mutex gen_mu;                 // shared: enqueueing batches; exclusive: the swap
+    Generation *gen = nullptr;
+    std::mutex scr_mu;                        // the stream -> scratch map only
+    std::map<hipStream_t, std::unique_ptr<Scratch>> scratch;
+    ncclComm_t comm = nullptr;
+    // last completed batch (gm_sync), for gm_stats / gm_debug_status
+    std::mutex last_mu;
+    uint64_t last_candidates = 0, last_pairs = 0, last_hits = 0, last_ctx_pass = 0, last_jobs = 0;
+    float last_ms[4] = {0, 0, 0, 0};
+    uint32_t last_status[STATUS_WORDS] = {};
 };
 
+// gm_last_error() is thread-local (include/gpumatch.h): concurrent callers on one ctx never see
+// each other's messages
 static thread_local std::string t_err;
 
-static int fail(gm_ctx *c, int code, const std::string &m) {
+static int fail(gm_ctx *, int code, const std::string &m) {
     t_err = m;
-    if (c) c->err = m;
     return code;
 }
 #define HIPCHK(c, x)                                                                         \
@@ -955,15 +967,47 @@ static int fail(gm_ctx *c, int code, const std::string &m) {
         if (e_ != hipSuccess) return fail((c), GM_E_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
     } while (0)
 
+// grow a scratch buffer of stream s: work already enqueued on s may still read the old one, so
+// the stream drains first (only when a batch outgrows the buffer, i.e. the first large batches)
 template <class T>
-static int grow(gm_ctx *c, T *&p, size_t &cap, size_t need) {
+static int grow(gm_ctx *c, hipStream_t s, T *&p, size_t &cap, size_t need) {
     if (need <= cap) return GM_OK;
-    if (p) HIPCHK(c, hipFree(p));
+    if (p) {
+        HIPCHK(c, hipStreamSynchronize(s));
+        HIPCHK(c, hipFree(p));
+    }
     p = nullptr;
-    size_t nc = std::max(need, cap + cap / 2);
+    cap = 0;
+    const size_t nc = need + need / 4;
     HIPCHK(c, hipMalloc((void **)&p, nc * sizeof(T)));
     cap = nc;
     return GM_OK;
+}
+
+// the scratch of `stream`, created on first use (with its side stream, events and status words)
+static Scratch *scratch_for(gm_ctx *c, hipStream_t stream) {
+    std::lock_guard<std::mutex> lk(c->scr_mu);
+    auto it = c->scratch.find(stream);
+    if (it != c->scratch.end()) return it->second.get();
+    std::unique_ptr<Scratch> s(new Scratch());
+    s->stream = stream;
+    if (hipMalloc((void **)&s->d_status, STATUS_WORDS * 4) != hipSuccess ||
+        hipHostMalloc((void **)&s->h_status, STATUS_WORDS * 4, hipHostMallocDefault) != hipSuccess ||
+        hipMemset(s->d_status, 0, STATUS_WORDS * 4) != hipSuccess ||
+        hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess) {
+        t_err = "scratch allocation failed";
+        return nullptr;
+    }
+    memset(s->h_status, 0, STATUS_WORDS * 4);
+    if (c->flags & GM_CREATE_PROFILE) {
+        for (auto &e : s->ev) if (hipEventCreate(&e) != hipSuccess) { t_err = "event create failed"; return nullptr; }
+        for (auto &e : s->ev_route) if (hipEventCreate(&e) != hipSuccess) { t_err = "event create failed"; return nullptr; }
+    }
+    Scratch *p = s.get();
+    c->scratch.emplace(stream, std::move(s));
+    return p;
 }
 
 extern "C" {
@@ -979,27 +1023,6 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
             c->cu_count = cus;
-        if (const char *ev = getenv("GM_SCAN_DEPTH")) c->scan_depth = atoi(ev);
-        if (const char *ev = getenv("GM_SCAN_STAGE")) c->scan_stage = atoi(ev);
-        if (const char *ev = getenv("GM_ROUTE_WPE")) c->route_wpe = atoi(ev);
-        if (const char *ev = getenv("GM_ROUTE_MODE")) c->route_mode = atoi(ev);
-        if (const char *ev = getenv("GM_ROUTE_SPLIT")) c->route_split = std::min(100, std::max(0, atoi(ev)));
-        if (const char *ev = getenv("GM_ROUTE_PRIO")) c->route_prio = atoi(ev);
-        if (hipMalloc((void **)&c->d_status, STATUS_WORDS * 4) != hipSuccess ||
-            hipHostMalloc((void **)&c->h_status, STATUS_WORDS * 4, hipHostMallocDefault) != hipSuccess) {
-            t_err = "status alloc failed"; delete c; return nullptr;
-        }
-        if (flags & GM_CREATE_PROFILE) {
-            for (auto &e : c->ev) (void)hipEventCreate(&e);
-            for (auto &e : c->ev_route) (void)hipEventCreate(&e);
-        }
-        if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ev_blk, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming) != hipSuccess) {
-            t_err = "stream/event create failed"; delete c; return nullptr;
-        }
     }
     return c;
 }
@@ -1009,34 +1032,22 @@ void gm_destroy(gm_ctx *c) {
     if (!(c->flags & GM_CREATE_COMPILE_ONLY)) {
         (void)hipSetDevice(c->dev);
         (void)hipDeviceSynchronize();
-        if (c->gen) (void)hipFree(c->gen->d_image);
-        for (void *p : {(void *)c->d_counters, (void *)c->d_status, (void *)c->d_blk2rec, (void *)c->d_cand, (void *)c->d_surv,
-                        (void *)c->d_pairs, (void *)c->d_pairs2, (void *)c->d_jobs, (void *)c->d_jobs2,
-                        (void *)c->d_keep, (void *)c->d_idx, (void *)c->d_temp, (void *)c->d_stage,
-                        (void *)c->d_ccnt})
-            if (p) (void)hipFree(p);
-        if (c->h_status) (void)hipHostFree(c->h_status);
+        c->scratch.clear();
         if (c->comm) ncclCommDestroy(c->comm);
-        for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
-        for (auto &e : c->ev_route) if (e) (void)hipEventDestroy(e);
-        if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-        if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-        if (c->ev_blk) (void)hipEventDestroy(c->ev_blk);
-        if (c->ev_scan) (void)hipEventDestroy(c->ev_scan);
-        if (c->side) (void)hipStreamDestroy(c->side);
     }
     delete c->gen;
     delete c;
 }
 
-const char *gm_last_error(gm_ctx *c) { return c ? c->err.c_str() : t_err.c_str(); }
+const char *gm_last_error(gm_ctx *) { return t_err.c_str(); }
 
 int gm_load_generation(gm_ctx *c, const void *blob, size_t len, uint32_t gen) {
     if (!c || !blob) return fail(c, GM_E_INVAL, "null argument");
-    std::lock_guard<std::mutex> lk(c->mu);
     CompileResult R = compile_generation((const uint8_t *)blob, len, gen);
     if (!R.ok) return fail(c, R.code, R.err);   // previous generation stays live
-    Generation *g = new Generation();
+    if (R.stats.n_sigs >= (1u << 21) || R.stats.n_sig_regex >= (1u << 21))
+        return fail(c, GM_E_INVAL, "more than 2^21 signatures");
+    std::unique_ptr<Generation> g(new Generation());
     g->hdr = R.hdr;
     g->host_image = R.image;
     g->stats = R.stats;
@@ -1045,26 +1056,32 @@ int gm_load_generation(gm_ctx *c, const void *blob, size_t len, uint32_t gen) {
         HIPCHK(c, hipMalloc((void **)&g->d_image, R.image.size()));
         HIPCHK(c, hipMemcpy(g->d_image, R.image.data(), R.image.size(), hipMemcpyHostToDevice));
         g->tab = make_gtab(g->hdr, g->d_image, gen);
-        size_t nctr = g->stats.n_counters;
-        if (nctr != c->n_counters || !c->d_counters) {
-            if (c->d_counters) HIPCHK(c, hipFree(c->d_counters));
-            HIPCHK(c, hipMalloc((void **)&c->d_counters, std::max<size_t>(nctr, 1) * 8));
-            c->n_counters = nctr;
-        }
-        HIPCHK(c, hipMemset(c->d_counters, 0, std::max<size_t>(nctr, 1) * 8));
-        // RCU-style swap: in-flight batches of the old generation complete first
-        HIPCHK(c, hipDeviceSynchronize());
-        if (c->gen) (void)hipFree(c->gen->d_image);
+        g->n_counters = g->stats.n_counters;
+        const size_t cb = std::max<size_t>(g->n_counters, 1) * 8;
+        HIPCHK(c, hipMalloc((void **)&g->d_counters, cb));
+        HIPCHK(c, hipMalloc((void **)&g->d_counters_sum, cb));
+        HIPCHK(c, hipMemset(g->d_counters, 0, cb));
+        HIPCHK(c, hipMemset(g->d_counters_sum, 0, cb));
     }
-    delete c->gen;
-    c->gen = g;
+    Generation *old;
+    {
+        std::unique_lock<std::shared_mutex> lk(c->gen_mu);
+        old = c->gen;
+        c->gen = g.release();
+    }
+    // RCU-style retirement: every batch that read the old generation finished enqueueing before
+    // the exclusive lock was granted; the device drains them before its memory is freed
+    if (old && !(c->flags & GM_CREATE_COMPILE_ONLY)) (void)hipDeviceSynchronize();
+    delete old;
     return GM_OK;
 }
 
 int gm_stats(gm_ctx *c, gm_stats_t *out) {
     if (!c || !out) return fail(c, GM_E_INVAL, "null argument");
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
     *out = c->gen->stats;
+    std::lock_guard<std::mutex> l2(c->last_mu);
     out->last_candidates = c->last_candidates;
     out->last_pairs = c->last_pairs;
     out->last_hits = c->last_hits;
@@ -1075,178 +1092,123 @@ int gm_stats(gm_ctx *c, gm_stats_t *out) {
     return GM_OK;
 }
 
-static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t alen, uint32_t n, gm_verdict *out,
-                     uint32_t *hit_ids, size_t hit_cap, hipStream_t s) {
-    const Generation *g = c->gen;
+// Enqueue one batch on stream s (device pointers).  No host synchronisation: every size a later
+// stage needs is a device status word or a host-known capacity.
+static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *reqs, const uint8_t *A, uint64_t alen,
+                     uint32_t n, gm_verdict *out, uint32_t *hit_ids, size_t hit_cap) {
+    hipStream_t s = S->stream;
     const GTab &t = g->tab;
     const bool waf = t.n_sigs > 0 && (t.n_lits > 0 || t.n_sig_regex > 0);
     const uint32_t nblk = (uint32_t)((alen >> BLK_SHIFT) + 1);
-    if (waf) { int e = grow(c, c->d_blk2rec, c->cap_blk, nblk); if (e) return e; }
     const bool prof = c->flags & GM_CREATE_PROFILE;
     auto mark = [&](int k) -> int {
-        if (prof) { HIPCHK(c, hipEventRecord(c->ev[k], s)); c->ev_used = k + 1; c->ev_pending = true; }
+        if (prof) { HIPCHK(c, hipEventRecord(S->ev[k], s)); S->ev_used = k + 1; S->ev_pending = true; }
         return GM_OK;
     };
-    c->ev_used = 0;
-    c->route_side = false;
-    HIPCHK(c, hipMemsetAsync(c->d_status, 0, STATUS_WORDS * 4, s));
+    S->ev_used = 0;
+    S->route_side = false;
+    HIPCHK(c, hipMemsetAsync(S->d_status, 0, STATUS_WORDS * 4, s));
     if (mark(0)) return GM_E_HIP;
     const uint32_t route_blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
                                                                            (uint32_t)c->cu_count * 8));
-    c->last_candidates = c->last_pairs = c->last_hits = c->last_ctx_pass = c->last_jobs = 0;
-    if (!waf || n == 0) {
-        if (t.rk_keys) k_route<3, true><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, c->d_counters, nullptr, nblk, 0);
-        else k_route<3><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, c->d_counters, nullptr, nblk, 0);
+    unsigned long long *ctr = g->d_counters;
+    if (!waf) {
+        if (t.rk_keys) k_route<3, true><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0);
+        else k_route<3><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0);
         HIPCHK(c, hipGetLastError());
         return mark(1) ? GM_E_HIP : GM_OK;
     }
-    // fork: k_route on the side stream.  route_mode 0: beside the WAF scan (its waves fit
-    // beside the scan's one workgroup per CU; the route launch is issued after the scan's, so
-    // the scan claims the CUs first).  route_mode 1: after the scan, beside the context filter
-    // and the exact check (latency-bound kernels), with blk2rec from k_blk2rec beside the scan.
-    HIPCHK(c, hipEventRecord(c->ev_fork, s));
-    HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_fork, 0));
-    // route_mode 0: k_route beside the scan; 1: after the scan, beside the context filter and the
-    // exact check; 2: split -- the first route_split % of the requests beside the scan, the rest
-    // after it (the scan with staged records is short enough that a whole route beside it ends
-    // later than the scan).  Modes 1 and 2 write blk2rec with k_blk2rec beside the scan.
-    const bool late = c->route_mode >= 1;
-    if (late) {
-        k_blk2rec<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 4)), 256, 0,
-                    c->side>>>(reqs, n, alen, c->d_blk2rec, nblk);
-        HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipEventRecord(c->ev_blk, c->side));
-    }
-    auto route_part = [&](uint32_t i0, uint32_t cnt, uint32_t *b2r, int prio) -> int {
-        if (cnt == 0) return GM_OK;
-        const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>((cnt + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
-                                                                     (uint32_t)c->cu_count * 8));
-        const gm_req *rq = reqs + i0;
-        gm_verdict *ov = out + i0;
-        if (t.rk_keys)
-            k_route<5, true><<<nb, ROUTE_BLOCK, 0, c->side>>>(rq, cnt, A, alen, t, ov, c->d_counters, b2r, nblk, prio);
-        else if (c->route_wpe == 5)
-            k_route<5><<<nb, ROUTE_BLOCK, 0, c->side>>>(rq, cnt, A, alen, t, ov, c->d_counters, b2r, nblk, prio);
-        else if (c->route_wpe == 6)
-            k_route<6><<<nb, ROUTE_BLOCK, 0, c->side>>>(rq, cnt, A, alen, t, ov, c->d_counters, b2r, nblk, prio);
-        else if (c->route_wpe == 4)
-            k_route<4><<<nb, ROUTE_BLOCK, 0, c->side>>>(rq, cnt, A, alen, t, ov, c->d_counters, b2r, nblk, prio);
-        else
-            k_route<3><<<nb, ROUTE_BLOCK, 0, c->side>>>(rq, cnt, A, alen, t, ov, c->d_counters, b2r, nblk, prio);
-        HIPCHK(c, hipGetLastError());
-        return GM_OK;
-    };
-    auto launch_route = [&]() -> int {
-        if (prof) HIPCHK(c, hipEventRecord(c->ev_route[0], c->side));
-        int e2;
-        const uint32_t n1 = c->route_mode == 2 ? (uint32_t)((uint64_t)n * (uint32_t)c->route_split / 100) : 0;
-        if (c->route_mode == 2 && (e2 = route_part(0, n1, nullptr, c->route_prio))) return e2;
-        if (late) {
-            HIPCHK(c, hipEventRecord(c->ev_scan, s));
-            HIPCHK(c, hipStreamWaitEvent(c->side, c->ev_scan, 0));
-        }
-        if ((e2 = route_part(n1, n - n1, late ? nullptr : c->d_blk2rec, late ? 0 : c->route_prio))) return e2;
-        if (prof) HIPCHK(c, hipEventRecord(c->ev_route[1], c->side));
-        HIPCHK(c, hipEventRecord(c->ev_join, c->side));
-        c->route_side = true;
-        return GM_OK;
-    };
-    if (mark(1)) return GM_E_HIP;
-
-    // candidate records: 32 B (4 x u64) each, room for one per 64 arena bytes (a lane with a
-    // candidate window in every 4th 16-byte slice) -- overflow is reported, never truncated
-    const size_t ccap = 4 * (alen / 64 + 16384), pcap = (size_t)n * 2 + 65536, jcap = (size_t)n + 65536;
     int e;
-    // persistent scan grid: one 1024-thread workgroup per CU (144 KiB LDS prefilter);
-    // every wave owns a contiguous arena range and a private candidate region of wcap entries
+    // ---- capacities (host-known: the arena length and the request count, never a device count)
+    // candidate records: 32 B (4 x u64) each, room for one per 64 arena bytes; survivors; unique
+    // pairs (2 per request on average) and jobs (1 per request); overflow is reported, never
+    // truncated silently
     const uint32_t scan_blocks = (uint32_t)c->cu_count;
     const uint32_t W = scan_blocks * SCAN_WAVES;
-    if ((e = grow(c, c->d_cand, c->cap_cand, std::max<size_t>(ccap, (size_t)W * 4096)))) return e;
-    if ((e = grow(c, c->d_ccnt, c->cap_ccnt, W + scan_blocks))) return e;   // scan-wave + ctx-block counts
-    if ((e = grow(c, c->d_surv, c->cap_surv, std::min<size_t>(alen / 256 + 65536, 0xFFFFFFFFu)))) return e;
-    const uint32_t wcap = (uint32_t)std::min<size_t>(c->cap_cand / 4 / W, 0xFFFFFFFFu);   // records per wave
-    u32x4 *cand = reinterpret_cast<u32x4 *>(c->d_cand);
-    { size_t cp = c->cap_pairs; if ((e = grow(c, c->d_pairs, cp, pcap))) return e;
-      size_t cp2 = c->cap_pairs; if ((e = grow(c, c->d_pairs2, cp2, pcap))) return e; c->cap_pairs = std::max(cp, cp2); }
-    { size_t cj = c->cap_jobs; if ((e = grow(c, c->d_jobs, cj, jcap))) return e;
-      size_t cj2 = c->cap_jobs; if ((e = grow(c, c->d_jobs2, cj2, jcap))) return e; c->cap_jobs = std::max(cj, cj2); }
+    const size_t ccap = 4 * (alen / 64 + 16384), pcap = (size_t)n * 2 + 65536, jcap = (size_t)n + 65536;
+    size_t set_need = 1;
+    while (set_need < 2 * (pcap + jcap)) set_need <<= 1;
+    size_t scan_tmp = 0;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
+    if ((e = grow(c, s, S->d_blk2rec, S->cap_blk, nblk))) return e;
+    if ((e = grow(c, s, S->d_cand, S->cap_cand, std::max<size_t>(ccap, (size_t)W * 4096)))) return e;
+    if ((e = grow(c, s, S->d_ccnt, S->cap_ccnt, W + scan_blocks))) return e;   // scan-wave + ctx-block counts
+    if ((e = grow(c, s, S->d_surv, S->cap_surv, std::min<size_t>(alen / 256 + 65536, 0xFFFFFFFFu)))) return e;
+    if ((e = grow(c, s, S->d_pairs, S->cap_pairs, pcap))) return e;
+    if ((e = grow(c, s, S->d_jobs, S->cap_jobs, jcap))) return e;
+    if ((e = grow(c, s, S->d_cnt, S->cap_cnt, (size_t)n + 1))) return e;
+    if ((e = grow(c, s, S->d_start, S->cap_start, (size_t)n + 1))) return e;
+    if ((e = grow(c, s, S->d_temp, S->cap_temp, scan_tmp))) return e;
+    if (set_need > S->cap_set) {
+        if ((e = grow(c, s, S->d_set, S->cap_set, set_need))) return e;
+        S->cap_set = set_need;   // exactly a power of two: the probe mask
+        S->epoch = 0;
+        HIPCHK(c, hipMemsetAsync(S->d_set, 0, S->cap_set * 8, s));
+    }
+    if (++S->epoch > 255) {   // epoch wrap: every slot becomes free again
+        S->epoch = 1;
+        HIPCHK(c, hipMemsetAsync(S->d_set, 0, S->cap_set * 8, s));
+    }
+    const uint32_t wcap = (uint32_t)std::min<size_t>(S->cap_cand / 4 / W, 0xFFFFFFFFu);   // records per wave
+    u32x4 *cand = reinterpret_cast<u32x4 *>(S->d_cand);
+    Dedup dd{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, out, S->d_cnt, S->d_status};
 
-    if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-    else if (t.bloom_pk == 2) {
-        if (c->scan_depth == 1) k_waf_scan<2, 1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else if (c->scan_depth == 2) k_waf_scan<2, 2><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else if (c->scan_depth == 106) k_waf_scan<2, 4, 6><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else if (c->scan_depth == 8) k_waf_scan<2, 8><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else if (c->scan_depth == 108) k_waf_scan<2, 8, 2><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else if (c->scan_depth == 110) k_waf_scan<2, 4, 5><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else if (c->scan_depth == 111) k_waf_scan<2, 8, 5><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else if (c->scan_depth == 6) k_waf_scan<2, 6><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else if (c->scan_depth == 101) k_waf_scan<2, 4, 1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else if (c->scan_depth == 102) k_waf_scan<2, 4, 2><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else if (c->scan_depth == 104) k_waf_scan<2, 4, 4><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else if (c->scan_depth == 105) k_waf_scan<1, 4, 1><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else if (c->scan_depth == 103) k_waf_scan<2, 4, 3><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else if (c->scan_stage) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-        else k_waf_scan<2, SCAN_DEPTH, 6><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
-    } else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, c->d_ccnt);
+    // ---- fork: k_route on the side stream, beside the WAF scan (independent inputs; its waves
+    // fit beside the scan's one workgroup per CU; issued after the scan so the scan claims the
+    // CUs first).  It writes the verdicts, the location counters, blk2rec and zeroes the counts.
+    HIPCHK(c, hipEventRecord(S->ev_fork, s));
+    HIPCHK(c, hipStreamWaitEvent(S->side, S->ev_fork, 0));
+    if (mark(1)) return GM_E_HIP;
+    // persistent scan grid: one 1024-thread workgroup per CU (128 KiB LDS prefilter); every wave
+    // owns a contiguous arena range and a private candidate region of wcap records
+    if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt);
+    else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt);
+    else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt);
     HIPCHK(c, hipGetLastError());
-    if ((e = launch_route())) return e;
+    {
+        const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
+                                                                     (uint32_t)c->cu_count * 8));
+        if (prof) HIPCHK(c, hipEventRecord(S->ev_route[0], S->side));
+        // raised issue priority: the route's short latency-bound waves finish early instead of
+        // stretching past the scan
+        if (t.rk_keys)
+            k_route<5, true><<<nb, ROUTE_BLOCK, 0, S->side>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1);
+        else
+            k_route<5><<<nb, ROUTE_BLOCK, 0, S->side>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1);
+        HIPCHK(c, hipGetLastError());
+        if (prof) HIPCHK(c, hipEventRecord(S->ev_route[1], S->side));
+        HIPCHK(c, hipEventRecord(S->ev_join, S->side));
+        S->route_side = true;
+    }
     if (mark(2)) return GM_E_HIP;
-    const uint32_t bcap = (uint32_t)std::min<size_t>(c->cap_surv / scan_blocks, 0xFFFFFFFFu);
-    k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, c->d_ccnt, W, t, c->d_surv, bcap, c->d_ccnt + W,
-                                                c->d_status);
+    const uint32_t bcap = (uint32_t)std::min<size_t>(S->cap_surv / scan_blocks, 0xFFFFFFFFu);
+    k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, S->d_ccnt, W, t, S->d_surv, bcap, S->d_ccnt + W,
+                                                S->d_status);
     HIPCHK(c, hipGetLastError());
-    // blk2rec must be written before the exact check; the route's verdicts before the pairs
-    HIPCHK(c, hipStreamWaitEvent(s, late ? c->ev_blk : c->ev_join, 0));
+    // join: blk2rec, the verdicts and the zeroed counts are complete before the exact check
+    HIPCHK(c, hipStreamWaitEvent(s, S->ev_join, 0));
     constexpr uint32_t EXACT_SUB = 8;
-    k_waf_exact<<<scan_blocks * EXACT_SUB, 256, 0, s>>>(A, alen, reqs, n, c->d_blk2rec, t, c->d_surv, bcap,
-                                                         c->d_ccnt + W, EXACT_SUB, c->d_pairs, (uint32_t)c->cap_pairs,
-                                                         c->d_jobs, (uint32_t)c->cap_jobs, c->d_status);
+    k_waf_exact<<<scan_blocks * EXACT_SUB, 256, 0, s>>>(A, alen, reqs, n, S->d_blk2rec, t, S->d_surv, bcap,
+                                                         S->d_ccnt + W, EXACT_SUB, S->d_pairs, (uint32_t)S->cap_pairs,
+                                                         S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, dd);
     HIPCHK(c, hipGetLastError());
-    if (late) HIPCHK(c, hipStreamWaitEvent(s, c->ev_join, 0));   // join
     if (mark(3)) return GM_E_HIP;
-    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, STATUS_WORDS * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    c->last_candidates = c->h_status[6];
-    c->last_ctx_pass = c->h_status[7];
-    c->last_jobs = c->h_status[2];
-    if (c->h_status[3]) return fail(c, GM_E_OVERFLOW, "WAF candidate/pair/job capacity exceeded");
-    uint32_t nj = std::min<uint32_t>(c->h_status[2], (uint32_t)c->cap_jobs);
-    int rec_bits = 1;
-    while (rec_bits < 32 && (1ull << rec_bits) < n) rec_bits++;
-    if (nj) {
-        size_t need = 0;
-        HIPCHK(c, hipcub::DeviceRadixSort::SortKeys(nullptr, need, c->d_jobs, c->d_jobs2, (int)nj, 0, 32 + rec_bits, s));
-        if ((e = grow(c, c->d_temp, c->cap_temp, need))) return e;
-        HIPCHK(c, hipcub::DeviceRadixSort::SortKeys(c->d_temp, need, c->d_jobs, c->d_jobs2, (int)nj, 0, 32 + rec_bits, s));
-        k_waf_regex<<<std::min<uint32_t>((nj + 255) / 256, c->cu_count * 8), 256, 0, s>>>(
-            A, reqs, t, c->d_jobs2, nj, c->d_pairs, (uint32_t)c->cap_pairs, c->d_status);
+    if (t.n_sig_regex) {
+        k_waf_regex<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(A, reqs, t, S->d_jobs, (uint32_t)S->cap_jobs, S->d_pairs,
+                                                               (uint32_t)S->cap_pairs, dd);
         HIPCHK(c, hipGetLastError());
     }
     if (t.n_always) {
-        k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(A, reqs, n, t, c->d_pairs, (uint32_t)c->cap_pairs, c->d_status);
+        k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(A, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd);
         HIPCHK(c, hipGetLastError());
     }
-    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, STATUS_WORDS * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    if (c->h_status[3]) return fail(c, GM_E_OVERFLOW, "WAF pair capacity exceeded");
-    uint32_t m = std::min<uint32_t>(c->h_status[1], (uint32_t)c->cap_pairs);
-    c->last_pairs = m;
-    if (m == 0) return mark(4) ? GM_E_HIP : GM_OK;
-    if ((e = grow(c, c->d_keep, c->cap_keep, m))) return e;
-    if ((e = grow(c, c->d_idx, c->cap_idx, m))) return e;
-    size_t need = 0;
-    HIPCHK(c, hipcub::DeviceRadixSort::SortKeys(nullptr, need, c->d_pairs, c->d_pairs2, (int)m, 0, 32 + rec_bits, s));
-    size_t need2 = 0;
-    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, need2, c->d_keep, c->d_keep, (int)m, s));
-    if ((e = grow(c, c->d_temp, c->cap_temp, std::max(need, need2)))) return e;
-    HIPCHK(c, hipcub::DeviceRadixSort::SortKeys(c->d_temp, need, c->d_pairs, c->d_pairs2, (int)m, 0, 32 + rec_bits, s));
-    uint32_t blocks = std::min<uint32_t>((m + 255) / 256, c->cu_count * 8);
-    k_pairs_mark<<<blocks, 256, 0, s>>>(c->d_pairs2, m, out, c->d_keep);
+    // ---- hit emission: offsets by an exclusive scan of the per-request counts (request order)
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_temp, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
+    k_hits_scatter<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(S->d_pairs, (uint32_t)S->cap_pairs, S->d_cnt, S->d_start,
+                                                              hit_ids, hit_cap, ctr, t.n_locs, S->d_status);
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->d_temp, need2, c->d_keep, c->d_idx, (int)m, s));
-    k_pairs_emit<<<blocks, 256, 0, s>>>(c->d_pairs2, m, c->d_keep, c->d_idx, out, hit_ids, hit_cap, c->d_counters,
-                                        t.n_locs, c->d_status);
+    k_hits_finalize<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8)), 256, 0, s>>>(
+        S->d_start, n, out, hit_ids, hit_cap, S->d_status);
     HIPCHK(c, hipGetLastError());
     if (mark(4)) return GM_E_HIP;
     return GM_OK;
@@ -1255,29 +1217,33 @@ static int run_batch(gm_ctx *c, const gm_req *reqs, const uint8_t *A, uint64_t a
 int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit_ids, size_t hit_cap, void *stream) {
     if (!c || !in || !out) return fail(c, GM_E_INVAL, "null argument");
     if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
-    if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
-    std::lock_guard<std::mutex> lk(c->mu);
     HIPCHK(c, hipSetDevice(c->dev));
     hipStream_t s = (hipStream_t)stream;
-    if (in->n == 0) { HIPCHK(c, hipMemsetAsync(c->d_status, 0, STATUS_WORDS * 4, s)); return GM_OK; }
+    Scratch *S = scratch_for(c, s);
+    if (!S) return fail(c, GM_E_NOMEM, t_err);
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    const Generation *g = c->gen;
+    if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
+    if (in->n == 0) { HIPCHK(c, hipMemsetAsync(S->d_status, 0, STATUS_WORDS * 4, s)); S->ev_pending = false; return GM_OK; }
     if (((uintptr_t)in->arena & 15) || ((uintptr_t)in->reqs & 15) || ((uintptr_t)out & 15))
         return fail(c, GM_E_INVAL, "reqs / arena / out must be 16-byte aligned");
+    if (hit_cap > 0xFFFFFFFFull) hit_cap = 0xFFFFFFFFull;   // hit offsets are u32
     if (!(in->flags & GM_BATCH_HOST))
-        return run_batch(c, in->reqs, in->arena, in->arena_len, in->n, out, hit_ids, hit_cap, s);
-    // host buffers: stage reqs + arena + verdicts + hits through HBM
+        return run_batch(c, S, g, in->reqs, in->arena, in->arena_len, in->n, out, hit_ids, hit_ids ? hit_cap : 0);
+    // host buffers: stage reqs + arena + verdicts + hits through HBM (PCIe both ways)
     size_t rq = (size_t)in->n * sizeof(gm_req), ar = (in->arena_len + 255) & ~255ull;
     size_t vo = (size_t)in->n * sizeof(gm_verdict), ho = hit_cap * 4;
     size_t tot = rq + ar + vo + ho + 1024;
-    int e = grow(c, c->d_stage, c->cap_stage, tot);
+    int e = grow(c, s, S->d_stage, S->cap_stage, tot);
     if (e) return e;
-    uint8_t *p = c->d_stage;
+    uint8_t *p = S->d_stage;
     gm_req *dr = (gm_req *)p; p += (rq + 255) & ~255ull;
     uint8_t *da = p; p += ar;
     gm_verdict *dv = (gm_verdict *)p; p += (vo + 255) & ~255ull;
     uint32_t *dh = (uint32_t *)p;
     HIPCHK(c, hipMemcpyAsync(dr, in->reqs, rq, hipMemcpyHostToDevice, s));
     if (in->arena_len) HIPCHK(c, hipMemcpyAsync(da, in->arena, in->arena_len, hipMemcpyHostToDevice, s));
-    e = run_batch(c, dr, da, in->arena_len, in->n, dv, dh, hit_cap, s);
+    e = run_batch(c, S, g, dr, da, in->arena_len, in->n, dv, dh, hit_ids ? hit_cap : 0);
     if (e) return e;
     HIPCHK(c, hipMemcpyAsync(out, dv, vo, hipMemcpyDeviceToHost, s));
     if (hit_ids && hit_cap) HIPCHK(c, hipMemcpyAsync(hit_ids, dh, ho, hipMemcpyDeviceToHost, s));
@@ -1289,37 +1255,66 @@ int gm_sync(gm_ctx *c, void *stream) {
     if (c->flags & GM_CREATE_COMPILE_ONLY) return GM_OK;
     HIPCHK(c, hipSetDevice(c->dev));
     hipStream_t s = (hipStream_t)stream;
-    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, STATUS_WORDS * 4, hipMemcpyDeviceToHost, s));
+    Scratch *S = scratch_for(c, s);
+    if (!S) return fail(c, GM_E_NOMEM, t_err);
+    HIPCHK(c, hipMemcpyAsync(S->h_status, S->d_status, STATUS_WORDS * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    c->last_hits = c->h_status[4];
-    if (c->ev_pending) {
-        for (int k = 0; k < 4; k++) {
-            c->last_ms[k] = 0;
-            if (k + 1 < c->ev_used) (void)hipEventElapsedTime(&c->last_ms[k], c->ev[k], c->ev[k + 1]);
+    {
+        std::lock_guard<std::mutex> lk(c->last_mu);
+        memcpy(c->last_status, S->h_status, STATUS_WORDS * 4);
+        c->last_candidates = S->h_status[6];
+        c->last_ctx_pass = S->h_status[7];
+        c->last_jobs = S->h_status[2];
+        c->last_pairs = S->h_status[1];
+        c->last_hits = S->h_status[4];
+        if (S->ev_pending) {
+            for (int k = 0; k < 4; k++) {
+                c->last_ms[k] = 0;
+                if (k + 1 < S->ev_used) (void)hipEventElapsedTime(&c->last_ms[k], S->ev[k], S->ev[k + 1]);
+            }
+            // stage 0 = the route on the side stream (its own time); stage 1 = the scan
+            if (S->route_side) (void)hipEventElapsedTime(&c->last_ms[0], S->ev_route[0], S->ev_route[1]);
+            S->ev_pending = false;
         }
-        // overlapped route: its own time on the side stream (the scan's stage starts at the fork)
-        if (c->route_side) (void)hipEventElapsedTime(&c->last_ms[0], c->ev_route[0], c->ev_route[1]);
-        c->ev_pending = false;
     }
-    if (c->h_status[3]) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded");
+    const uint32_t ov = S->h_status[3];
+    if (ov & 2u) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded");
+    if (ov) return fail(c, GM_E_OVERFLOW, "WAF candidate / survivor / pair / job capacity exceeded");
     return GM_OK;
 }
 
 int gm_counters(gm_ctx *c, uint64_t *out, size_t n) {
     if (!c || !out) return fail(c, GM_E_INVAL, "null argument");
     if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
     HIPCHK(c, hipSetDevice(c->dev));
     HIPCHK(c, hipDeviceSynchronize());
-    HIPCHK(c, hipMemcpy(out, c->d_counters, std::min(n, c->n_counters) * 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(out, c->gen->d_counters, std::min(n, c->gen->n_counters) * 8, hipMemcpyDeviceToHost));
+    return GM_OK;
+}
+
+int gm_counters_global(gm_ctx *c, uint64_t *out, size_t n) {
+    if (!c || !out) return fail(c, GM_E_INVAL, "null argument");
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
+    HIPCHK(c, hipSetDevice(c->dev));
+    HIPCHK(c, hipDeviceSynchronize());
+    HIPCHK(c, hipMemcpy(out, c->gen->d_counters_sum, std::min(n, c->gen->n_counters) * 8, hipMemcpyDeviceToHost));
     return GM_OK;
 }
 
 int gm_counters_reset(gm_ctx *c) {
     if (!c) return fail(c, GM_E_INVAL, "null ctx");
-    if (c->flags & GM_CREATE_COMPILE_ONLY || !c->d_counters) return GM_OK;
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return GM_OK;
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    if (!c->gen) return GM_OK;
     HIPCHK(c, hipSetDevice(c->dev));
-    HIPCHK(c, hipMemset(c->d_counters, 0, std::max<size_t>(c->n_counters, 1) * 8));
+    HIPCHK(c, hipDeviceSynchronize());
+    const size_t cb = std::max<size_t>(c->gen->n_counters, 1) * 8;
+    HIPCHK(c, hipMemset(c->gen->d_counters, 0, cb));
+    HIPCHK(c, hipMemset(c->gen->d_counters_sum, 0, cb));
     return GM_OK;
 }
 
@@ -1340,11 +1335,16 @@ int gm_comm_init(gm_ctx *c, const void *uid, int nranks, int rank) {
     return GM_OK;
 }
 
+// Out of place: the cumulative local counters stay this device's own; their sum over the ranks
+// goes to the generation's reduced buffer (gm_counters_global).  Any number of calls give the
+// true totals (an in-place reduction of cumulative counters would add them up again each time).
 int gm_counters_allreduce(gm_ctx *c, void *stream) {
     if (!c || !c->comm) return fail(c, GM_E_COMM, "gm_comm_init not called");
-    if (!c->d_counters) return fail(c, GM_E_NOGEN, "no counters");
-    ncclResult_t r = ncclAllReduce(c->d_counters, c->d_counters, c->n_counters, ncclUint64, ncclSum, c->comm,
-                                   (hipStream_t)stream);
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    if (!c->gen || !c->gen->d_counters) return fail(c, GM_E_NOGEN, "no counters");
+    HIPCHK(c, hipSetDevice(c->dev));
+    ncclResult_t r = ncclAllReduce(c->gen->d_counters, c->gen->d_counters_sum, std::max<size_t>(c->gen->n_counters, 1),
+                                   ncclUint64, ncclSum, c->comm, (hipStream_t)stream);
     if (r != ncclSuccess) return fail(c, GM_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
     return GM_OK;
 }
@@ -1367,7 +1367,8 @@ extern "C" int gm_debug_waf_keys(gm_ctx *c, uint32_t *out, size_t cap) {
 extern "C" int gm_debug_status(gm_ctx *c, uint32_t *out, size_t n) {
     if (!c || !out) return fail(c, GM_E_INVAL, "null argument");
     if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
-    memcpy(out, c->h_status, std::min<size_t>(n, STATUS_WORDS) * 4);
+    std::lock_guard<std::mutex> lk(c->last_mu);
+    memcpy(out, c->last_status, std::min<size_t>(n, STATUS_WORDS) * 4);
     return (int)std::min<size_t>(n, STATUS_WORDS);
 }
 
@@ -1566,6 +1567,12 @@ extern "C" int gm_normalize_uris(gm_ctx *c, const uint8_t *arena, const uint64_t
     if (n == 0) return GM_OK;
     if (!arena || !off || !len || !out || !out_len) return fail(c, GM_E_INVAL, "null argument");
     HIPCHK(c, hipSetDevice(c->dev));
+    // the call is this stream's last enqueued work: its status words start clean, so a gm_sync
+    // after it reports OK (no stale match-batch overflow)
+    Scratch *S = scratch_for(c, (hipStream_t)stream);
+    if (!S) return fail(c, GM_E_NOMEM, t_err);
+    HIPCHK(c, hipMemsetAsync(S->d_status, 0, STATUS_WORDS * 4, (hipStream_t)stream));
+    S->ev_pending = false;
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 16));
     k_uri_normalize<<<blocks, 256, 0, (hipStream_t)stream>>>(arena, off, len, n, out, out_len);
     HIPCHK(c, hipGetLastError());

@@ -49,7 +49,7 @@ class GmBatch(ctypes.Structure):
 
 EXPORTS = ["gm_create", "gm_destroy", "gm_abi_version", "gm_load_generation", "gm_match_batch", "gm_sync",
            "gm_counters", "gm_counters_reset", "gm_comm_unique_id", "gm_comm_init", "gm_counters_allreduce",
-           "gm_stats", "gm_last_error", "gm_normalize_uris"]
+           "gm_stats", "gm_last_error", "gm_normalize_uris", "gm_counters_global"]
 
 _lib = None
 
@@ -73,6 +73,7 @@ def lib():
         L.gm_comm_unique_id.argtypes = [ctypes.c_void_p]
         L.gm_comm_init.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         L.gm_counters_allreduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.gm_counters_global.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
         L.gm_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(GmStats)]
         L.gm_normalize_uris.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -187,4 +188,12 @@ class Engine:
         self._chk(lib().gm_comm_init(self.h, uid, nranks, rank))
 
     def counters_allreduce(self, stream=0):
+        """Enqueue the out-of-place sum of every rank's cumulative counters (RCCL)."""
         self._chk(lib().gm_counters_allreduce(self.h, stream))
+
+    def counters_global(self) -> np.ndarray:
+        """The job-wide counter totals computed by the last counters_allreduce."""
+        n = self.stats()["n_counters"]
+        out = np.zeros(max(n, 1), dtype=np.uint64)
+        self._chk(lib().gm_counters_global(self.h, out.ctypes.data, n))
+        return out[:n]

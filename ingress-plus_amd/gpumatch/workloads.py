@@ -153,6 +153,32 @@ def c4_sigset(n_lit=8000, n_re=2000) -> sigs.SigSet:
     return sigs.gen_waf_sigset(n_lit, n_re)
 
 
+def c4_bench_generation():
+    """The benchmarked C4 generation (bench.py): the 10k-rule set on the cafe Ingress in
+    wallarm_mode block, with a benign traffic sample (disjoint seed) steering the prefilter's
+    key choice.  Returns (sigset, blob)."""
+    ss = c4_sigset()
+    return ss, c4_blob(ss, "block", sample=c4_sample(ss))
+
+
+C4_POOL_SEED = records.SEED_BASE + 3
+
+
+def replicate_pool(preqs: np.ndarray, parena_len: int, n: int):
+    """Headers of ``n`` requests that repeat a ``len(preqs)``-request pool: copy k of the pool's
+    arena sits at k * plen (plen = the pool arena rounded up to 16 B).  Returns (reqs, plen,
+    reps, arena_len); the caller lays the ``reps`` arena copies out in device memory."""
+    pool_n = len(preqs)
+    plen = (parena_len + 15) & ~15
+    reps = (n + pool_n - 1) // pool_n
+    reqs = np.tile(preqs, reps)[:n]
+    reqs["base"] += (np.repeat(np.arange(reps, dtype=np.uint64), pool_n)[:n] * np.uint64(plen))
+    last = reqs[-1]
+    arena_len = int(last["base"]) + sum(int(last[f]) for f in ("uri_len", "args_len", "hdr_len", "body_len",
+                                                                "host_len", "method_len", "ruri_len", "raddr_len"))
+    return reqs, plen, reps, arena_len
+
+
 # algorithmic bytes per request (SURVEY.md §8(d)): 64 B header + payload of the fields the
 # config reads + 32 B verdict (+ 4 B per hit id, added by the caller)
 def algorithmic_bytes(reqs: np.ndarray, config: str) -> int:

@@ -163,10 +163,11 @@ typedef struct {
     char *err418;             /* error_page 418 = <complex value> */
     int waf_mode;
     int pcre_only;            /* regex location the engine rejects (orc_pcre_only) */
+    int nested;               /* contains location / if / rewrite: deferred (GM_ACT_UNSUPPORTED) */
     pcre *relaxed;            /* its superset pattern (orc_relax), NULL = none */
 } loc_t;
 
-typedef struct { char *var; int op; char *val; pcre *re; int code; char *text; int is_return_only; } sif_t;
+typedef struct { char *var; int op; char *val; pcre *re; int code; char *text; int is_return_only; int unsupported; } sif_t;
 
 typedef struct {
     int id; int nports; int ports[16]; int ssl[16]; int def[16];
@@ -398,7 +399,7 @@ static void add_location(build_t *B, srv_t *S, dir_t *d, int srv_waf) {
     for (int i = 0; i < d->nkids; i++) {
         dir_t *k = &d->kids[i];
         if (!k->nargs) continue;
-        if (!strcmp(k->args[0], "proxy_pass") && k->nargs == 2) {
+        if ((!strcmp(k->args[0], "proxy_pass") || !strcmp(k->args[0], "grpc_pass")) && k->nargs == 2) {
             const char *u = k->args[1];
             const char *p = strstr(u, "://"); p = p ? p + 3 : u;
             int n = 0; while (p[n] && p[n] != '/' && p[n] != '$') n++;
@@ -411,6 +412,8 @@ static void add_location(build_t *B, srv_t *S, dir_t *d, int srv_waf) {
             L.err418 = strdup(k->args[3]);
         } else if (!strcmp(k->args[0], "wallarm_mode") && k->nargs == 2) {
             L.waf_mode = waf_mode_of(k->args[1]);
+        } else if (!strcmp(k->args[0], "location") || !strcmp(k->args[0], "if") || !strcmp(k->args[0], "rewrite")) {
+            L.nested = 1;   /* nested location / if / rewrite: outside the restated subset */
         }
     }
     if (L.has_proxy && L.plen && L.path[L.plen - 1] == '/' && (L.kind == LK_PREFIX || L.kind == LK_EXACT ||
@@ -484,6 +487,11 @@ static void add_server(build_t *B, dir_t *s, int http_waf) {
                 }
             }
             if (!has_ret) continue;   /* e.g. HSTS `if` only sets a header variable */
+            S.ifs = realloc(S.ifs, sizeof(sif_t) * (S.nifs + 1)); S.ifs[S.nifs++] = f;
+        } else if (!strcmp(n, "rewrite")) {
+            /* server-level rewrite (server snippets): outside the restated subset, a request that
+             * reaches it in the server rewrite phase is deferred (GM_ACT_UNSUPPORTED) */
+            sif_t f; memset(&f, 0, sizeof f); f.unsupported = 1;
             S.ifs = realloc(S.ifs, sizeof(sif_t) * (S.nifs + 1)); S.ifs[S.nifs++] = f;
         } else if (!strcmp(n, "return") && d->nargs >= 2) {
             sif_t f; memset(&f, 0, sizeof f); f.is_return_only = 1;
@@ -1086,6 +1094,7 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
     for (int i = 0; i < S->nifs; i++) {
         sif_t *f = &S->ifs[i];
         int hit = 0;
+        if (f->unsupported) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
         if (f->is_return_only) hit = 1;
         else {
             const char *vn = f->var; sv val = {"", 0};
@@ -1106,7 +1115,7 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
     v->location_id = (uint32_t)lid;
     if (a301) { v->action = GM_ACT_AUTO_301; v->status = 301; return; }
     loc_t *L = &c->loc[lid];
-    if (L->pcre_only) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
+    if (L->pcre_only || L->nested) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
     loc_t *F = L;   /* location that runs the content phase */
     if (L->has_return && L->ret_code == 418 && L->err418) {
         int pidx = -2, part = -2;
@@ -1119,19 +1128,23 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
             int nl = find_named(c, S, target);
             if (nl < 0) { v->action = GM_ACT_NOT_FOUND; v->status = 404; return; }
             F = &c->loc[nl];
+            if (F->nested) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
         } else if (target.n == 0) {
             v->action = GM_ACT_ERRPAGE; v->status = 302; return;
         } else {
             v->action = GM_ACT_UNSUPPORTED; v->status = 0; return;
         }
     } else if (L->has_return) {
-        v->action = (L->ret_code >= 301 && L->ret_code <= 308) ? GM_ACT_REDIRECT : GM_ACT_RETURN;
+        v->action = (L->ret_code == 301 || L->ret_code == 302 || L->ret_code == 303 || L->ret_code == 307 ||
+                     L->ret_code == 308) ? GM_ACT_REDIRECT : GM_ACT_RETURN;
         v->status = (uint32_t)L->ret_code; return;
     } else if (L->has_proxy) {
         v->route_kind = GM_ROUTE_PLAIN;
     }
     if (F->has_return && F != L) {
-        v->action = GM_ACT_RETURN; v->status = (uint32_t)F->ret_code; return;
+        v->action = (F->ret_code == 301 || F->ret_code == 302 || F->ret_code == 303 || F->ret_code == 307 ||
+                     F->ret_code == 308) ? GM_ACT_REDIRECT : GM_ACT_RETURN;
+        v->status = (uint32_t)F->ret_code; return;
     }
     if (!F->has_proxy) { v->action = GM_ACT_NOT_FOUND; v->status = 404; return; }
     v->action = GM_ACT_PROXY; v->status = 0;

@@ -1,0 +1,190 @@
+"""The boundary's pipeline properties on the GPU, through libgpumatch.so:
+
+- the benchmarked workload itself (bench.py's C4 generation and its 1M-request pool, replicated
+  x10 in HBM) against the oracle, and every HBM replica identical;
+- gm_match_batch is asynchronous (returns before the device finishes) and thread-safe per
+  (ctx, stream): two batches on two streams, each checked against the oracle;
+- counters: cumulative per device, the RCCL reduction out of place (N calls = true totals);
+- status hygiene: a normalisation after an overflowing batch syncs clean.
+"""
+
+import threading
+
+import numpy as np
+import pytest
+
+from gpumatch import engine, records, workloads
+from helpers import assert_verdicts_equal
+from oracle_py import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "GPU test without a GPU"
+    return torch, torch.device("cuda", 0)
+
+
+def _to_dev(torch, dev, reqs, arena, extra=1024):
+    d_reqs = torch.from_numpy(np.ascontiguousarray(reqs).view(np.uint8).reshape(-1)).to(dev)
+    d_arena = torch.zeros(len(arena) + extra, dtype=torch.uint8, device=dev)
+    if len(arena):
+        d_arena[:len(arena)].copy_(torch.from_numpy(np.ascontiguousarray(arena)))
+    return d_reqs, d_arena
+
+
+def _split_hits(v, hits):
+    return [hits[int(o):int(o) + int(k)] for o, k in zip(v["first_hit_off"], v["n_hits"])]
+
+
+def test_benched_c4_pool_parity_and_replicas(torch_dev):
+    """bench.py's exact workload: 200k requests of the 1M-request pool against the oracle, and all
+    ten HBM replicas of the pool (10M requests, one batch) give identical verdicts and hit lists."""
+    torch, dev = torch_dev
+    ss, gblob = workloads.c4_bench_generation()
+    preqs, parena = records.gen_c4(1_000_000, ss, seed=workloads.C4_POOL_SEED)
+    n = 10_000_000
+    reqs, plen, reps, arena_len = workloads.replicate_pool(preqs, len(parena), n)
+    d_pool = torch.from_numpy(np.ascontiguousarray(parena)).to(dev)
+    d_arena = torch.zeros(reps * plen + 1024, dtype=torch.uint8, device=dev)
+    for k in range(reps):
+        d_arena[k * plen:k * plen + len(parena)].copy_(d_pool)
+    del d_pool
+    d_reqs = torch.from_numpy(reqs.view(np.uint8).reshape(-1)).to(dev)
+    d_out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    cap = n // 4 + (1 << 20)
+    d_hits = torch.empty(cap, dtype=torch.int32, device=dev)
+    e = engine.Engine(0)
+    e.load(gblob, 1)
+    s = torch.cuda.current_stream()
+    e.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), arena_len, n, d_out.data_ptr(), d_hits.data_ptr(), cap,
+                s.cuda_stream)
+    e.sync(s.cuda_stream)
+    total = e.stats()["last_hits"]
+    v = d_out.cpu().numpy().view(records.VERDICT_DTYPE)
+    h = d_hits[:total].cpu().numpy().view(np.uint32)
+    pool_n = len(preqs)
+    per = total // reps
+    assert per * reps == total and per > 5000
+    v0 = v[:pool_n]
+    for k in range(1, reps):
+        vk = v[k * pool_n:(k + 1) * pool_n].copy()
+        has = vk["n_hits"] > 0
+        assert np.array_equal(vk["first_hit_off"][has] - k * per, v0["first_hit_off"][has])
+        vk["first_hit_off"] = v0["first_hit_off"]
+        assert vk.tobytes() == v0.tobytes(), f"replica {k} verdicts differ"
+        assert np.array_equal(h[k * per:(k + 1) * per], h[:per]), f"replica {k} hit ids differ"
+    m = 200_000
+    exp, eh = Oracle(gblob, 1).match(preqs[:m], parena, nthreads=16, hit_cap=8 * m + 1024)
+    got = v0[:m].copy()
+    nh = int(got["n_hits"].sum())
+    assert_verdicts_equal(got, exp, h[:nh], eh, "benched C4 pool")
+    assert (exp["action"] == 6).sum() > 1000
+
+
+def _batch(seed, n):
+    ss = workloads.c4_sigset(800, 200)
+    reqs, arena = records.gen_c4(n, ss, seed=seed, plant_rate=0.05, pool_mb=8)
+    return workloads.c4_blob(ss, "block"), reqs, arena
+
+
+def test_async_two_streams_two_threads(torch_dev):
+    """gm_match_batch returns before its batch completes, and two batches enqueued from two
+    threads on two streams of one ctx each match the oracle."""
+    torch, dev = torch_dev
+    ss = workloads.c4_sigset(800, 200)
+    blob = workloads.c4_blob(ss, "block")
+    batches = []
+    for seed in (101, 202):
+        reqs, arena = records.gen_c4(150_000, ss, seed=seed, plant_rate=0.05, pool_mb=8)
+        batches.append((reqs, arena))
+    e = engine.Engine(0)
+    e.load(blob, 4)
+    e.sync(0)
+    streams = [torch.cuda.Stream(device=dev) for _ in batches]
+    bufs = []
+    for (reqs, arena) in batches:
+        d_reqs, d_arena = _to_dev(torch, dev, reqs, arena)
+        n = len(reqs)
+        bufs.append((d_reqs, d_arena, len(arena), n, torch.empty(n * 32, dtype=torch.uint8, device=dev),
+                     torch.empty(4 * n + 1024, dtype=torch.int32, device=dev)))
+    torch.cuda.synchronize()
+    pending = [None, None]
+
+    def enqueue(k):
+        d_reqs, d_arena, alen, n, d_out, d_hits = bufs[k]
+        e.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), alen, n, d_out.data_ptr(), d_hits.data_ptr(),
+                    d_hits.numel(), streams[k].cuda_stream)
+        pending[k] = not streams[k].query()   # still running when the call returned
+
+    # warm the per-stream scratch (first batches on a stream allocate it)
+    for k in range(2):
+        enqueue(k)
+        e.sync(streams[k].cuda_stream)
+    th = [threading.Thread(target=enqueue, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert any(pending), "gm_match_batch waited for the device"
+    oracle = Oracle(blob, 4)
+    for k, (reqs, arena) in enumerate(batches):
+        e.sync(streams[k].cuda_stream)
+        total = e.stats()["last_hits"]
+        d_reqs, d_arena, alen, n, d_out, d_hits = bufs[k]
+        got = d_out.cpu().numpy().view(records.VERDICT_DTYPE)
+        gh = d_hits.cpu().numpy().view(np.uint32)
+        exp, eh = oracle.match(reqs, arena)
+        assert_verdicts_equal(got, exp, gh[:len(eh)], eh, f"stream {k}")
+        assert int(got["n_hits"].sum()) == len(eh) and total == len(eh)
+
+
+def test_counters_cumulative_and_allreduce_out_of_place(torch_dev):
+    """Counters accumulate over batches; the RCCL reduction (1 rank here) is out of place, so
+    calling it after every batch gives the true totals, never a doubled count."""
+    ss = workloads.c4_sigset(400, 100)
+    reqs, arena = records.gen_c4(20_000, ss, plant_rate=0.1, pool_mb=4)
+    b = workloads.c4_blob(ss, "monitoring")
+    e = engine.Engine(0)
+    e.load(b, 3)
+    e.comm_init(engine.Engine.comm_unique_id(), 1, 0)
+    got, gh = e.match_host(reqs, arena)
+    st = e.stats()
+    nl = st["n_locations"]
+    loc = got["location_id"][got["location_id"] != 0xFFFFFFFF]
+    one = np.concatenate([np.bincount(loc, minlength=nl), np.bincount(gh, minlength=st["n_sigs"])]).astype(np.uint64)
+    for k in (1, 2, 3):
+        if k > 1:
+            e.match_host(reqs, arena)
+        e.counters_allreduce(0)
+        e.sync(0)
+        assert np.array_equal(e.counters(), k * one)
+        assert np.array_equal(e.counters_global(), k * one)
+        e.counters_allreduce(0)   # a second reduction of the same state changes nothing
+        assert np.array_equal(e.counters_global(), k * one)
+
+
+def test_normalize_after_overflow_syncs_clean(torch_dev):
+    """A normalisation enqueued after an overflowing batch completes with GM_OK (its own status)."""
+    torch, dev = torch_dev
+    ss = workloads.c4_sigset(200, 50)
+    reqs, arena = records.gen_c4(5_000, ss, plant_rate=0.5, pool_mb=4)
+    e = engine.Engine(0)
+    e.load(workloads.c4_blob(ss), 3)
+    with pytest.raises(engine.GmError) as ei:
+        e.match_host(reqs, arena, hit_cap=10)
+    assert ei.value.code == engine.GM_E_OVERFLOW
+    paths = [b"/a/./b/../c", b"//x//y", b"/%41%2f"]
+    buf = b"".join(p.ljust(16, b"\0") for p in paths)
+    d_a = torch.from_numpy(np.frombuffer(buf, np.uint8).copy()).to(dev)
+    d_off = torch.tensor([16 * i for i in range(len(paths))], dtype=torch.int64, device=dev)
+    d_len = torch.tensor([len(p) for p in paths], dtype=torch.int32, device=dev)
+    d_ol = torch.zeros(len(paths), dtype=torch.int32, device=dev)
+    e.normalize_uris_ptr(d_a.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(paths), d_a.data_ptr(),
+                         d_ol.data_ptr(), 0)
+    e.sync(0)
+    out = d_a.cpu().numpy().tobytes()
+    ol = d_ol.cpu().numpy()
+    assert [out[16 * i:16 * i + int(ol[i])] for i in range(len(paths))] == [b"/a/c", b"/x/y", b"/A/"]

@@ -1,7 +1,12 @@
 """N > 1 path on the CPU: world_size-2 `gloo` ranks shard a C4 batch with gpumatch.shard,
 classify their shard (the oracle stands in for the GPU here), all-reduce the per-location and
 per-rule counters, and gather the verdicts.  The merged result must equal the single-process
-batch bit for bit, and the reduced counters must equal its counters (SURVEY.md §8 e)."""
+batch bit for bit, and the reduced counters must equal its counters (SURVEY.md §8 e).
+
+Counters follow libgpumatch's contract (include/gpumatch.h gm_counters_allreduce): each rank's
+counters are cumulative over its batches, and every reduction is OUT OF PLACE into a separate
+buffer -- so after step k the reduced totals are exactly k x the single-process counters (an
+in-place reduction of cumulative counters would double-count from the second call on)."""
 
 import os
 import socket
@@ -16,6 +21,7 @@ from gpumatch import records, shard, workloads
 from oracle_py import Oracle
 
 N = 3000
+STEPS = 2
 
 
 def _batch():
@@ -36,13 +42,17 @@ def _rank(rank, world, port, out_dir):
     blob, reqs, arena, n_rules = _batch()
     lo, hi = shard.shard_bounds(len(reqs), world, rank)
     part, parena = shard.slice_batch(reqs, arena, lo, hi)
-    v, h = Oracle(blob, 1).match(part, parena, nthreads=2)
-    c = torch.from_numpy(_counters(v, h, 8, n_rules))
-    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    local = torch.zeros(8 + n_rules, dtype=torch.int64)   # this rank's cumulative counters
+    for step in range(1, STEPS + 1):
+        v, h = Oracle(blob, 1).match(part, parena, nthreads=2)
+        local += torch.from_numpy(_counters(v, h, 8, n_rules))
+        c = local.clone()                                    # out of place: `local` stays this rank's
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        if rank == 0:
+            np.save(os.path.join(out_dir, f"counters_{step}.npy"), c.numpy())
     gathered = [None] * world
     dist.all_gather_object(gathered, (v.tobytes(), h.tobytes()))
     if rank == 0:
-        np.save(os.path.join(out_dir, "counters.npy"), c.numpy())
         vs = [np.frombuffer(b, dtype=records.VERDICT_DTYPE) for b, _ in gathered]
         hs = [np.frombuffer(x, dtype=np.uint32) for _, x in gathered]
         mv, mh = shard.merge_hits(vs, hs)
@@ -76,5 +86,6 @@ def test_two_rank_gloo_shards_match_single_batch(tmp_path):
     mh = np.load(tmp_path / "hits.npy")
     assert mv.tobytes() == v.tobytes()
     assert np.array_equal(mh, h)
-    assert np.array_equal(np.load(tmp_path / "counters.npy"), _counters(v, h, 8, n_rules))
+    for step in range(1, STEPS + 1):
+        assert np.array_equal(np.load(tmp_path / f"counters_{step}.npy"), step * _counters(v, h, 8, n_rules))
     assert len(h) > 0
