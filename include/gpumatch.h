@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 1u
+#define GM_ABI_VERSION 2u
 
 /* ---------------------------------------------------------------- status codes */
 #define GM_OK            0
@@ -81,13 +81,20 @@ typedef struct gm_req {
 #define GM_REQ_HTTPS   0x01u  /* connection is TLS: $scheme = https, $https = on          */
 #define GM_REQ_HTTP2   0x02u  /* $http2 = "h2"                                            */
 #define GM_REQ_HTTP10  0x04u  /* request line protocol HTTP/1.0 (else HTTP/1.1 / HTTP/2.0) */
+#define GM_REQ_INVALID 0x08u  /* the wire parser rejected the request (gm_parse_requests): the  */
+                              /* HTTP status nginx answers is in pad0[1] | pad0[2] << 8, and   */
+                              /* gm_match_batch answers GM_ACT_BAD_REQUEST with that status     */
 
 typedef struct gm_batch {
     const gm_req  *reqs;      /* n headers (device pointer unless GM_BATCH_HOST)          */
     const uint8_t *arena;     /* payload arena (device pointer unless GM_BATCH_HOST)      */
-    uint64_t       arena_len;
+    uint64_t       arena_len; /* bytes; with arena_len_dev: the arena's capacity          */
     uint32_t       n;
     uint32_t       flags;     /* GM_BATCH_*                                               */
+    /* optional device u64 holding the arena's length (e.g. written by gm_parse_requests on
+     * the same stream): the kernels read it on the device, so parse -> match needs no host
+     * round trip.  NULL: arena_len is the length. */
+    const uint64_t *arena_len_dev;
 } gm_batch;
 
 #define GM_BATCH_HOST  0x1u   /* reqs/arena/out/hit_ids are host memory: staged through HBM */
@@ -224,6 +231,35 @@ int         gm_counters_global(gm_ctx *ctx, uint64_t *out, size_t n);
  * the stream's batch status, so the sync reports no match-batch overflow). */
 int         gm_normalize_uris(gm_ctx *ctx, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
                               uint32_t n, uint8_t *out, uint32_t *out_len, void *stream);
+
+/* ---------------------------------------------------------------- HTTP/1.x wire parser
+ * (the on-the-wire step before the engine.)  nginx's request-line / header /
+ * body handling (ngx_http_parse_request_line, ngx_http_parse_header_line,
+ * ngx_http_parse_complex_uri, ngx_http_process_request_headers, the chunked body filter) turns
+ * raw request bytes into exactly the fields the templates' rules read: $request_method, $uri,
+ * $args, $request_uri, $host, the header lines behind $http_* / $cookie_* (nginx.virtualserver.
+ * tmpl:25-31 maps) and the body the Wallarm phase scans.  See DESIGN.md §4 for the rules. */
+typedef struct gm_wire_msg {
+    uint64_t off;             /* the request's bytes: wire[off .. off + len)               */
+    uint32_t len;
+    uint16_t port;            /* local listen port ($server_port)                          */
+    uint16_t remote_port;
+    uint8_t  flags;           /* connection: GM_REQ_HTTPS, GM_REQ_HTTP2                    */
+    uint8_t  raddr_len;       /* $remote_addr text length, <= 40                           */
+    uint8_t  pad[2];
+    uint8_t  rid[16];         /* $request_id raw bytes                                     */
+    uint8_t  raddr[40];       /* $remote_addr text                                         */
+} gm_wire_msg;                /* 80 B */
+
+/* Parse n requests into gm_req records + a payload arena (field order of gm_req, records
+ * 16-B aligned and packed in request order).  Device pointers, asynchronous on `stream`;
+ * *arena_len_dev (device) receives the arena's length -- hand it to gm_match_batch through
+ * gm_batch.arena_len_dev, with arena_cap as gm_batch.arena_len.  A request nginx would reject
+ * gets GM_REQ_INVALID and its status (400 / 501 / 505).  arena_cap >= the sum over requests of
+ * align16(2 * len + raddr_len) always suffices; gm_sync reports GM_E_OVERFLOW if it is exceeded. */
+int         gm_parse_requests(gm_ctx *ctx, const uint8_t *wire, const gm_wire_msg *msgs, uint32_t n,
+                              gm_req *reqs, uint8_t *arena, uint64_t arena_cap, uint64_t *arena_len_dev,
+                              void *stream);
 
 int         gm_stats(gm_ctx *ctx, gm_stats_t *out);
 /* Message of the calling thread's last failing call (thread-local; ctx is not consulted). */

@@ -20,6 +20,9 @@ Restated reference code (wallarm/ingress-plus 1.5.5-wallarm-r1):
 * ``internal/configs/virtualserver.go:444-472``  generateSSLConfig
 * ``internal/configs/configurator.go:172-190,556-571`` TLS pem names, conf.d file names
 * ``internal/k8s/controller.go:1827-1886``       getMinionsForMaster (path dedupe, first wins)
+* ``internal/k8s/controller.go:1519-1591``       createVirtualServer (VSR resolution + endpoints)
+* ``pkg/apis/configuration/validation/validation.go:15-476`` ValidateVirtualServer /
+  ValidateVirtualServerRouteForVirtualServer (the legal input domain: what never reaches nginx)
 * templates ``version1/nginx.ingress.tmpl``, ``version1/nginx.tmpl:81-129``,
   ``version2/nginx.virtualserver.tmpl`` -- rendered here by ``render_*``; only the
   directive *sequence* matters to the engine, whitespace is free.
@@ -31,6 +34,7 @@ Go unit tests' expected structs can be transcribed 1:1 into ``tests/golden``.
 from __future__ import annotations
 
 import copy
+import re
 
 PEM_MISSING = "/etc/nginx/secrets/default"      # configurator.go:19
 PEM_WILDCARD = "/etc/nginx/secrets/wildcard"    # configurator.go:20
@@ -65,7 +69,7 @@ def default_config_params() -> dict:
         "Wallarm": None,
         "ServerSnippets": [],
         "LocationSnippets": [],
-        "HSTS": False,
+        "HSTS": False, "HSTSMaxAge": 2592000, "HSTSIncludeSubdomains": False, "HSTSBehindProxy": False,
     }
 
 
@@ -195,7 +199,9 @@ def generate_nginx_cfg(ing_ex: dict, pems: dict, is_minion: bool, base: dict) ->
         host = rule.get("host", "")
         server = {"Name": host, "ServerTokens": p["ServerTokens"], "HTTP2": p["HTTP2"],
                   "RedirectToHTTPS": p["RedirectToHTTPS"], "SSLRedirect": p["SSLRedirect"],
-                  "ProxyProtocol": p["ProxyProtocol"], "HSTS": p["HSTS"], "StatusZone": host,
+                  "ProxyProtocol": p["ProxyProtocol"], "HSTS": p["HSTS"], "HSTSMaxAge": p["HSTSMaxAge"],
+                  "HSTSIncludeSubdomains": p["HSTSIncludeSubdomains"], "HSTSBehindProxy": p["HSTSBehindProxy"],
+                  "StatusZone": host,
                   "Ports": list(p["Ports"]), "SSLPorts": list(p["SSLPorts"]), "Wallarm": p["Wallarm"],
                   "SSL": False, "SSLCertificate": "", "SSLCertificateKey": "", "SSLCiphers": "",
                   "GRPCOnly": False, "ServerSnippets": list(p["ServerSnippets"])}
@@ -482,6 +488,272 @@ def generate_virtual_server_config(vs_ex: dict, pem_name: str, base: dict) -> di
             "Keepalive": str(p["Keepalive"]) if p["Keepalive"] > 0 else ""}
 
 
+# --------------------------------------------------------------------------- validation
+# pkg/apis/configuration/validation/validation.go: a VirtualServer (or a VirtualServerRoute for its
+# VirtualServer) that fails validation is never rendered -- the controller deletes its config
+# (controller.go:608-617) or skips the VSR (controller.go:1572-1577).  Each check returns a list
+# of error strings (empty = valid), like the Go field.ErrorList.
+
+_DNS1123_LABEL = r"[a-z0-9]([-a-z0-9]*[a-z0-9])?"
+_DNS1123_SUBDOMAIN = re.compile(r"^" + _DNS1123_LABEL + r"(\." + _DNS1123_LABEL + r")*$")
+_DNS1035_LABEL = re.compile(r"^[a-z]([-a-z0-9]*[a-z0-9])?$")
+_QUALIFIED_NAME = re.compile(r"^([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9]$")
+_HTTP_HEADER_NAME = re.compile(r"^[-A-Za-z0-9]+$")
+_PATH = re.compile(r"^/[^\s{};]*$")                      # validation.go:244-263 pathFmt
+_COOKIE_ARG = re.compile(r"^[_A-Za-z0-9]+$")             # validation.go:327-349
+_MATCH_VALUE = re.compile(r'^([^"\\]|\\.)*$', re.S)      # validation.go:381-398 matchValueFmt
+VALID_VARIABLE_NAMES = frozenset(("$args", "$http2", "$https", "$remote_addr", "$remote_port", "$query_string",
+                                  "$request", "$request_body", "$request_uri", "$request_method", "$scheme"))
+
+
+def _is_dns1123_subdomain(s):
+    return len(s) <= 253 and bool(_DNS1123_SUBDOMAIN.match(s))
+
+
+def _is_dns1035_label(s):
+    return len(s) <= 63 and bool(_DNS1035_LABEL.match(s))
+
+
+def _is_qualified_name(s):
+    """k8s IsQualifiedName: [prefix/]name, prefix a DNS-1123 subdomain, name <= 63."""
+    parts = s.split("/")
+    if len(parts) == 2:
+        prefix, name = parts
+        if not prefix or not _is_dns1123_subdomain(prefix):
+            return False
+    elif len(parts) == 1:
+        name = parts[0]
+    else:
+        return False
+    return 0 < len(name) <= 63 and bool(_QUALIFIED_NAME.match(name))
+
+
+def validate_host(host):
+    if host == "":
+        return ["host: Required"]
+    return [] if _is_dns1123_subdomain(host) else [f"host {host!r}: not a DNS-1123 subdomain"]
+
+
+def validate_path(path):
+    """validation.go:244-263."""
+    if path == "":
+        return ["path: Required"]
+    return [] if _PATH.match(path) else [f"path {path!r}: must start with / and have no whitespace, {{, }} or ;"]
+
+
+def is_valid_match_value(value):
+    """validation.go:390-398: every '"' escaped, no trailing unescaped '\\'."""
+    return [] if _MATCH_VALUE.match(value) else [f"value {value!r}: unescaped quote or trailing backslash"]
+
+
+def _validate_name_1035(name, what):
+    if name == "":
+        return [f"{what}: Required"]
+    return [] if _is_dns1035_label(name) else [f"{what} {name!r}: not a DNS-1035 label"]
+
+
+def validate_upstreams(upstreams):
+    """validation.go:76-100 -> (errors, names)."""
+    errs, names = [], set()
+    for u in upstreams or []:
+        e = _validate_name_1035(u.get("name", ""), "upstream name")
+        if e:
+            errs += e
+        elif u["name"] in names:
+            errs.append(f"upstream name {u['name']!r}: Duplicate")
+        else:
+            names.add(u["name"])
+        errs += _validate_name_1035(u.get("service", ""), "service")
+        port = u.get("port", 0)
+        if not (isinstance(port, int) and 1 <= port <= 65535):
+            errs.append(f"port {port!r}: not a valid port number")
+    return errs, names
+
+
+def _validate_referenced_upstream(name, names):
+    e = _validate_name_1035(name or "", "upstream")
+    if e:
+        return e
+    return [] if name in names else [f"upstream {name!r}: Not found"]
+
+
+def validate_splits(splits, names):
+    """validation.go:216-242."""
+    if len(splits or []) < 2:
+        return ["splits: must include at least 2 splits"]
+    errs, total = [], 0
+    for s in splits:
+        w = s.get("weight", 0)
+        if not (1 <= w <= 99):
+            errs.append(f"weight {w}: must be between 1 and 99")
+        errs += _validate_referenced_upstream(s.get("upstream", ""), names)
+        total += w
+    if total != 100:
+        errs.append("splits: the sum of the weights must be 100")
+    return errs
+
+
+def validate_condition(c):
+    """validation.go:289-325."""
+    errs, count = [], 0
+    if c.get("header"):
+        if not _HTTP_HEADER_NAME.match(c["header"]):
+            errs.append(f"header {c['header']!r}: not a valid HTTP header name")
+        count += 1
+    if c.get("cookie"):
+        if not _COOKIE_ARG.match(c["cookie"]):
+            errs.append(f"cookie {c['cookie']!r}: invalid name")
+        count += 1
+    if c.get("argument"):
+        if not _COOKIE_ARG.match(c["argument"]):
+            errs.append(f"argument {c['argument']!r}: invalid name")
+        count += 1
+    if c.get("variable"):
+        v = c["variable"]
+        if not v.startswith("$"):
+            errs.append(f"variable {v!r}: must start with $")
+        elif v not in VALID_VARIABLE_NAMES:
+            errs.append(f"variable {v!r}: not allowed")
+        count += 1
+    if count != 1:
+        errs.append("condition: must specify exactly one of header, cookie, argument or variable")
+    return errs
+
+
+def validate_match(m, n_conditions, names):
+    """validation.go:367-388."""
+    errs = []
+    vals = m.get("values") or []
+    if len(vals) != n_conditions:
+        errs.append(f"values: must specify {n_conditions} values")
+    for v in vals:
+        errs += is_valid_match_value(v)
+    return errs + _validate_referenced_upstream(m.get("upstream", ""), names)
+
+
+def validate_rules(rules, names):
+    """validation.go:265-287."""
+    errs = []
+    conds = rules.get("conditions") or []
+    if not conds:
+        errs.append("conditions: Required")
+    for c in conds:
+        errs += validate_condition(c)
+    matches = rules.get("matches") or []
+    if not matches:
+        errs.append("matches: Required")
+    for m in matches:
+        errs += validate_match(m, len(conds), names)
+    return errs + _validate_referenced_upstream(rules.get("defaultUpstream", ""), names)
+
+
+def validate_route(r, names, route_forbidden):
+    """validation.go:148-190."""
+    errs = validate_path(r.get("path", ""))
+    count = 0
+    if r.get("upstream"):
+        errs += _validate_referenced_upstream(r["upstream"], names)
+        count += 1
+    if r.get("splits"):
+        errs += validate_splits(r["splits"], names)
+        count += 1
+    if r.get("rules") is not None:
+        errs += validate_rules(r["rules"], names)
+        count += 1
+    if r.get("route"):
+        if route_forbidden:
+            errs.append("route: is not allowed")
+        else:
+            if not _is_qualified_name(r["route"]):
+                errs.append(f"route {r['route']!r}: not a qualified name")
+            count += 1
+    if count != 1:
+        errs.append("route: must specify exactly one of upstream, splits, rules" + ("" if route_forbidden else " or route"))
+    return errs
+
+
+def validate_virtual_server(vs):
+    """ValidateVirtualServer (validation.go:15-33)."""
+    spec = vs.get("spec") or {}
+    errs = validate_host(spec.get("host", ""))
+    tls = spec.get("tls")
+    if tls is not None:
+        sec = tls.get("secret", "")
+        errs += ["tls secret: Required"] if sec == "" else ([] if _is_dns1123_subdomain(sec) else ["tls secret: invalid"])
+    ue, names = validate_upstreams(spec.get("upstreams"))
+    errs += ue
+    paths = set()
+    for r in spec.get("routes") or []:
+        re_ = validate_route(r, names, False)
+        if re_:
+            errs += re_
+        elif r["path"] in paths:
+            errs.append(f"path {r['path']!r}: Duplicate")
+        else:
+            paths.add(r["path"])
+    return errs
+
+
+def validate_virtual_server_route(vsr, vs_host="", path_prefix="/"):
+    """ValidateVirtualServerRouteForVirtualServer (validation.go:411-476)."""
+    spec = vsr.get("spec") or {}
+    host = spec.get("host", "")
+    errs = validate_host(host)
+    if vs_host and host != vs_host:
+        errs.append(f"host {host!r}: must be equal to {vs_host!r}")
+    ue, names = validate_upstreams(spec.get("upstreams"))
+    errs += ue
+    paths = set()
+    for r in spec.get("subroutes") or []:
+        re_ = validate_route(r, names, True)
+        if path_prefix and not r.get("path", "").startswith(path_prefix):
+            re_.append(f"path {r.get('path')!r}: must start with {path_prefix!r}")
+        if re_:
+            errs += re_
+        elif r["path"] in paths:
+            errs.append(f"path {r['path']!r}: Duplicate")
+        else:
+            paths.add(r["path"])
+    return errs
+
+
+def generate_endpoints_key(ns, service, port):
+    """configs.GenerateEndpointsKey: "<ns>/<service>:<port>"."""
+    return f"{ns}/{service}:{port}"
+
+
+def create_virtual_server(vs, vsr_store, endpoints_of=None):
+    """controller.go:1519-1591: the VirtualServerEx the Configurator receives -- every `route:`
+    reference resolved in the VSR store ({"ns/name": vsr}, a missing namespace meaning the VS's),
+    skipped with a warning when missing or invalid for this VS (host, path prefix); endpoints for
+    the VS's and the accepted VSRs' upstreams (endpoints_of(ns, service, port) -> ["ip:port"]).
+    Returns (vs_ex, vsr_errors)."""
+    endpoints_of = endpoints_of or (lambda ns, svc, port: [])
+    vns, _ = _meta(vs)
+    spec = vs["spec"]
+    eps = {}
+    for u in spec.get("upstreams") or []:
+        eps[generate_endpoints_key(vns, u["service"], u["port"])] = endpoints_of(vns, u["service"], u["port"])
+    vsrs, errors = [], []
+    for r in spec.get("routes") or []:
+        if not r.get("route"):
+            continue
+        key = r["route"] if "/" in r["route"] else f"{vns}/{r['route']}"
+        vsr = vsr_store.get(key)
+        if vsr is None:
+            errors.append((key, "VirtualServerRoute doesn't exist"))
+            continue
+        e = validate_virtual_server_route(vsr, spec["host"], r["path"])
+        if e:
+            errors.append((key, "; ".join(e)))
+            continue
+        vsrs.append(vsr)
+        rns, _ = _meta(vsr)
+        for u in vsr["spec"].get("upstreams") or []:
+            eps[generate_endpoints_key(rns, u["service"], u["port"])] = endpoints_of(rns, u["service"], u["port"])
+    return {"VirtualServer": vs, "Endpoints": eps, "VirtualServerRoutes": vsrs}, errors
+
+
 def vs_file_name(vs) -> str:
     """configurator.go:564-566."""
     ns, name = _meta(vs)
@@ -678,12 +950,21 @@ def mergeable_files(masters, minions, base=None, wildcard=False, secrets=()):
     return out
 
 
-def virtual_server_files(vss, base=None, vsrs_by_vs=None, pem_name="/etc/nginx/secrets/default-cafe-secret"):
+def virtual_server_files(vss, base=None, vsrs_by_vs=None, pem_name="/etc/nginx/secrets/default-cafe-secret",
+                         vsr_store=None, endpoints_of=None):
+    """Configurator.AddOrUpdateVirtualServer for each VS -> {file stem: text}.  With a VSR store
+    the controller's resolution applies (create_virtual_server); an invalid VS gets no file
+    (controller.go:608-617).  ``vsrs_by_vs`` ({"ns/name": [vsr]}) bypasses the resolution."""
     base = base or default_config_params()
     out = {}
     for vs in vss:
-        key = "%s/%s" % _meta(vs)
-        ex = {"VirtualServer": vs, "Endpoints": {}, "VirtualServerRoutes": (vsrs_by_vs or {}).get(key, [])}
+        if validate_virtual_server(vs):
+            continue
+        if vsr_store is not None:
+            ex, _ = create_virtual_server(vs, vsr_store, endpoints_of)
+        else:
+            key = "%s/%s" % _meta(vs)
+            ex = {"VirtualServer": vs, "Endpoints": {}, "VirtualServerRoutes": (vsrs_by_vs or {}).get(key, [])}
         cfg = generate_virtual_server_config(ex, pem_name, base)
         out[vs_file_name(vs)] = render_virtual_server(cfg)
     return out

@@ -15,6 +15,15 @@ tests assert, transcribed as data.
   examples.json           examples/complete-example/cafe-ingress.yaml,
                           examples-of-custom-resources/{advanced-routing,traffic-splitting}/*.yaml,
                           examples/mergeable-ingress-types/{cafe-master,coffee-minion,tea-minion}.yaml
+  reference_configs.json  internal/configs/virtualserver_test.go:163-731 (whole-VS configs incl.
+                          VirtualServerRoutes), internal/configs/ingress_test.go:75-107 (missing /
+                          wildcard TLS secret), :255-270 + :347-563 (mergeable master + minions),
+                          pkg/apis/configuration/validation/validation_test.go:642-672 (paths),
+                          :1157-1188 (match values)
+  e2e_routes.json         tests/suite/test_v_s_route.py:260-322 with tests/data/virtual-server-route/
+                          (VSR delegation, no-endpoint 502, deleted VSR 404) and
+                          tests/suite/test_virtual_server.py:25-73 with tests/data/virtual-server/
+                          standard/ (host change: old host 404, restore; backend port change 502)
 """
 
 import json
@@ -170,6 +179,171 @@ def main():
                               y("examples/mergeable-ingress-types/tea-minion.yaml")[0]],
     }
     dump("examples.json", ex)
+
+    # ---- virtualserver_test.go:163-731: generateVirtualServerConfig on a VirtualServerEx
+    def ups(name, svc):
+        return {"name": name, "service": svc, "port": 80}
+    vsr_coffee = lambda upstreams, sub: {"metadata": {"name": "coffee", "namespace": "default"},
+                                         "spec": {"host": "cafe.example.com", "upstreams": upstreams,
+                                                  "subroutes": [sub]}}
+    vs_cafe = lambda upstreams, tea: {"metadata": {"name": "cafe", "namespace": "default"},
+                                      "spec": {"host": "cafe.example.com", "upstreams": upstreams,
+                                               "routes": [tea, {"path": "/coffee", "route": "default/coffee"}]}}
+    eps4 = {"default/tea-svc-v1:80": ["10.0.0.20:80"], "default/tea-svc-v2:80": ["10.0.0.21:80"],
+            "default/coffee-svc-v1:80": ["10.0.0.30:80"], "default/coffee-svc-v2:80": ["10.0.0.31:80"]}
+    ups4 = [["vs_default_cafe_tea-v1", "10.0.0.20:80"], ["vs_default_cafe_tea-v2", "10.0.0.21:80"],
+            ["vs_default_cafe_vsr_default_coffee_coffee-v1", "10.0.0.30:80"],
+            ["vs_default_cafe_vsr_default_coffee_coffee-v2", "10.0.0.31:80"]]
+    vsc = {}
+    vsc["basic"] = {   # :163-282
+        "source": "internal/configs/virtualserver_test.go:163-282",
+        "vs": vs_cafe([ups("tea", "tea-svc")], {"path": "/tea", "upstream": "tea"}),
+        "vsrs": [vsr_coffee([ups("coffee", "coffee-svc")], {"path": "/coffee", "upstream": "coffee"})],
+        "endpoints": {"default/tea-svc:80": ["10.0.0.20:80"], "default/coffee-svc:80": ["10.0.0.30:80"]},
+        "params": {"ServerTokens": "off", "Keepalive": 16, "ServerSnippets": ["# server snippet"],
+                   "ProxyProtocol": True, "RedirectToHTTPS": True},
+        "expected": {
+            "Upstreams": [["vs_default_cafe_tea", "10.0.0.20:80"],
+                          ["vs_default_cafe_vsr_default_coffee_coffee", "10.0.0.30:80"]],
+            "SplitClients": [], "Maps": [],
+            "Server": {"ServerName": "cafe.example.com", "ProxyProtocol": True,
+                       "RedirectToHTTPSBasedOnXForwarderProto": True, "ServerTokens": "off",
+                       "Snippets": ["# server snippet"], "InternalRedirectLocations": [],
+                       "Locations": [["/tea", "http://vs_default_cafe_tea"],
+                                     ["/coffee", "http://vs_default_cafe_vsr_default_coffee_coffee"]]},
+            "Keepalive": "16"}}
+    vsc["splits"] = {   # :283-487
+        "source": "internal/configs/virtualserver_test.go:283-487",
+        "vs": vs_cafe([ups("tea-v1", "tea-svc-v1"), ups("tea-v2", "tea-svc-v2")],
+                      {"path": "/tea", "splits": [{"weight": 90, "upstream": "tea-v1"}, {"weight": 10, "upstream": "tea-v2"}]}),
+        "vsrs": [vsr_coffee([ups("coffee-v1", "coffee-svc-v1"), ups("coffee-v2", "coffee-svc-v2")],
+                            {"path": "/coffee", "splits": [{"weight": 40, "upstream": "coffee-v1"},
+                                                            {"weight": 60, "upstream": "coffee-v2"}]})],
+        "endpoints": eps4, "params": {},
+        "expected": {
+            "Upstreams": ups4,
+            "SplitClients": [
+                {"Source": "$request_id", "Variable": "$vs_default_cafe_splits_0",
+                 "Distributions": [{"Weight": "90%", "Value": "@splits_0_split_0"}, {"Weight": "10%", "Value": "@splits_0_split_1"}]},
+                {"Source": "$request_id", "Variable": "$vs_default_cafe_splits_1",
+                 "Distributions": [{"Weight": "40%", "Value": "@splits_1_split_0"}, {"Weight": "60%", "Value": "@splits_1_split_1"}]}],
+            "Maps": [],
+            "Server": {"ServerName": "cafe.example.com",
+                       "InternalRedirectLocations": [{"Path": "/tea", "Destination": "$vs_default_cafe_splits_0"},
+                                                     {"Path": "/coffee", "Destination": "$vs_default_cafe_splits_1"}],
+                       "Locations": [["@splits_0_split_0", "http://vs_default_cafe_tea-v1"],
+                                     ["@splits_0_split_1", "http://vs_default_cafe_tea-v2"],
+                                     ["@splits_1_split_0", "http://vs_default_cafe_vsr_default_coffee_coffee-v1"],
+                                     ["@splits_1_split_1", "http://vs_default_cafe_vsr_default_coffee_coffee-v2"]]}}}
+    def rmap(src_, var, val, res):
+        return {"Source": src_, "Variable": var, "Parameters": [{"Value": val, "Result": res[0]},
+                                                               {"Value": "default", "Result": res[1]}]}
+    vsc["rules"] = {   # :489-731
+        "source": "internal/configs/virtualserver_test.go:489-731",
+        "vs": vs_cafe([ups("tea-v1", "tea-svc-v1"), ups("tea-v2", "tea-svc-v2")],
+                      {"path": "/tea", "rules": {"conditions": [{"header": "x-version"}],
+                                                 "matches": [{"values": ["v2"], "upstream": "tea-v2"}],
+                                                 "defaultUpstream": "tea-v1"}}),
+        "vsrs": [vsr_coffee([ups("coffee-v1", "coffee-svc-v1"), ups("coffee-v2", "coffee-svc-v2")],
+                            {"path": "/coffee", "rules": {"conditions": [{"argument": "version"}],
+                                                          "matches": [{"values": ["v2"], "upstream": "coffee-v2"}],
+                                                          "defaultUpstream": "coffee-v1"}})],
+        "endpoints": eps4, "params": {},
+        "expected": {
+            "Upstreams": ups4, "SplitClients": [],
+            "Maps": [rmap("$http_x_version", "$vs_default_cafe_rules_0_match_0_cond_0", '"v2"', ["1", "0"]),
+                     rmap("$vs_default_cafe_rules_0_match_0_cond_0", "$vs_default_cafe_rules_0", "~^1",
+                          ["@rules_0_match_0", "@rules_0_default"]),
+                     rmap("$arg_version", "$vs_default_cafe_rules_1_match_0_cond_0", '"v2"', ["1", "0"]),
+                     rmap("$vs_default_cafe_rules_1_match_0_cond_0", "$vs_default_cafe_rules_1", "~^1",
+                          ["@rules_1_match_0", "@rules_1_default"])],
+            "Server": {"ServerName": "cafe.example.com",
+                       "InternalRedirectLocations": [{"Path": "/tea", "Destination": "$vs_default_cafe_rules_0"},
+                                                     {"Path": "/coffee", "Destination": "$vs_default_cafe_rules_1"}],
+                       "Locations": [["@rules_0_match_0", "http://vs_default_cafe_tea-v2"],
+                                     ["@rules_0_default", "http://vs_default_cafe_tea-v1"],
+                                     ["@rules_1_match_0", "http://vs_default_cafe_vsr_default_coffee_coffee-v2"],
+                                     ["@rules_1_default", "http://vs_default_cafe_vsr_default_coffee_coffee-v1"]]}}}
+
+    # ---- ingress_test.go:255-270 + 347-563 (mergeable), :75-107 (TLS secrets)
+    ann = lambda kind: {"kubernetes.io/ingress.class": "nginx", "nginx.org/mergeable-ingress-type": kind}
+    minion = lambda name, path, svc: {"metadata": {"name": name, "namespace": "default", "annotations": ann("minion")},
+                                      "spec": {"rules": [{"host": "cafe.example.com", "http": {"paths": [
+                                          {"path": path, "backend": {"serviceName": svc, "servicePort": "80"}}]}}]}}
+    mergeable = {
+        "source": "internal/configs/ingress_test.go:255-270,347-563",
+        "master": {"metadata": {"name": "cafe-ingress-master", "namespace": "default", "annotations": ann("master")},
+                   "spec": {"tls": [{"hosts": ["cafe.example.com"], "secretName": "cafe-secret"}],
+                            "rules": [{"host": "cafe.example.com", "http": {"paths": []}}]}},
+        "master_endpoints": {"coffee-svc80": ["10.0.0.1:80"], "tea-svc80": ["10.0.0.2:80"]},
+        "minions": [[minion("cafe-ingress-coffee-minion", "/coffee", "coffee-svc"), {"coffee-svc80": ["10.0.0.1:80"]}],
+                    [minion("cafe-ingress-tea-minion", "/tea", "tea-svc"), {"tea-svc80": ["10.0.0.2:80"]}]],
+        "pems": {"cafe.example.com": "/etc/nginx/secrets/default-cafe-secret"},
+        "expected": {
+            "upstreams": [["default-cafe-ingress-coffee-minion-cafe.example.com-coffee-svc-80", "random two least_conn",
+                           [["10.0.0.1", "80", 1, "10s"]]],
+                          ["default-cafe-ingress-tea-minion-cafe.example.com-tea-svc-80", "random two least_conn",
+                           [["10.0.0.2", "80", 1, "10s"]]]],
+            "server": {"Name": "cafe.example.com", "ServerTokens": "on", "SSL": True,
+                       "SSLCertificate": "/etc/nginx/secrets/default-cafe-secret",
+                       "SSLCertificateKey": "/etc/nginx/secrets/default-cafe-secret",
+                       "StatusZone": "cafe.example.com", "HSTSMaxAge": 2592000, "Ports": [80], "SSLPorts": [443],
+                       "SSLRedirect": True},
+            "locations": [["/coffee", "default-cafe-ingress-coffee-minion-cafe.example.com-coffee-svc-80",
+                           "cafe-ingress-coffee-minion", "60s", "60s", "1m", True],
+                          ["/tea", "default-cafe-ingress-tea-minion-cafe.example.com-tea-svc-80",
+                           "cafe-ingress-tea-minion", "60s", "60s", "1m", True]],
+            "ingress": ["cafe-ingress-master", "default"]}}
+    tls = {"source": "internal/configs/ingress_test.go:75-107, configurator.go:19-20",
+           "missing": {"pem": "/etc/nginx/secrets/default", "expect_ciphers": "NULL"},
+           "wildcard": {"pem": "/etc/nginx/secrets/wildcard", "expect_certificate": "/etc/nginx/secrets/wildcard",
+                        "expect_certificate_key": "/etc/nginx/secrets/wildcard"}}
+    validation = {
+        "source": "pkg/apis/configuration/validation/validation_test.go:642-672,1157-1188",
+        "valid_paths": ["/", "/path", "/a-1/_A/"],
+        "invalid_paths": ["", " /", "/ ", "/{", "/}", "/abc;"],
+        "valid_match_values": ["abc", "123", '\\" \n\t\tabc\\"'.replace("\\n", "\n").replace("\\t", "\t"), '\\"'],
+        "invalid_match_values": ['"', "\\", 'abc"', "abc\\\\\\", 'a"b'],
+    }
+    dump("reference_configs.json", {"vs_configs": vsc, "mergeable": mergeable, "tls": tls, "validation": validation})
+
+    # ---- e2e: VirtualServerRoute (test_v_s_route.py) and VirtualServer (test_virtual_server.py)
+    vsr_dir = "tests/data/virtual-server-route/"
+    vs_dir = "tests/data/virtual-server/standard/"
+    dump("e2e_routes.json", {
+        "v_s_route": {
+            "source": "tests/suite/test_v_s_route.py:100-160,260-322",
+            # the fixture creates the VS and VSR "backends" in the VS's first route namespace and
+            # VSR "backend2" in the second (get_route_namespace_from_vs_yaml)
+            "vs": y(vsr_dir + "standard/virtual-server.yaml")[0], "vs_namespace": "backends-namespace",
+            "vsrs": [["backends-namespace", y(vsr_dir + "route-multiple.yaml")[0]],
+                     ["backend2-namespace", y(vsr_dir + "route-single.yaml")[0]]],
+            "steps": [
+                {"step": "initial", "paths": [["/backends/backend1", 200], ["/backends/backend3", 200], ["/backend2", 200]]},
+                # Step 4: backend1-svc port 80 -> 8080: no endpoints for backend1-svc:80 -> 502
+                {"step": "backend1 port changed", "no_endpoints": ["backends-namespace/backend1-svc:80"],
+                 "paths": [["/backends/backend1", 502], ["/backends/backend3", 200]]},
+                # Step 6: VSR backends deleted -> its paths 404, the other VSR still 200
+                {"step": "vsr deleted", "deleted": ["backends-namespace/backends"],
+                 "paths": [["/backends/backend1", 404], ["/backends/backend3", 404], ["/backend2", 200]]}]},
+        "virtual_server": {
+            "source": "tests/suite/test_virtual_server.py:25-73",
+            "vs": y(vs_dir + "virtual-server.yaml")[0], "vs_updated": y(vs_dir + "virtual-server-updated.yaml")[0],
+            # the test builds URLs f"...:{port}/{path}" with paths that start with "/": the request
+            # path is "//backend1" (nginx merges the slashes into $uri "/backend1")
+            "steps": [
+                {"step": "updated", "config": "vs_updated",
+                 "requests": [["virtual-server.example.com", "//backend1", 404], ["virtual-server.example.com", "//backend2", 404],
+                              ["virtual-server-up.example.com", "//updated-backend1", 200],
+                              ["virtual-server-up.example.com", "//updated-backend2", 200]]},
+                {"step": "restored", "config": "vs",
+                 "requests": [["virtual-server-up.example.com", "//updated-backend1", 404],
+                              ["virtual-server-up.example.com", "//updated-backend2", 404],
+                              ["virtual-server.example.com", "//backend1", 200], ["virtual-server.example.com", "//backend2", 200]]},
+                {"step": "backend1 port changed", "config": "vs", "no_endpoints": ["test-namespace/backend1-svc:80"],
+                 "requests": [["virtual-server.example.com", "//backend1", 502], ["virtual-server.example.com", "//backend2", 200]]}],
+            "vs_namespace": "test-namespace"},
+    })
 
 
 if __name__ == "__main__":

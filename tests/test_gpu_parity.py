@@ -281,3 +281,52 @@ def test_regex_location_prefilter_edges(eng):
     reqs, arena = records.from_dicts([{"host": "e.example.com", "uri": u} for u in uris])
     got, gh, exp, eh = run_both(eng, b, reqs, arena)
     assert_verdicts_equal(got, exp, gh, eh, "regex prefilter edges")
+
+
+GRPC_CONF = """
+http {
+  upstream g1 { server 1.1.1.1; }
+  upstream u1 { server 1.1.1.2; }
+  server {
+    listen 80 default_server;
+    server_name g.example.com;
+    location /grpc/ { grpc_pass grpc://g1; }
+    location /grpcs { grpc_pass grpcs://g1; }
+    location = /r304 { return 304; }
+    location = /r307 { return 307; }
+    location /nested { proxy_pass http://u1; if ($arg_x) { return 403; } }
+    location / { proxy_pass http://u1; }
+  }
+  server {
+    listen 80;
+    server_name rw.example.com;
+    if ($http_x_early = 'yes') { return 418; }
+    rewrite ^/old/(.*)$ /new/$1 last;
+    location / { proxy_pass http://u1; }
+  }
+}"""
+
+
+def test_grpc_return_and_unsupported_constructs_on_gpu(eng):
+    """grpc_pass proxies like proxy_pass (incl. auto_redirect, nginx.org/grpc-services,
+    version1/nginx.ingress.tmpl:154-158); `return 304` is not a redirect; a nested `if` in a
+    location and a server-level `rewrite` defer to nginx (GM_ACT_UNSUPPORTED), counted."""
+    b = blob.make_blob(GRPC_CONF, {})
+    items = [{"host": "g.example.com", "uri": u} for u in ("/grpc/x", "/grpc", "/grpcs/a", "/r304", "/r307",
+                                                           "/nested/a", "/other")]
+    items += [{"host": "rw.example.com", "uri": "/old/a"},
+              {"host": "rw.example.com", "uri": "/x", "headers": [("X-Early", "yes")]}]
+    reqs, arena = records.from_dicts(items)
+    got, gh, exp, eh = run_both(eng, b, reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "grpc / return / unsupported")
+    ups = upstream_table(b)
+    assert got[0]["action"] == 0 and ups[got[0]["upstream_id"]] == "g1"
+    assert got[1]["action"] == 3 and got[1]["status"] == 301          # auto_redirect for grpc_pass
+    assert got[2]["action"] == 0 and ups[got[2]["upstream_id"]] == "g1"
+    assert got[3]["action"] == 2 and got[3]["status"] == 304
+    assert got[4]["action"] == 1 and got[4]["status"] == 307
+    assert got[5]["action"] == 8 and got[6]["action"] == 0
+    assert got[7]["action"] == 8                                       # server rewrite reached
+    assert got[8]["action"] == 2 and got[8]["status"] == 418           # the `if` before it answers first
+    eng.load(b, 2)
+    assert eng.stats()["n_rejected_other"] == 2
