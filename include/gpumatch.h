@@ -53,7 +53,8 @@ extern "C" {
  * stored):
  *     uri | args | hdrs | body | host | method | ruri | raddr
  * The first four are the WAF-scanned zones.  `hdrs` is the header block exactly as parsed:
- * lines "Name: value\r\n" (single space after ':' not required; OWS trimmed by the producer).
+ * lines "Name: value\r\n" (the space after ':' optional; leading / trailing spaces of a value are
+ * not part of it, tabs are -- nginx's header parser).
  * `uri` is nginx's normalised $uri; `args` is $args without '?'; `host` is the raw Host header
  * value (host_len == 0: header absent); `ruri` is the raw $request_uri (ruri_len == 0: derived
  * as uri ["?" args]); `raddr` is $remote_addr text.  $request_id is the 16 raw random bytes in
@@ -249,6 +250,7 @@ typedef struct gm_wire_msg {
     uint8_t  pad[2];
     uint8_t  rid[16];         /* $request_id raw bytes                                     */
     uint8_t  raddr[40];       /* $remote_addr text                                         */
+    uint8_t  pad2[4];
 } gm_wire_msg;                /* 80 B */
 
 /* Parse n requests into gm_req records + a payload arena (field order of gm_req, records

@@ -21,6 +21,8 @@ struct gm_ctx;
 /* The last batch's device status words (counts, profiling counters) as of the last gm_sync;
  * returns the number copied. */
 int gm_debug_status(struct gm_ctx *ctx, uint32_t *out, size_t n);
+/* the last gm_parse_requests' per-request slot sizes (its size pass) on `stream` */
+int gm_debug_wire_sizes(struct gm_ctx *ctx, void *stream, uint64_t *out, size_t n);
 /* DServer words of server `sid`, then its (dfa, loc) regex-location pairs; returns words written. */
 int gm_debug_server(struct gm_ctx *ctx, uint32_t sid, uint32_t *out, size_t cap);
 int gm_debug_waf_keys(struct gm_ctx *ctx, uint32_t *out, size_t cap);

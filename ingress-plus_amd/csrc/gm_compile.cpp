@@ -1385,19 +1385,17 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         }
         buckets.back().second.second++;
     }
-    // probes per window: pk = 2 or 3 (K = 4 or 6 bits), whichever minimises scan + verify cost:
-    // pk = 3 costs ~20 % more scan time per probe (measured: 4.2 -> 5.9 ms on C4); a false
-    // positive costs ~20 probes' worth (its 32-byte record and the stage-2 context test)
+    // probes per window: K = 4 bits as one bit per byte (BLOOM_PK_PERM: 2 VALU ops per probe on
+    // the device), or pk = 3 packed shifts (K = 6, 4 ops) when that cuts the modelled false
+    // positives enough: a false positive costs ~20 probes' worth (its 32-byte record and the
+    // stage-2 context test)
     uint32_t bloom_pk = BLOOM_PK_DEFAULT, bloom_mul = kBloomMuls[0];
     if (!keys.empty()) {
-        int forced = 0;
-        if (const char *ev = getenv("GM_BLOOM_PK")) forced = std::min(3, std::max(1, atoi(ev)));   // tuning knob
-        if (forced) bloom_pk = forced;
         BloomChoice b = choose_bloom_mul(keys, bloom_pk, KM, waf_a);
-        if (!forced) {
+        {
             std::vector<uint32_t> f3(BLOOM_WORDS, 0);
             BloomChoice b3 = choose_bloom_mul(keys, 3, KM, f3);
-            if (0.2 + 20.0 * b3.fp < 20.0 * b.fp) { b = b3; bloom_pk = 3; waf_a.swap(f3); }
+            if (0.4 + 20.0 * b3.fp < 20.0 * b.fp) { b = b3; bloom_pk = 3; waf_a.swap(f3); }
         }
         bloom_mul = b.mul;
         st.bloom_fp_ppm = (uint32_t)std::min(1e9, b.fp * 1e6);

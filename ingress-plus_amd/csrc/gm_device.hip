@@ -41,6 +41,7 @@ struct Rec {
     uint32_t uri_len, args_len, hdr_len, body_len;
     uint32_t host_len, method_len, ruri_len, raddr_len;
     uint32_t port, rport, flags;
+    uint32_t bad_status;     // GM_REQ_INVALID: the wire parser's HTTP status (pad0[1..2])
     uint32_t rid[4];
 };
 
@@ -51,7 +52,7 @@ __device__ __forceinline__ Rec load_rec(const gm_req *r) {
     x.base = (uint64_t)a.x | ((uint64_t)a.y << 32);
     x.uri_len = a.z; x.args_len = a.w; x.hdr_len = b.x; x.body_len = b.y;
     x.host_len = b.z & 0xFFFF; x.method_len = b.z >> 16; x.ruri_len = b.w & 0xFFFF; x.raddr_len = b.w >> 16;
-    x.port = c.x & 0xFFFF; x.rport = c.x >> 16; x.flags = c.y & 0xFF;
+    x.port = c.x & 0xFFFF; x.rport = c.x >> 16; x.flags = c.y & 0xFF; x.bad_status = c.y >> 16;   // pad0[1] | pad0[2] << 8
     x.rid[0] = c.z; x.rid[1] = c.w; x.rid[2] = d.x; x.rid[3] = d.y;
     return x;
 }
@@ -131,7 +132,7 @@ __device__ uint64_t find_byte2(const uint8_t *A, uint64_t p, uint64_t e, uint32_
     return e;
 }
 
-// iterate "Name: value\r\n" lines; returns false at end
+// iterate "Name: value\r\n" lines (ngx_http_parse_header_line); returns false at end
 struct HdrIt { uint64_t pos, end; };
 __device__ bool hdr_next(const uint8_t *A, HdrIt &it, uint64_t &ns, uint32_t &nl, uint64_t &vs, uint32_t &vl) {
     while (it.pos < it.end) {
@@ -143,10 +144,11 @@ __device__ bool hdr_next(const uint8_t *A, HdrIt &it, uint64_t &ns, uint32_t &nl
         const uint64_t c = find_byte(A, st, le, ':');
         if (c >= le) continue;
         ns = st; nl = (uint32_t)(c - st);
+        // the value without leading / trailing spaces (nginx skips ' ' only: a tab is value)
         uint64_t v0 = c + 1;
-        while (v0 < le && (A[v0] == ' ' || A[v0] == '\t')) v0++;
+        while (v0 < le && A[v0] == ' ') v0++;
         uint64_t v1 = le;
-        while (v1 > v0 && (A[v1 - 1] == ' ' || A[v1 - 1] == '\t')) v1--;
+        while (v1 > v0 && A[v1 - 1] == ' ') v1--;
         vs = v0; vl = (uint32_t)(v1 - v0);
         return true;
     }
@@ -675,6 +677,10 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
     const bool https = r.flags & GM_REQ_HTTPS;
     if (https && !P.ssl) return;
     uint32_t sid = P.default_server;
+    if (r.flags & GM_REQ_INVALID) {   // rejected by the wire parser: its status, from the port's default server
+        o.server = sid; o.action = GM_ACT_BAD_REQUEST; o.status = r.bad_status;
+        return;
+    }
     // ---- host -> server (exact > *.x/.x > x.*)
     bool bad = false;
     if (r.host_len) {
@@ -823,7 +829,9 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
                                                        GTab t, gm_verdict *__restrict__ out,
                                                        unsigned long long *__restrict__ counters,
                                                        uint32_t *__restrict__ blk2rec, uint32_t nblk,
-                                                       uint32_t *__restrict__ hcnt, int prio) {
+                                                       uint32_t *__restrict__ hcnt, int prio,
+                                                       const uint64_t *__restrict__ dlen) {
+    if (dlen) arena_len = *dlen;   // gm_batch.arena_len_dev: the length a producer wrote on the device
     // beside the WAF scan: issue priority over the scan's waves, so the route's short
     // latency-bound waves finish early instead of stretching past the scan (GM_ROUTE_PRIO)
     if (prio) __builtin_amdgcn_s_setprio(2);
@@ -923,10 +931,12 @@ struct Scratch {
     uint32_t *d_ccnt = nullptr; size_t cap_ccnt = 0;
     uint8_t *d_temp = nullptr; size_t cap_temp = 0;
     uint8_t *d_stage = nullptr; size_t cap_stage = 0;            // GM_BATCH_HOST staging
+    uint64_t *d_wsize = nullptr, *d_wbase = nullptr; size_t cap_wsize = 0, cap_wbase = 0;   // wire parser
+    uint8_t *d_wtemp = nullptr; size_t cap_wtemp = 0;
     ~Scratch() {
         for (void *p : {(void *)d_status, (void *)d_blk2rec, (void *)d_cand, (void *)d_surv, (void *)d_pairs,
                         (void *)d_jobs, (void *)d_set, (void *)d_cnt, (void *)d_start, (void *)d_ccnt,
-                        (void *)d_temp, (void *)d_stage})
+                        (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
         for (auto &e : ev) if (e) (void)hipEventDestroy(e);
@@ -1095,7 +1105,7 @@ int gm_stats(gm_ctx *c, gm_stats_t *out) {
 // Enqueue one batch on stream s (device pointers).  No host synchronisation: every size a later
 // stage needs is a device status word or a host-known capacity.
 static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *reqs, const uint8_t *A, uint64_t alen,
-                     uint32_t n, gm_verdict *out, uint32_t *hit_ids, size_t hit_cap) {
+                     uint32_t n, gm_verdict *out, uint32_t *hit_ids, size_t hit_cap, const uint64_t *dlen) {
     hipStream_t s = S->stream;
     const GTab &t = g->tab;
     const bool waf = t.n_sigs > 0 && (t.n_lits > 0 || t.n_sig_regex > 0);
@@ -1107,14 +1117,14 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     };
     S->ev_used = 0;
     S->route_side = false;
-    HIPCHK(c, hipMemsetAsync(S->d_status, 0, STATUS_WORDS * 4, s));
+    HIPCHK(c, hipMemsetAsync(S->d_status, 0, BATCH_STATUS_WORDS * 4, s));
     if (mark(0)) return GM_E_HIP;
     const uint32_t route_blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
                                                                            (uint32_t)c->cu_count * 8));
     unsigned long long *ctr = g->d_counters;
     if (!waf) {
-        if (t.rk_keys) k_route<3, true><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0);
-        else k_route<3><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0);
+        if (t.rk_keys) k_route<3, true><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen);
+        else k_route<3><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen);
         HIPCHK(c, hipGetLastError());
         return mark(1) ? GM_E_HIP : GM_OK;
     }
@@ -1161,9 +1171,10 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     if (mark(1)) return GM_E_HIP;
     // persistent scan grid: one 1024-thread workgroup per CU (128 KiB LDS prefilter); every wave
     // owns a contiguous arena range and a private candidate region of wcap records
-    if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt);
-    else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt);
-    else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt);
+    if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
+    else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
+    else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
+    else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
     HIPCHK(c, hipGetLastError());
     {
         const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
@@ -1172,9 +1183,9 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         // raised issue priority: the route's short latency-bound waves finish early instead of
         // stretching past the scan
         if (t.rk_keys)
-            k_route<5, true><<<nb, ROUTE_BLOCK, 0, S->side>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1);
+            k_route<5, true><<<nb, ROUTE_BLOCK, 0, S->side>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1, dlen);
         else
-            k_route<5><<<nb, ROUTE_BLOCK, 0, S->side>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1);
+            k_route<5><<<nb, ROUTE_BLOCK, 0, S->side>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1, dlen);
         HIPCHK(c, hipGetLastError());
         if (prof) HIPCHK(c, hipEventRecord(S->ev_route[1], S->side));
         HIPCHK(c, hipEventRecord(S->ev_join, S->side));
@@ -1190,7 +1201,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     constexpr uint32_t EXACT_SUB = 8;
     k_waf_exact<<<scan_blocks * EXACT_SUB, 256, 0, s>>>(A, alen, reqs, n, S->d_blk2rec, t, S->d_surv, bcap,
                                                          S->d_ccnt + W, EXACT_SUB, S->d_pairs, (uint32_t)S->cap_pairs,
-                                                         S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, dd);
+                                                         S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, dd, dlen);
     HIPCHK(c, hipGetLastError());
     if (mark(3)) return GM_E_HIP;
     if (t.n_sig_regex) {
@@ -1224,12 +1235,13 @@ int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     const Generation *g = c->gen;
     if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
-    if (in->n == 0) { HIPCHK(c, hipMemsetAsync(S->d_status, 0, STATUS_WORDS * 4, s)); S->ev_pending = false; return GM_OK; }
+    if (in->n == 0) { HIPCHK(c, hipMemsetAsync(S->d_status, 0, BATCH_STATUS_WORDS * 4, s)); S->ev_pending = false; return GM_OK; }
     if (((uintptr_t)in->arena & 15) || ((uintptr_t)in->reqs & 15) || ((uintptr_t)out & 15))
         return fail(c, GM_E_INVAL, "reqs / arena / out must be 16-byte aligned");
     if (hit_cap > 0xFFFFFFFFull) hit_cap = 0xFFFFFFFFull;   // hit offsets are u32
     if (!(in->flags & GM_BATCH_HOST))
-        return run_batch(c, S, g, in->reqs, in->arena, in->arena_len, in->n, out, hit_ids, hit_ids ? hit_cap : 0);
+        return run_batch(c, S, g, in->reqs, in->arena, in->arena_len, in->n, out, hit_ids, hit_ids ? hit_cap : 0,
+                         in->arena_len_dev);
     // host buffers: stage reqs + arena + verdicts + hits through HBM (PCIe both ways)
     size_t rq = (size_t)in->n * sizeof(gm_req), ar = (in->arena_len + 255) & ~255ull;
     size_t vo = (size_t)in->n * sizeof(gm_verdict), ho = hit_cap * 4;
@@ -1243,7 +1255,8 @@ int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit
     uint32_t *dh = (uint32_t *)p;
     HIPCHK(c, hipMemcpyAsync(dr, in->reqs, rq, hipMemcpyHostToDevice, s));
     if (in->arena_len) HIPCHK(c, hipMemcpyAsync(da, in->arena, in->arena_len, hipMemcpyHostToDevice, s));
-    e = run_batch(c, S, g, dr, da, in->arena_len, in->n, dv, dh, hit_ids ? hit_cap : 0);
+    if (in->arena_len_dev) return fail(c, GM_E_INVAL, "arena_len_dev with GM_BATCH_HOST");
+    e = run_batch(c, S, g, dr, da, in->arena_len, in->n, dv, dh, hit_ids ? hit_cap : 0, nullptr);
     if (e) return e;
     HIPCHK(c, hipMemcpyAsync(out, dv, vo, hipMemcpyDeviceToHost, s));
     if (hit_ids && hit_cap) HIPCHK(c, hipMemcpyAsync(hit_ids, dh, ho, hipMemcpyDeviceToHost, s));
@@ -1278,6 +1291,7 @@ int gm_sync(gm_ctx *c, void *stream) {
         }
     }
     const uint32_t ov = S->h_status[3];
+    if (S->h_status[PARSE_STATUS_WORD + 3]) return fail(c, GM_E_OVERFLOW, "gm_parse_requests: arena capacity exceeded");
     if (ov & 2u) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded");
     if (ov) return fail(c, GM_E_OVERFLOW, "WAF candidate / survivor / pair / job capacity exceeded");
     return GM_OK;
@@ -1558,6 +1572,8 @@ __global__ __launch_bounds__(256) void k_uri_normalize(const uint8_t *A, const u
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
         out_len[i] = un_one(A + off[i], len[i], out + off[i]);
 }
+
+#include "gm_wire.inc"
 }  // namespace
 
 extern "C" int gm_normalize_uris(gm_ctx *c, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
@@ -1576,5 +1592,44 @@ extern "C" int gm_normalize_uris(gm_ctx *c, const uint8_t *arena, const uint64_t
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 16));
     k_uri_normalize<<<blocks, 256, 0, (hipStream_t)stream>>>(arena, off, len, n, out, out_len);
     HIPCHK(c, hipGetLastError());
+    return GM_OK;
+}
+
+extern "C" int gm_parse_requests(gm_ctx *c, const uint8_t *wire, const gm_wire_msg *msgs, uint32_t n, gm_req *reqs,
+                      uint8_t *arena, uint64_t arena_cap, uint64_t *arena_len_dev, void *stream) {
+    if (!c) return fail(c, GM_E_INVAL, "null ctx");
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
+    if (!arena_len_dev || (n && (!wire || !msgs || !reqs || !arena))) return fail(c, GM_E_INVAL, "null argument");
+    if (((uintptr_t)reqs & 15) || ((uintptr_t)arena & 15)) return fail(c, GM_E_INVAL, "reqs / arena must be 16-byte aligned");
+    HIPCHK(c, hipSetDevice(c->dev));
+    hipStream_t s = (hipStream_t)stream;
+    Scratch *S = scratch_for(c, s);
+    if (!S) return fail(c, GM_E_NOMEM, t_err);
+    HIPCHK(c, hipMemsetAsync(S->d_status + PARSE_STATUS_WORD, 0, (STATUS_WORDS - PARSE_STATUS_WORD) * 4, s));
+    if (n == 0) { HIPCHK(c, hipMemsetAsync(arena_len_dev, 0, 8, s)); return GM_OK; }
+    size_t tmp = 0;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, S->d_wsize, S->d_wbase, (int)n + 1, s));
+    int e;
+    if ((e = grow(c, s, S->d_wsize, S->cap_wsize, (size_t)n + 1))) return e;
+    if ((e = grow(c, s, S->d_wbase, S->cap_wbase, (size_t)n + 1))) return e;
+    if ((e = grow(c, s, S->d_wtemp, S->cap_wtemp, tmp))) return e;
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + WIRE_WAVES - 1) / WIRE_WAVES,
+                                                                     (uint32_t)c->cu_count * 16));
+    k_wire_size<<<blocks, 64 * WIRE_WAVES, 0, s>>>(wire, msgs, n, S->d_wsize);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_wtemp, tmp, S->d_wsize, S->d_wbase, (int)n + 1, s));
+    k_wire_emit<<<blocks, 64 * WIRE_WAVES, 0, s>>>(wire, msgs, n, S->d_wsize, S->d_wbase, reqs, arena, arena_cap,
+                                                   arena_len_dev, S->d_status + PARSE_STATUS_WORD);
+    HIPCHK(c, hipGetLastError());
+    return GM_OK;
+}
+
+// The last gm_parse_requests' per-request slot sizes on `stream` (size pass), for debugging.
+extern "C" int gm_debug_wire_sizes(gm_ctx *c, void *stream, uint64_t *out, size_t n) {
+    if (!c || !out) return fail(c, GM_E_INVAL, "null argument");
+    Scratch *S = scratch_for(c, (hipStream_t)stream);
+    if (!S || !S->d_wsize) return fail(c, GM_E_INVAL, "no parse on this stream");
+    HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
+    HIPCHK(c, hipMemcpy(out, S->d_wsize, std::min(n, S->cap_wsize) * 8, hipMemcpyDeviceToHost));
     return GM_OK;
 }

@@ -166,7 +166,8 @@ struct DDfa {
 // 1024-thread workgroup per CU.  Every arena offset is probed: one ds_read_b32 and pk
 // packed 16-bit shifts (2 bits each) per byte position.
 constexpr int BLOOM_LOG2 = 15;
-constexpr int BLOOM_PK_DEFAULT = 2;  // K = 2 * pk bits per key (pk = 1..3, per generation)
+constexpr int BLOOM_PK_DEFAULT = 4;  // BLOOM_PK_PERM: K = 4 bits, one per byte (else K = 2 * pk, pk = 1..3)
+constexpr uint32_t BLOOM_PK_PERM = 4;
 constexpr uint32_t BLOOM_WORDS = 1u << BLOOM_LOG2;
 constexpr uint32_t SCAN_LDS_BYTES = 4u * BLOOM_WORDS;
 constexpr int CAND_SHARDS = 64;      // candidate-list shards (one atomic tail per shard)
@@ -207,7 +208,7 @@ struct TabHeader {
     uint64_t total;
     uint32_t bloom_log2;     // BLOOM_LOG2 the image was built for
     uint32_t bloom_mul;      // Bloom hash multiplier (chosen per generation, see gm_compile.cpp)
-    uint32_t bloom_pk;       // packed shifts per probe (K = 2 * bloom_pk)
+    uint32_t bloom_pk;       // probe kind: BLOOM_PK_PERM (4 bits, one per byte) or pk packed shifts (K = 2 pk)
     uint32_t ctx_mul;        // stage-2 context filter multiplier (waf_b, see ctx_key)
     uint32_t n_rk_cap, n_rk_ids;   // regex-location prefilter: key table (pow2) and id lists
     uint32_t n_rk_ents_keys, pad_rk;   // distinct (server, key) pairs
@@ -250,11 +251,20 @@ struct BloomProbe { uint32_t block, mask; };
 __host__ __device__ inline uint32_t pk_bits(uint32_t x) {
     return (1u << (x & 15)) | (1u << (16 + ((x >> 16) & 15)));
 }
+// BLOOM_PK_PERM: one bit in each byte of the block, at bit (hi >> 8k) & 7 of byte k -- on the
+// device one v_and_b32 and one v_perm_b32 that reads the byte table {1, 2, 4, ..., 128}
+// (0x80402010'08040201) with those four selectors: 2 VALU ops for 4 bits (pk_bits: 3 ops).
+__host__ __device__ inline uint32_t perm_bits(uint32_t hi) {
+    uint32_t m = 0;
+    for (uint32_t k = 0; k < 4; k++) m |= 1u << (8 * k + ((hi >> (8 * k)) & 7));
+    return m;
+}
 __host__ __device__ inline BloomProbe bloom_probe(uint32_t w, uint32_t mul, uint32_t pk) {
     const uint64_t p = (uint64_t)w * mul;
     const uint32_t lo = (uint32_t)p, hi = (uint32_t)(p >> 32);
     uint32_t m = 0;
-    for (uint32_t q = 0; q < pk; q++) m |= pk_bits(hi >> (4 * q));
+    if (pk == BLOOM_PK_PERM) m = perm_bits(hi);
+    else for (uint32_t q = 0; q < pk; q++) m |= pk_bits(hi >> (4 * q));
     return BloomProbe{lo >> (32 - BLOOM_LOG2), m};
 }
 // Stage-2 context filter (waf_b, same size as the scan Bloom filter; staged into LDS by

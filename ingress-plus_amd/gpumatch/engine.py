@@ -44,12 +44,12 @@ class GmStats(ctypes.Structure):
 
 class GmBatch(ctypes.Structure):
     _fields_ = [("reqs", ctypes.c_void_p), ("arena", ctypes.c_void_p), ("arena_len", ctypes.c_uint64),
-                ("n", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+                ("n", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("arena_len_dev", ctypes.c_void_p)]
 
 
 EXPORTS = ["gm_create", "gm_destroy", "gm_abi_version", "gm_load_generation", "gm_match_batch", "gm_sync",
            "gm_counters", "gm_counters_reset", "gm_comm_unique_id", "gm_comm_init", "gm_counters_allreduce",
-           "gm_stats", "gm_last_error", "gm_normalize_uris", "gm_counters_global"]
+           "gm_stats", "gm_last_error", "gm_normalize_uris", "gm_counters_global", "gm_parse_requests"]
 
 _lib = None
 
@@ -77,6 +77,9 @@ def lib():
         L.gm_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(GmStats)]
         L.gm_normalize_uris.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.gm_parse_requests.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                        ctypes.c_void_p]
         L.gm_last_error.restype = ctypes.c_char_p
         L.gm_last_error.argtypes = [ctypes.c_void_p]
         _lib = L
@@ -124,8 +127,11 @@ class Engine:
         self._chk(lib().gm_stats(self.h, ctypes.byref(s)))
         return {f: getattr(s, f) for f in STATS_FIELDS + STATS_FIELDS64 + STATS_FIELDS_MS + STATS_FIELDS_WAF}
 
-    def match_ptr(self, reqs_ptr, arena_ptr, arena_len, n, out_ptr, hits_ptr, hit_cap, stream=0, host=False):
-        b = GmBatch(reqs_ptr, arena_ptr, arena_len, n, GM_BATCH_HOST if host else 0)
+    def match_ptr(self, reqs_ptr, arena_ptr, arena_len, n, out_ptr, hits_ptr, hit_cap, stream=0, host=False,
+                  arena_len_dev=None):
+        """gm_match_batch on pointers; ``arena_len_dev``: a device u64 holding the arena's length
+        (then ``arena_len`` is the capacity), e.g. written by parse_ptr on the same stream."""
+        b = GmBatch(reqs_ptr, arena_ptr, arena_len, n, GM_BATCH_HOST if host else 0, arena_len_dev)
         self._chk(lib().gm_match_batch(self.h, ctypes.byref(b), out_ptr, hits_ptr, hit_cap, stream))
 
     def sync(self, stream=0):
@@ -144,6 +150,11 @@ class Engine:
         self.sync(0)
         total = self.stats()["last_hits"]
         return out, hits[:total]
+
+    def parse_ptr(self, wire_ptr, msgs_ptr, n, reqs_ptr, arena_ptr, arena_cap, arena_len_dev_ptr, stream=0):
+        """gm_parse_requests on device pointers (HTTP/1.x wire bytes -> gm_req records + arena)."""
+        self._chk(lib().gm_parse_requests(self.h, wire_ptr, msgs_ptr, n, reqs_ptr, arena_ptr, arena_cap,
+                                          arena_len_dev_ptr, stream))
 
     def normalize_uris_ptr(self, arena_ptr, off_ptr, len_ptr, n, out_ptr, out_len_ptr, stream=0):
         """gm_normalize_uris on device pointers (nginx $uri normalisation, include/gpumatch.h)."""

@@ -27,7 +27,7 @@ assert REQ_DTYPE.itemsize == 64
 LEN_FIELD = {"uri": "uri_len", "args": "args_len", "hdrs": "hdr_len", "body": "body_len",
              "host": "host_len", "method": "method_len", "ruri": "ruri_len", "raddr": "raddr_len"}
 
-REQ_HTTPS, REQ_HTTP2, REQ_HTTP10 = 0x01, 0x02, 0x04
+REQ_HTTPS, REQ_HTTP2, REQ_HTTP10, REQ_INVALID = 0x01, 0x02, 0x04, 0x08
 
 VERDICT_DTYPE = np.dtype([
     ("gen", "<u4"), ("server_id", "<u4"), ("location_id", "<u4"), ("upstream_id", "<u4"),

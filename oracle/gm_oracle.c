@@ -668,7 +668,9 @@ static void sc_reset(scratch_t *s) {
     if (s->head) s->head->used = 0;
 }
 
-/* iterate header lines "Name: value\r\n"; value OWS-trimmed */
+/* iterate header lines "Name: value\r\n"; the value without leading / trailing spaces (nginx
+ * ngx_http_parse_header_line sw_space_before_value / sw_space_after_value skip ' ' only: a tab
+ * is part of the value) */
 static int hdr_next(sv h, int *pos, sv *name, sv *val) {
     while (*pos < h.n) {
         int st = *pos, e = st;
@@ -678,8 +680,8 @@ static int hdr_next(sv h, int *pos, sv *name, sv *val) {
         int c = st; while (c < le && h.p[c] != ':') c++;
         if (c >= le) continue;
         *name = (sv){h.p + st, c - st};
-        int vs = c + 1; while (vs < le && (h.p[vs] == ' ' || h.p[vs] == '\t')) vs++;
-        int ve = le; while (ve > vs && (h.p[ve - 1] == ' ' || h.p[ve - 1] == '\t')) ve--;
+        int vs = c + 1; while (vs < le && h.p[vs] == ' ') vs++;
+        int ve = le; while (ve > vs && h.p[ve - 1] == ' ') ve--;
         *val = (sv){h.p + vs, ve - vs};
         return 1;
     }
@@ -1088,6 +1090,9 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
         v->server_id = GM_NONE; v->action = GM_ACT_NO_LISTENER; v->status = 0; return;
     }
     v->server_id = (uint32_t)sidx;
+    if (r->flags & GM_REQ_INVALID) {   /* rejected by the wire parser: its status, from the default server */
+        v->action = GM_ACT_BAD_REQUEST; v->status = (uint32_t)r->pad0[1] | (uint32_t)r->pad0[2] << 8; return;
+    }
     if (bad || (port_ssl && !(r->flags & GM_REQ_HTTPS))) { v->action = GM_ACT_BAD_REQUEST; v->status = 400; return; }
     srv_t *S = &c->srv[sidx];
     ev_t E = {c, &q, sc, 0, NULL, NULL};
@@ -1303,4 +1308,263 @@ void orc_normalize_batch(const uint8_t *arena, const uint64_t *off, const uint32
         int64_t r = orc_normalize_uri(arena + off[i], len[i], out + off[i]);
         out_len[i] = r < 0 ? 0xFFFFFFFFu : (uint32_t)r;
     }
+}
+
+/* ------------------------------------------------------------------------------------------
+ * HTTP/1.x wire-parser oracle.  TEST INFRASTRUCTURE ONLY.
+ * Restates nginx 1.17.3's request intake (source not in /root/reference; the reference's
+ * templates read its results: $request_method / $uri / $args / $request_uri / $host and the
+ * header lines behind $http_* / $cookie_*, nginx.virtualserver.tmpl:25-31, and the body the
+ * Wallarm phase scans, nginx.ingress.tmpl:12-29):
+ *   - ngx_http_parse_request_line: leading CR/LF skipped; method [A-Z_-]+; 1+ spaces; target
+ *     origin-form "/..." or absolute-form "scheme://host[:port][/...]"; 1+ spaces; "HTTP/"
+ *     major "." minor; spaces; CRLF or LF.  No version (HTTP/0.9) -> 400 here (nginx serves a
+ *     0.9 GET: a documented divergence); major > 1 -> 505; NUL in the line -> 400.
+ *   - $uri = ngx_http_parse_complex_uri of the path (orc_normalize_uri, failure -> 400);
+ *     $args = after the first '?' that precedes any '#'; $request_uri = the target from its
+ *     path (absolute-form: the scheme and host are not part of it; no path -> "/").
+ *   - ngx_http_parse_header_line + ngx_http_process_request_headers (ignore_invalid_headers on,
+ *     underscores_in_headers off): a line whose name has a byte outside [A-Za-z0-9-] (incl. '_',
+ *     a leading space -- obs-fold continuation lines -- or an empty name) is dropped; a NUL
+ *     anywhere -> 400; the value loses leading / trailing spaces only; a line without ':' is a
+ *     header with an empty value.  Kept lines are emitted "Name: value\r\n" in order.
+ *   - Host: a second Host line -> 400; HTTP/1.1 without Host (and no absolute-form host) -> 400;
+ *     the absolute-form host takes precedence.  Content-Length: a second one -> 400, not all
+ *     digits -> 400.  Transfer-Encoding (the first): "chunked" (caseless) -> chunked body,
+ *     Content-Length ignored; "identity" -> ignored; anything else -> 501.
+ *   - body: Content-Length bytes (fewer present -> 400) or the chunked body decoded
+ *     (hex size [;ext] CRLF data CRLF ... "0" CRLF trailers CRLF; malformed or short -> 400).
+ *   - more than 255 header lines -> 400 (the device's line table; nginx's limit is its buffers).
+ * A rejected request keeps its connection fields and gets GM_REQ_INVALID + its status.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct {
+    int status;                        /* 0 ok, else 400 / 501 / 505 */
+    int minor;
+    const uint8_t *method; int method_len;
+    const uint8_t *target; int target_len;   /* $request_uri */
+    const uint8_t *path; int path_len;       /* bytes normalised into $uri (stops at ? / #) */
+    const uint8_t *args; int args_len;
+    const uint8_t *uhost; int uhost_len;     /* absolute-form host */
+    int body_start;                          /* offset of the first body byte */
+} orc_rl_t;
+
+static int orc_rl_parse(const uint8_t *b, int n, orc_rl_t *r) {
+    memset(r, 0, sizeof *r);
+    int i = 0;
+    while (i < n && (b[i] == '\r' || b[i] == '\n')) i++;
+    int m0 = i;
+    while (i < n && ((b[i] >= 'A' && b[i] <= 'Z') || b[i] == '_' || b[i] == '-')) i++;
+    if (i == m0 || i >= n || b[i] != ' ') return 400;
+    r->method = b + m0; r->method_len = i - m0;
+    while (i < n && b[i] == ' ') i++;
+    if (i >= n) return 400;
+    int t0 = i;
+    if (b[i] != '/') {                       /* absolute-form: scheme "://" host [":" port] */
+        int s0 = i;
+        while (i < n && ((b[i] | 0x20) >= 'a' && (b[i] | 0x20) <= 'z')) i++;
+        if (i == s0 || i + 3 > n || b[i] != ':' || b[i + 1] != '/' || b[i + 2] != '/') return 400;
+        i += 3;
+        int h0 = i;
+        while (i < n && (isalnum(b[i]) || b[i] == '.' || b[i] == '-')) i++;
+        if (i == h0) return 400;
+        r->uhost = b + h0; r->uhost_len = i - h0;
+        if (i < n && b[i] == ':') { i++; while (i < n && b[i] >= '0' && b[i] <= '9') i++; }
+        if (i >= n) return 400;
+        if (b[i] != '/' && b[i] != ' ') return 400;
+        t0 = i;
+    }
+    int te = t0;
+    while (te < n && b[te] != ' ' && b[te] != '\r' && b[te] != '\n') { if (b[te] == 0) return 400; te++; }
+    if (te >= n || b[te] != ' ') return 400;   /* HTTP/0.9 (no version) or truncated */
+    if (te == t0) { static const uint8_t slash = '/'; r->target = &slash; r->target_len = 1; r->path = &slash; r->path_len = 1; }
+    else {
+        r->target = b + t0; r->target_len = te - t0;
+        int q = t0; while (q < te && b[q] != '?' && b[q] != '#') q++;
+        r->path = b + t0; r->path_len = q - t0;
+        if (q < te && b[q] == '?') { r->args = b + q + 1; r->args_len = te - q - 1; }
+    }
+    i = te;
+    while (i < n && b[i] == ' ') i++;
+    if (i + 5 > n || memcmp(b + i, "HTTP/", 5)) return 400;
+    i += 5;
+    long major = 0, minor = 0; int d0 = i;
+    while (i < n && b[i] >= '0' && b[i] <= '9') { major = major * 10 + (b[i] - '0'); if (major > 99) return 400; i++; }
+    if (i == d0 || i >= n || b[i] != '.') return 400;
+    i++; d0 = i;
+    while (i < n && b[i] >= '0' && b[i] <= '9') { minor = minor * 10 + (b[i] - '0'); if (minor > 99) return 400; i++; }
+    if (i == d0) return 400;
+    while (i < n && b[i] == ' ') i++;
+    if (i < n && b[i] == '\r') i++;
+    if (i >= n || b[i] != '\n') return 400;
+    if (major > 1) return 505;
+    if (major < 1) return 400;
+    r->minor = (int)minor;
+    r->body_start = i + 1;   /* the first header line (the caller continues from here) */
+    return 0;
+}
+
+static int orc_hname_ok(const uint8_t *p, int n) {
+    if (n == 0) return 0;
+    for (int k = 0; k < n; k++) if (!(isalnum(p[k]) || p[k] == '-')) return 0;
+    return 1;
+}
+static int orc_ieq(const uint8_t *p, int n, const char *s) {
+    int l = (int)strlen(s);
+    if (n != l) return 0;
+    for (int k = 0; k < n; k++) if (lc(p[k]) != (unsigned char)s[k]) return 0;
+    return 1;
+}
+
+typedef struct { uint8_t *p; size_t n, cap; } obuf_t;
+static void ob_put(obuf_t *o, const void *s, size_t n) {
+    if (o->n + n > o->cap) { o->cap = (o->n + n) * 2 + 64; o->p = realloc(o->p, o->cap); }
+    memcpy(o->p + o->n, s, n); o->n += n;
+}
+
+/* one request -> status and its fields (appended to the per-request buffers).  nginx's order:
+ * the request line (400 / 505 / 414), its complex URI (400), header lines as they are read
+ * (NUL, a second Host or Content-Length, an over-long line: 400), then after the header:
+ * HTTP/1.1 without a Host header (400), an invalid Content-Length (400), an unknown
+ * Transfer-Encoding (501), and the body (400 if short or malformed). */
+static int orc_parse_one(const uint8_t *b, int n, orc_rl_t *R, obuf_t *uri, obuf_t *hdrs, obuf_t *body,
+                         const uint8_t **host, int *host_len) {
+    {   /* the request line (through its LF) must fit one 8 KiB large_client_header_buffers buffer */
+        int s0 = 0; while (s0 < n && (b[s0] == '\r' || b[s0] == '\n')) s0++;
+        int e = s0; while (e < n && b[e] != '\n') e++;
+        if (e < n && e + 1 - s0 > 8192) return 414;
+    }
+    int st = orc_rl_parse(b, n, R);
+    if (st) return st;
+    int64_t u = uri->n;
+    if (uri->n + R->path_len + 1 > uri->cap) { uri->cap = uri->n + R->path_len + 64; uri->p = realloc(uri->p, uri->cap); }
+    int64_t nl = orc_normalize_uri(R->path, (uint32_t)R->path_len, uri->p + u);
+    if (nl < 0) return 400;
+    uri->n += (size_t)nl;
+    int i = R->body_start, nlines = 0, hosts = 0, cls = 0, cl_bad = 0, te_kind = 0;
+    int64_t clen = -1;
+    *host = NULL; *host_len = 0;
+    for (;;) {
+        if (i >= n) return 400;                 /* no empty line: incomplete header */
+        int e = i; while (e < n && b[e] != '\n') e++;
+        if (e >= n) return 400;
+        int le = e; if (le > i && b[le - 1] == '\r') le--;
+        if (le == i) { i = e + 1; break; }      /* empty line: end of the header */
+        if (e + 1 - i > 8192) return 400;       /* header line larger than a buffer */
+        for (int k = i; k < le; k++) if (b[k] == 0) return 400;
+        if (++nlines > 254) return 400;
+        int c = i; while (c < le && b[c] != ':') c++;
+        const uint8_t *nm = b + i; int nlen = c - i;
+        int vs = c < le ? c + 1 : le;
+        while (vs < le && b[vs] == ' ') vs++;
+        int ve = le; while (ve > vs && b[ve - 1] == ' ') ve--;
+        i = e + 1;
+        if (!orc_hname_ok(nm, nlen)) continue;  /* invalid header line: ignored */
+        ob_put(hdrs, nm, nlen); ob_put(hdrs, ": ", 2); ob_put(hdrs, b + vs, ve - vs); ob_put(hdrs, "\r\n", 2);
+        if (orc_ieq(nm, nlen, "host")) {
+            if (++hosts > 1) return 400;        /* "client sent duplicate host header" */
+            if (!R->uhost) { *host = b + vs; *host_len = ve - vs; }
+        } else if (orc_ieq(nm, nlen, "content-length")) {
+            if (++cls > 1) return 400;          /* unique header line */
+            clen = 0;
+            if (ve == vs) cl_bad = 1;
+            for (int k = vs; k < ve && !cl_bad; k++) {
+                if (b[k] < '0' || b[k] > '9' || clen > (INT64_MAX - 9) / 10) cl_bad = 1;
+                else clen = clen * 10 + (b[k] - '0');
+            }
+        } else if (orc_ieq(nm, nlen, "transfer-encoding") && !te_kind) {
+            te_kind = orc_ieq(b + vs, ve - vs, "chunked") ? 1 : orc_ieq(b + vs, ve - vs, "identity") ? 2 : 3;
+        }
+    }
+    if (!hosts && R->minor >= 1) return 400;    /* HTTP/1.1 without a Host header */
+    if (R->uhost) { *host = R->uhost; *host_len = R->uhost_len; }   /* the absolute URI's host wins */
+    if (cl_bad) return 400;
+    if (te_kind == 3) return 501;
+    if (te_kind == 1) {
+        for (;;) {
+            /* chunk-size line: hex digits, then CRLF / LF, or an extension (';', SP, HT ...) up
+             * to LF (ngx_http_parse_chunked sw_chunk_size / sw_chunk_extension) */
+            int64_t sz = 0; int d0 = i;
+            while (i < n && isxdigit(b[i])) {
+                int v = isdigit(b[i]) ? b[i] - '0' : (lc(b[i]) - 'a' + 10);
+                if (sz > (INT64_MAX >> 4) - 1) return 400;
+                sz = sz * 16 + v; i++;
+            }
+            if (i == d0 || i >= n) return 400;
+            if (b[i] == '\r') { i++; if (i >= n || b[i] != '\n') return 400; }
+            else if (b[i] == ';' || b[i] == ' ' || b[i] == '\t') { while (i < n && b[i] != '\n') i++; if (i >= n) return 400; }
+            else if (b[i] != '\n') return 400;
+            i++;
+            if (sz == 0) {                        /* trailer lines up to the empty line */
+                for (;;) {
+                    if (i >= n) return 400;
+                    int e = i; while (e < n && b[e] != '\n') e++;
+                    if (e >= n) return 400;
+                    int le = e; if (le > i && b[le - 1] == '\r') le--;
+                    const int empty = le == i;
+                    i = e + 1;
+                    if (empty) break;
+                }
+                break;
+            }
+            if ((int64_t)(n - i) < sz) return 400;
+            ob_put(body, b + i, (size_t)sz);
+            i += (int)sz;
+            if (i < n && b[i] == '\r') i++;
+            if (i >= n || b[i] != '\n') return 400;
+            i++;
+        }
+        if (body->n > 0xFFFFFFFFu) return 400;
+    } else if (clen > 0) {
+        if ((int64_t)(n - i) < clen) return 400;
+        ob_put(body, b + i, (size_t)clen);
+    }
+    return 0;
+}
+
+/* n requests -> gm_req records + a packed payload arena (gm_req field order, 16-B aligned
+ * bases).  Returns the arena length, or -1 if `cap` is too small. */
+int64_t orc_parse_requests(const uint8_t *wire, const gm_wire_msg *msgs, uint32_t n, gm_req *reqs, uint8_t *arena,
+                           uint64_t cap) {
+    obuf_t uri = {0}, hdrs = {0}, body = {0};
+    uint64_t o = 0;
+    int64_t rc = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const gm_wire_msg *m = &msgs[k];
+        orc_rl_t R;
+        const uint8_t *host; int host_len;
+        uri.n = hdrs.n = body.n = 0;
+        int st = orc_parse_one(wire + m->off, (int)m->len, &R, &uri, &hdrs, &body, &host, &host_len);
+        gm_req *r = &reqs[k];
+        memset(r, 0, sizeof *r);
+        r->base = o;
+        r->port = m->port; r->remote_port = m->remote_port;
+        memcpy(r->rid, m->rid, 16);
+        const int ra = m->raddr_len > 40 ? 40 : m->raddr_len;
+        r->flags = m->flags & (GM_REQ_HTTPS | GM_REQ_HTTP2);
+        const uint8_t *seg[8]; size_t len[8] = {0};
+        if (st) {
+            r->flags |= GM_REQ_INVALID;
+            r->pad0[1] = (uint8_t)(st & 0xFF); r->pad0[2] = (uint8_t)(st >> 8);
+        } else {
+            if (R.minor == 0) r->flags |= GM_REQ_HTTP10;
+            seg[0] = uri.p; len[0] = uri.n;
+            seg[1] = R.args; len[1] = (size_t)R.args_len;
+            seg[2] = hdrs.p; len[2] = hdrs.n;
+            seg[3] = body.p; len[3] = body.n;
+            seg[4] = host; len[4] = (size_t)host_len;
+            seg[5] = R.method; len[5] = (size_t)R.method_len;
+            seg[6] = R.target; len[6] = (size_t)R.target_len;
+        }
+        seg[7] = m->raddr; len[7] = (size_t)ra;
+        r->uri_len = (uint32_t)len[0]; r->args_len = (uint32_t)len[1]; r->hdr_len = (uint32_t)len[2];
+        r->body_len = (uint32_t)len[3]; r->host_len = (uint16_t)len[4]; r->method_len = (uint16_t)len[5];
+        r->ruri_len = (uint16_t)len[6]; r->raddr_len = (uint16_t)len[7];
+        size_t tot = 0;
+        for (int f = 0; f < 8; f++) tot += len[f];
+        if (o + tot > cap) { rc = -1; break; }
+        for (int f = 0; f < 8; f++) if (len[f]) { memcpy(arena + o, seg[f], len[f]); o += len[f]; }
+        while (o & 15) { if (o < cap) arena[o] = 0; o++; }
+    }
+    free(uri.p); free(hdrs.p); free(body.p);
+    return rc < 0 ? -1 : (int64_t)o;
 }

@@ -66,3 +66,22 @@ def murmur2(b: bytes) -> int:
 
 def pcre_match(pat: str, subj: bytes, caseless: bool = False) -> int:
     return int(lib().orc_pcre_match(pat.encode(), 1 if caseless else 0, subj, len(subj)))
+
+
+def parse_requests(wire: np.ndarray, msgs: np.ndarray):
+    """oracle/gm_oracle.c orc_parse_requests: HTTP/1.x bytes -> (gm_req records, arena)."""
+    from gpumatch.records import REQ_DTYPE
+    L = lib()
+    L.orc_parse_requests.restype = ctypes.c_int64
+    L.orc_parse_requests.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_uint64]
+    n = len(msgs)
+    reqs = np.zeros(n, dtype=REQ_DTYPE)
+    cap = int((2 * msgs["len"].astype(np.int64) + msgs["raddr_len"] + 16).sum()) + 16
+    arena = np.zeros(cap, dtype=np.uint8)
+    w = np.ascontiguousarray(wire)
+    m = np.ascontiguousarray(msgs)
+    tot = L.orc_parse_requests(w.ctypes.data, m.ctypes.data, n, reqs.ctypes.data, arena.ctypes.data, cap)
+    if tot < 0:
+        raise RuntimeError("oracle parse: arena capacity")
+    return reqs, arena[:tot]
