@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--pool", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--serial", action="store_true",
+                    help="measurement: the route stage alone before the scan (GM_CREATE_SERIAL)")
     args = ap.parse_args()
 
     import torch
@@ -56,7 +58,7 @@ def main():
     t0 = time.time()
     # benign traffic sample (disjoint seed) for the prefilter's key / hash choice (GM_ENTRY_SAMPLE)
     ss, gblob = workloads.c4_bench_generation()
-    eng = engine.Engine(local, profile=True)
+    eng = engine.Engine(local, profile=True, serial=args.serial)
     eng.load(gblob, 1)
     st = eng.stats()
     log(f"[rank {rank}] generation: {st['n_sigs']} rules ({st['n_sig_literals']} lit, {st['n_sig_regex']} re), "

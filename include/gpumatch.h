@@ -46,6 +46,9 @@ extern "C" {
 /* ---------------------------------------------------------------- gm_create flags */
 #define GM_CREATE_COMPILE_ONLY  0x1u  /* no HIP device: compile + stats only (host tests) */
 #define GM_CREATE_PROFILE       0x2u  /* record HIP events per stage (gm_stats_t.last_ms_*) */
+#define GM_CREATE_SERIAL        0x4u  /* measurement: run the route stage alone before the WAF scan */
+                                      /* (default: beside it on a side stream), so each stage's     */
+                                      /* HIP-event time is its own                                  */
 
 /* ---------------------------------------------------------------- packed request record
  * One 64-byte header per request; payload bytes live in one byte arena.  The payload of a

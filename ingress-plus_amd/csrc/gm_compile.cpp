@@ -1059,23 +1059,33 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             }
         }
     }
+    std::vector<uint8_t> name_bytes;   // server-name strings (their own hot section, see off_hot_end)
+    auto put_name = [&](const std::string &nm) {
+        const uint32_t off = (uint32_t)name_bytes.size();
+        name_bytes.insert(name_bytes.end(), nm.begin(), nm.end());
+        return off;
+    };
     auto build_names = [&](std::vector<NameKey> &keys, uint32_t &mask) {
         uint32_t cap = pow2_at_least(keys.size() * 2 + 1);
         std::vector<DName> tab(cap);
         for (auto &k : keys) {
-            uint32_t h = 2166136261u;
-            for (char c : k.name) h = fnv1a_step(h, (uint8_t)c);
+            uint32_t h = name_hash_init((uint32_t)k.name.size());
+            for (size_t o = 0; o < k.name.size(); o += 4) {
+                uint32_t w = 0;
+                for (size_t q = 0; q < 4 && o + q < k.name.size(); q++) w |= (uint32_t)(uint8_t)k.name[o + q] << (8 * q);
+                h = name_hash_word(h, w);
+            }
             h = name_hash_fin(h, (uint32_t)k.port);
             uint32_t i = h & (cap - 1);
             bool dup = false;
             while (tab[i].hash) {
                 const DName &e = tab[i];
                 if (e.hash == h && e.port_idx == k.port && e.name_len == k.name.size() &&
-                    !memcmp(C.bytes.data() + e.name_off, k.name.data(), k.name.size())) { dup = true; break; }
+                    !memcmp(name_bytes.data() + e.name_off, k.name.data(), k.name.size())) { dup = true; break; }
                 i = (i + 1) & (cap - 1);
             }
             if (dup) continue;   // duplicate name on this port: first definition wins
-            tab[i].hash = h; tab[i].name_off = C.put_bytes(k.name); tab[i].name_len = (uint16_t)k.name.size();
+            tab[i].hash = h; tab[i].name_off = put_name(k.name); tab[i].name_len = (uint16_t)k.name.size();
             tab[i].port_idx = (uint16_t)k.port; tab[i].server = k.server;
         }
         mask = cap - 1;
@@ -1431,10 +1441,16 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.n_dfas = (uint32_t)C.dfas.size();
     h.n_lit_buckets_cap = lcap; h.n_lits = (uint32_t)dlits.size(); h.n_sig_regex = (uint32_t)sregex.size();
     h.n_always = (uint32_t)always.size(); h.n_sigs = st.n_sigs;
+    // the route's hot tables first, contiguous (k_route stages them into LDS when they fit)
     h.off_ports = I.put(ports);
     h.off_names = I.put(tab_exact); h.off_wild_head = I.put(tab_head); h.off_wild_tail = I.put(tab_tail);
-    h.off_servers = I.put(dservers); h.off_server_ifs = I.put(sifs); h.off_rlocs = I.put(rlocs);
-    h.off_nodes = I.put(nodes); h.off_edges = I.put(edges); h.off_locs = I.put(dlocs);
+    h.off_servers = I.put(dservers); h.off_server_ifs = I.put(sifs);
+    h.off_small = I.put(smalls); h.off_locs = I.put(dlocs);
+    name_bytes.resize(name_bytes.size() + 64, 0);   // slack: 16-B block loads may over-read
+    h.off_name_bytes = I.put(name_bytes);
+    h.off_hot_end = (I.buf.size() + 15) & ~size_t(15);
+    h.off_rlocs = I.put(rlocs);
+    h.off_nodes = I.put(nodes); h.off_edges = I.put(edges);
     h.off_srcs = I.put(C.srcs); h.off_conds = I.put(C.conds); h.off_chain_heads = I.put(C.chain_heads);
     h.off_rules = I.put(C.rules); h.off_rtab = I.put(C.rtab); h.off_rtargets = I.put(C.rtargets);
     h.off_splits = I.put(C.splits); h.off_parts = I.put(C.parts);
@@ -1444,7 +1460,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_lit_buckets = I.put(ltab); h.off_lits = I.put(dlits); h.off_sig_regex = I.put(sregex);
     h.off_always = I.put(always);
     h.n_rk_cap = rkcap; h.n_rk_ids = (uint32_t)rk_ids.size(); h.n_rk_ents_keys = (uint32_t)rk_lists.size();
-    h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_small = I.put(smalls); h.off_rk_ents = I.put(rk_ents); h.off_rk_bloom = I.put(rk_bloom);
+    h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_rk_ents = I.put(rk_ents); h.off_rk_bloom = I.put(rk_bloom);
     C.bytes.resize(C.bytes.size() + 64, 0);   // slack: vector compares may over-read
     h.off_bytes = I.put(C.bytes);
     I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
@@ -1495,6 +1511,9 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.rk_ents = (const DRlocEnt *)(b + h.off_rk_ents);
     t.rk_bloom = (const uint32_t *)(b + h.off_rk_bloom);
     t.rk_keys = h.n_rk_ents_keys;
+    t.name_bytes = b + h.off_name_bytes;
+    t.hot_base = b + h.off_ports;
+    t.hot_len = h.off_hot_end - h.off_ports <= ROUTE_STAGE_BYTES ? (uint32_t)(h.off_hot_end - h.off_ports) : 0u;
     t.n_ports = h.n_ports;
     t.names_mask = h.n_names_cap - 1; t.wild_head_mask = h.n_wild_head_cap - 1; t.wild_tail_mask = h.n_wild_tail_cap - 1;
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;

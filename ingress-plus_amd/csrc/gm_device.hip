@@ -459,8 +459,12 @@ __device__ int validate_host(const uint8_t *h, uint32_t n) {
 
 __device__ uint32_t name_probe(const DName *tab, uint32_t mask, const uint8_t *bytes, const uint8_t *h,
                                uint32_t off, uint32_t len, uint32_t port_idx) {
-    uint32_t hs = 2166136261u;
-    for (uint32_t i = 0; i < len; i++) hs = fnv1a_step(hs, lc(h[off + i]));
+    uint32_t hs = name_hash_init(len);
+    for (uint32_t i = 0; i < len; i += 4) {
+        uint32_t w = 0;
+        for (uint32_t q = 0; q < 4 && i + q < len; q++) w |= lc(h[off + i + q]) << (8 * q);
+        hs = name_hash_word(hs, w);
+    }
     hs = name_hash_fin(hs, port_idx);
     for (uint32_t i = hs & mask;; i = (i + 1) & mask) {
         const DName e = tab[i];
@@ -527,16 +531,29 @@ __device__ __forceinline__ void load_span_n(const uint8_t *A, uint64_t off, uint
 
 __device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[8], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xFF; }
 
+// exact per-byte equality flags of a word against a byte value: bit 8k+7 set iff byte k == c
+__device__ __forceinline__ uint32_t byte_eq_flags(uint32_t w, uint32_t c) {
+    const uint32_t t = w ^ (c * 0x01010101u);
+    return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+}
+// the four flags of a word as a nibble (bit k = byte k): the multiply gathers bits 7/15/23/31
+__device__ __forceinline__ uint32_t flags_nibble(uint32_t f) { return ((f >> 7) * 0x10204080u) >> 28; }
+
 // Host of <= 32 bytes held in registers: validate_host + exact-name probe (the common case).
 // Returns the normalised length (-1 = invalid) and the exact-table server (GM_NONE = miss).
+// SWAR: per 4-byte word, exact byte-equality flags for '.', ':', '/', NUL, gathered into 32-bit
+// position masks; ngx_http_validate_host's rules then follow from the masks (".." = adjacent
+// dots; the first ':' ends the host; the last '.' is stripped when it ends the host).  A host
+// starting with '[' (IPv6 literal) takes the byte loop.
 __device__ __forceinline__ int host_fast(const uint32_t (&hw)[8], uint32_t n, const GTab &t, uint32_t pi,
                                          uint32_t &server) {
     server = GM_NONE;
-    int dot_pos = (int)n, host_len = (int)n, state = 0;
-    bool bad = false;
-#pragma unroll
-    for (int i = 0; i < 32; i++) {
-        if (i < (int)n) {
+    int host_len;
+    if ((hw[0] & 0xFF) == '[') {
+        int dot_pos = (int)n, state = 0;
+        bool bad = false;
+        host_len = (int)n;
+        for (int i = 0; i < (int)n; i++) {
             const uint32_t ch = byte_of(hw, i);
             if (ch == '.') { bad |= dot_pos == i - 1; dot_pos = i; }
             else if (ch == ':') { if (state == 0) { host_len = i; state = 2; } }
@@ -544,19 +561,39 @@ __device__ __forceinline__ int host_fast(const uint32_t (&hw)[8], uint32_t n, co
             else if (ch == ']') { if (state == 1) { host_len = i + 1; state = 2; } }
             else if (ch == 0 || ch == '/') bad = true;
         }
-    }
-    if (dot_pos == host_len - 1) host_len--;
-    if (bad || host_len <= 0) return -1;
-    uint32_t hs = 2166136261u;
+        if (dot_pos == host_len - 1) host_len--;
+        if (bad || host_len <= 0) return -1;
+    } else {
+        uint32_t dots = 0, colons = 0, badm = 0;
 #pragma unroll
-    for (int i = 0; i < 32; i++) if (i < host_len) hs = fnv1a_step(hs, lc(byte_of(hw, i)));
+        for (int k = 0; k < 8; k++) {
+            const int rem = (int)n - 4 * k;
+            const uint32_t lm = rem >= 4 ? 0xFFFFFFFFu : rem > 0 ? (1u << (8 * rem)) - 1 : 0u;
+            const uint32_t w = hw[k];
+            dots |= flags_nibble(byte_eq_flags(w, '.') & lm) << (4 * k);
+            colons |= flags_nibble(byte_eq_flags(w, ':') & lm) << (4 * k);
+            badm |= (byte_eq_flags(w, '/') | byte_eq_flags(w, 0)) & lm;
+        }
+        if (badm || (dots & (dots >> 1))) return -1;
+        host_len = colons ? __builtin_ctz(colons) : (int)n;
+        if (dots && 31 - __builtin_clz(dots) == host_len - 1) host_len--;
+        if (host_len <= 0) return -1;
+    }
+    uint32_t hs = name_hash_init((uint32_t)host_len);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int rem = host_len - 4 * k;
+        if (rem <= 0) break;
+        const uint32_t m = rem >= 4 ? 0xFFFFFFFFu : (1u << (8 * rem)) - 1;
+        hs = name_hash_word(hs, lower4(hw[k]) & m);
+    }
     hs = name_hash_fin(hs, pi);
     for (uint32_t i = hs & t.names_mask;; i = (i + 1) & t.names_mask) {
         const DName e = t.names[i];
         if (e.hash == 0) break;
         if (e.hash == hs && e.port_idx == pi && e.name_len == (uint32_t)host_len) {
             uint32_t tw[8];
-            load_span32(t.bytes, e.name_off, ~0ull, tw);   // the bytes pool ends with 64 B of slack
+            load_span32(t.name_bytes, e.name_off, ~0ull, tw);   // the name strings end with 64 B of slack
             uint32_t diff = 0;
 #pragma unroll
             for (int k = 0; k < 8; k++) {
@@ -574,15 +611,15 @@ __device__ __forceinline__ int host_fast(const uint32_t (&hw)[8], uint32_t n, co
 // the arena (rare path).
 __device__ __noinline__ uint32_t host_wildcards(const uint8_t *h, int hl, const GTab &t, uint32_t pi) {
     uint32_t s = GM_NONE;
-    uint32_t w = name_probe(t.wild_head, t.wild_head_mask, t.bytes, h, 0, (uint32_t)hl, pi);
+    uint32_t w = name_probe(t.wild_head, t.wild_head_mask, t.name_bytes, h, 0, (uint32_t)hl, pi);
     if (w != GM_NONE && (w & 0x80000000u)) s = w & 0x7FFFFFFFu;      // ".x" matches x itself
     for (int d = 0; s == GM_NONE && d < hl; d++)
         if (h[d] == '.') {
-            w = name_probe(t.wild_head, t.wild_head_mask, t.bytes, h, d + 1, (uint32_t)(hl - d - 1), pi);
+            w = name_probe(t.wild_head, t.wild_head_mask, t.name_bytes, h, d + 1, (uint32_t)(hl - d - 1), pi);
             if (w != GM_NONE) s = w & 0x7FFFFFFFu;
         }
     for (int d = hl - 2; s == GM_NONE && d > 0; d--)
-        if (h[d] == '.') s = name_probe(t.wild_tail, t.wild_tail_mask, t.bytes, h, 0, (uint32_t)d, pi);
+        if (h[d] == '.') s = name_probe(t.wild_tail, t.wild_tail_mask, t.name_bytes, h, 0, (uint32_t)d, pi);
     return s;
 }
 
@@ -664,8 +701,19 @@ __device__ __noinline__ uint32_t split_generic(const uint8_t *A, const gm_req *r
     return 0xFFu;
 }
 
-__device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const GTab &t, RouteOut &o,
-                          const uint32_t *rkb) {
+// The first 32 bytes of a request's Host and URI, both loaded as soon as its record is known (two
+// independent HBM loads instead of host, then the server's tables, then the URI).  (Loading them
+// one request ahead was measured slower: a wave's loads complete in order, so the prefetch made
+// every table lookup of the current request wait for the next request's HBM loads.)
+struct RoutePre { uint32_t hw[8], uw[8]; };
+__device__ __forceinline__ void route_prefetch(const uint8_t *A, uint64_t alen, const Rec &r, RoutePre &p) {
+    const uint64_t f_uri = r.base, f_host = r.base + r.uri_len + r.args_len + r.hdr_len + r.body_len;
+    load_span_n(A, f_host, alen, min(r.host_len, 32u), p.hw);
+    load_span_n(A, f_uri, alen, min(r.uri_len, 32u), p.uw);
+}
+
+__device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const RoutePre &pre,
+                          const GTab &t, RouteOut &o, const uint32_t *rkb) {
     o.server = GM_NONE; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0;
     o.action = GM_ACT_NO_LISTENER; o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF;
     const uint64_t f_uri = r.base, f_host = r.base + r.uri_len + r.args_len + r.hdr_len + r.body_len;
@@ -687,12 +735,10 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
         uint32_t s = GM_NONE;
         int hl;
         if (r.host_len <= 32) {
-            uint32_t hw[8];
-            load_span_n(A, f_host, alen, r.host_len, hw);
-            hl = host_fast(hw, r.host_len, t, pi, s);
+            hl = host_fast(pre.hw, r.host_len, t, pi, s);
         } else {
             hl = validate_host(A + f_host, r.host_len);
-            if (hl >= 0) s = name_probe(t.names, t.names_mask, t.bytes, A + f_host, 0, (uint32_t)hl, pi);
+            if (hl >= 0) s = name_probe(t.names, t.names_mask, t.name_bytes, A + f_host, 0, (uint32_t)hl, pi);
         }
         if (hl < 0) bad = true;
         else {
@@ -717,8 +763,8 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
     // The first 32 URI bytes come from registers (a window shifted one dword per 4 bytes).
     const uint8_t *u = A + f_uri;
     uint32_t uw[8];
-    // only the bytes the walk can read: it stops at the server's deepest location name
-    load_span_n(A, f_uri, alen, min(min(r.uri_len, S.trie_depth + 1u), 32u), uw);
+#pragma unroll
+    for (int k = 0; k < 8; k++) uw[k] = pre.uw[k];
     int32_t best = -1, fexact = -1, far = -1;
     bool full = false;   // a location-trie node spells the whole URI
     if (S.sl_n) {
@@ -826,7 +872,7 @@ constexpr uint32_t LDS_HIST_MAX = 512;
 template <int WPE, bool RK = false>
 __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_route(const gm_req *__restrict__ reqs, uint32_t n,
                                                        const uint8_t *__restrict__ A, uint64_t arena_len,
-                                                       GTab t, gm_verdict *__restrict__ out,
+                                                       GTab tg, gm_verdict *__restrict__ out,
                                                        unsigned long long *__restrict__ counters,
                                                        uint32_t *__restrict__ blk2rec, uint32_t nblk,
                                                        uint32_t *__restrict__ hcnt, int prio,
@@ -836,6 +882,25 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
     // latency-bound waves finish early instead of stretching past the scan (GM_ROUTE_PRIO)
     if (prio) __builtin_amdgcn_s_setprio(2);
     __shared__ uint32_t hist[LDS_HIST_MAX];
+    // the generation's hot tables in LDS (gm_tables.hpp ROUTE_STAGE_BYTES): every pointer into
+    // the hot prefix is rebased onto the block's copy; generic (flat) loads then hit LDS
+    __shared__ uint4 hot[ROUTE_STAGE_BYTES / 16];
+    GTab t = tg;
+    if (tg.hot_len) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(tg.hot_base);
+        for (uint32_t k = threadIdx.x; k < tg.hot_len / 16; k += blockDim.x) hot[k] = src[k];
+        const uint8_t *lb = reinterpret_cast<const uint8_t *>(hot);
+        auto rb = [&](const void *p) { return lb + (reinterpret_cast<const uint8_t *>(p) - tg.hot_base); };
+        t.ports = (const DPort *)rb(tg.ports);
+        t.names = (const DName *)rb(tg.names);
+        t.wild_head = (const DName *)rb(tg.wild_head);
+        t.wild_tail = (const DName *)rb(tg.wild_tail);
+        t.servers = (const DServer *)rb(tg.servers);
+        t.server_ifs = (const DServerIf *)rb(tg.server_ifs);
+        t.small = (const DSmallLoc *)rb(tg.small);
+        t.locs = (const DLoc *)rb(tg.locs);
+        t.name_bytes = rb(tg.name_bytes);
+    }
     const bool use_hist = t.n_locs <= LDS_HIST_MAX;
     if (use_hist) for (uint32_t k = threadIdx.x; k < t.n_locs; k += blockDim.x) hist[k] = 0;
     // RK: servers with many regex locations -- the prefilter's key bit filter in LDS
@@ -844,8 +909,10 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
     __syncthreads();
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const Rec r = load_rec(reqs + i);
+        RoutePre pre;
+        route_prefetch(A, arena_len, r, pre);
         RouteOut o;
-        route_one(A, arena_len, reqs + i, r, t, o, RK ? rkb : nullptr);
+        route_one(A, arena_len, reqs + i, r, pre, t, o, RK ? rkb : nullptr);
         uint4 w0, w1;
         w0.x = t.gen; w0.y = o.server; w0.z = o.loc; w0.w = o.ups;
         w1.x = (uint32_t)o.action | ((uint32_t)o.kind << 8) | ((uint32_t)o.bucket << 16) | ((uint32_t)o.match << 24);
@@ -1030,6 +1097,13 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
     c->flags = flags;
     if (!(flags & GM_CREATE_COMPILE_ONLY)) {
         if (hipSetDevice(hip_device) != hipSuccess) { t_err = "hipSetDevice failed"; delete c; return nullptr; }
+        // the WAF scan's Bloom filter is dynamic LDS beyond the 64 KiB default
+        const void *scans[] = {(const void *)k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH>, (const void *)k_waf_scan<1, SCAN_DEPTH>,
+                               (const void *)k_waf_scan<2, SCAN_DEPTH>, (const void *)k_waf_scan<3, SCAN_DEPTH>};
+        for (const void *f : scans)
+            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SCAN_LDS_BYTES) != hipSuccess) {
+                t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
+            }
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
             c->cu_count = cus;
@@ -1166,38 +1240,48 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     // ---- fork: k_route on the side stream, beside the WAF scan (independent inputs; its waves
     // fit beside the scan's one workgroup per CU; issued after the scan so the scan claims the
     // CUs first).  It writes the verdicts, the location counters, blk2rec and zeroes the counts.
-    HIPCHK(c, hipEventRecord(S->ev_fork, s));
-    HIPCHK(c, hipStreamWaitEvent(S->side, S->ev_fork, 0));
+    // GM_CREATE_SERIAL (measurement): the route alone first, on the caller's stream.
+    const bool serial = c->flags & GM_CREATE_SERIAL;
+    hipStream_t rs = serial ? s : S->side;
+    if (!serial) {
+        HIPCHK(c, hipEventRecord(S->ev_fork, s));
+        HIPCHK(c, hipStreamWaitEvent(S->side, S->ev_fork, 0));
+    }
+    auto launch_route = [&]() -> int {
+        // beside the scan, 2 route blocks per CU: 1 leaves the route the tail of the step, 3+
+        // steal issue slots from the scan (measured on C4: 6.75 / 5.88 / 5.99 ms per step)
+        const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
+                                                                     (uint32_t)c->cu_count * (serial ? 8 : 2)));
+        if (prof) HIPCHK(c, hipEventRecord(S->ev_route[0], rs));
+        // raised issue priority beside the scan: the route's short latency-bound waves finish
+        // early instead of stretching past the scan
+        if (t.rk_keys)
+            k_route<5, true><<<nb, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1, dlen);
+        else
+            k_route<5><<<nb, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1, dlen);
+        HIPCHK(c, hipGetLastError());
+        if (prof) HIPCHK(c, hipEventRecord(S->ev_route[1], rs));
+        if (!serial) HIPCHK(c, hipEventRecord(S->ev_join, rs));
+        S->route_side = true;
+        return GM_OK;
+    };
+    if (serial && (e = launch_route())) return e;
     if (mark(1)) return GM_E_HIP;
     // persistent scan grid: one 1024-thread workgroup per CU (128 KiB LDS prefilter); every wave
     // owns a contiguous arena range and a private candidate region of wcap records
-    if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
-    else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
-    else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
-    else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, 0, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
+    if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
+    else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
+    else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
+    else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
     HIPCHK(c, hipGetLastError());
-    {
-        const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
-                                                                     (uint32_t)c->cu_count * 8));
-        if (prof) HIPCHK(c, hipEventRecord(S->ev_route[0], S->side));
-        // raised issue priority: the route's short latency-bound waves finish early instead of
-        // stretching past the scan
-        if (t.rk_keys)
-            k_route<5, true><<<nb, ROUTE_BLOCK, 0, S->side>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1, dlen);
-        else
-            k_route<5><<<nb, ROUTE_BLOCK, 0, S->side>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1, dlen);
-        HIPCHK(c, hipGetLastError());
-        if (prof) HIPCHK(c, hipEventRecord(S->ev_route[1], S->side));
-        HIPCHK(c, hipEventRecord(S->ev_join, S->side));
-        S->route_side = true;
-    }
+    if (!serial && (e = launch_route())) return e;
     if (mark(2)) return GM_E_HIP;
     const uint32_t bcap = (uint32_t)std::min<size_t>(S->cap_surv / scan_blocks, 0xFFFFFFFFu);
     k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, S->d_ccnt, W, t, S->d_surv, bcap, S->d_ccnt + W,
                                                 S->d_status);
     HIPCHK(c, hipGetLastError());
     // join: blk2rec, the verdicts and the zeroed counts are complete before the exact check
-    HIPCHK(c, hipStreamWaitEvent(s, S->ev_join, 0));
+    if (!serial) HIPCHK(c, hipStreamWaitEvent(s, S->ev_join, 0));
     constexpr uint32_t EXACT_SUB = 8;
     k_waf_exact<<<scan_blocks * EXACT_SUB, 256, 0, s>>>(A, alen, reqs, n, S->d_blk2rec, t, S->d_surv, bcap,
                                                          S->d_ccnt + W, EXACT_SUB, S->d_pairs, (uint32_t)S->cap_pairs,

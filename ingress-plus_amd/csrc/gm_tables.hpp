@@ -216,7 +216,14 @@ struct TabHeader {
     uint64_t off_small;            // DSmallLoc lists
     uint64_t off_rk_ents;          // DRlocEnt lists
     uint64_t off_rk_bloom;         // RK_BLOOM_WORDS: one bit per (server, key), top bits of rk_hash
+    uint64_t off_name_bytes;       // server-name strings (DName.name_off), 64 B of slack
+    uint64_t off_hot_end;          // [off_ports, off_hot_end): the route's hot tables, contiguous
 };
+// The route's hot tables -- ports, the three name tables, servers, server ifs, small-location
+// lists, locations and the name strings -- are laid out first and contiguously in the image;
+// k_route copies them into LDS when they fit ROUTE_STAGE_BYTES (small configs: the cafe Ingress,
+// VirtualServers), so its per-request chain of dependent table reads hits LDS, not L2.
+constexpr uint32_t ROUTE_STAGE_BYTES = 8192;
 
 struct GTab {                // device pointers, built on host from the image base
     const DPort *ports; const DName *names; const DName *wild_head; const DName *wild_tail;
@@ -229,13 +236,20 @@ struct GTab {                // device pointers, built on host from the image ba
     const DLitBucket *lit_buckets; const DLit *lits; const DSigRegex *sig_regex; const uint32_t *always;
     const DRlocKey *rk; const uint32_t *rk_ids; uint32_t rk_mask; const DSmallLoc *small; const DRlocEnt *rk_ents;
     const uint32_t *rk_bloom; uint32_t rk_keys;
+    const uint8_t *name_bytes;
+    const uint8_t *hot_base; uint32_t hot_len;   // the hot prefix (hot_len 0: larger than ROUTE_STAGE_BYTES)
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
     uint32_t gen;
 };
 
 // hashing shared by compiler and kernels
-__host__ __device__ inline uint32_t fnv1a_step(uint32_t h, uint32_t b) { return (h ^ b) * 16777619u; }
+// server-name hash: 4-byte little-endian words of the lowercased name (the last one zero padded),
+// so the device hashes a host held in registers a word per step (SWAR), not a byte per step
+__host__ __device__ inline uint32_t name_hash_word(uint32_t h, uint32_t w) {
+    h ^= w; h *= 0x9E3779B1u; return h ^ (h >> 15);
+}
+__host__ __device__ inline uint32_t name_hash_init(uint32_t len) { return 2166136261u ^ (len * 0x85EBCA77u); }
 __host__ __device__ inline uint32_t name_hash_fin(uint32_t h, uint32_t port_idx) {
     h ^= port_idx * 0x9E3779B9u; h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13;
     return h | 1u;           // never 0 (0 marks an empty slot)

@@ -34,6 +34,7 @@ STATS_FIELDS64 = ["table_bytes", "lds_bytes_scan", "last_candidates", "last_pair
 STATS_FIELDS_MS = ["last_ms_route", "last_ms_scan", "last_ms_verify", "last_ms_tail"]
 STATS_FIELDS_WAF = ["n_waf_keys", "bloom_pk", "bloom_fp_ppm", "last_ctx_pass", "last_jobs", "reserved0"]
 GM_CREATE_PROFILE = 0x2
+GM_CREATE_SERIAL = 0x4
 
 
 class GmStats(ctypes.Structure):
@@ -95,9 +96,10 @@ class GmError(RuntimeError):
 class Engine:
     """One context per HIP device (one process per GPU)."""
 
-    def __init__(self, device: int = 0, compile_only: bool = False, profile: bool = False):
+    def __init__(self, device: int = 0, compile_only: bool = False, profile: bool = False, serial: bool = False):
         L = lib()
-        fl = (GM_CREATE_COMPILE_ONLY if compile_only else 0) | (GM_CREATE_PROFILE if profile else 0)
+        fl = (GM_CREATE_COMPILE_ONLY if compile_only else 0) | (GM_CREATE_PROFILE if profile else 0) | \
+             (GM_CREATE_SERIAL if serial else 0)
         self.h = L.gm_create(device, fl)
         if not self.h:
             raise GmError(-1, L.gm_last_error(None).decode())
