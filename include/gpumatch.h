@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 2u
+#define GM_ABI_VERSION 3u
 
 /* ---------------------------------------------------------------- status codes */
 #define GM_OK            0
@@ -179,7 +179,10 @@ typedef struct gm_stats_t {
      * and the modelled false-positive weight per probed window (ppm) the compiler chose on. */
     uint32_t n_waf_keys, bloom_pk, bloom_fp_ppm;
     /* last batch: candidate windows passing the stage-2 context filter; regex jobs queued */
-    uint32_t last_ctx_pass, last_jobs, reserved0;
+    uint32_t last_ctx_pass, last_jobs;
+    uint32_t n_peers;             /* upstream `server` peers: gm_peer_state entries     */
+    uint32_t n_upstreams_deferred;/* upstreams whose balancing the engine leaves to nginx */
+    uint32_t reserved1;
 } gm_stats_t;
 
 typedef struct gm_ctx gm_ctx;
@@ -265,6 +268,45 @@ typedef struct gm_wire_msg {
 int         gm_parse_requests(gm_ctx *ctx, const uint8_t *wire, const gm_wire_msg *msgs, uint32_t n,
                               gm_req *reqs, uint8_t *arena, uint64_t arena_cap, uint64_t *arena_len_dev,
                               void *stream);
+
+/* ---------------------------------------------------------------- upstream peer selection
+ * (the step after the path.)  The upstream blocks the templates render
+ * (version1/nginx.ingress.tmpl:2-8, version2/nginx.virtualserver.tmpl:2-10) -- `server` lines
+ * from the endpoints (ingress.go:277-301) and the LBMethod (default "random two least_conn",
+ * config_params.go:123; ParseLBMethod parsing_helpers.go:89-161) -- restated per request:
+ * round robin and least_conn (nginx's smooth weighted round robin / least_conn with its
+ * current_weight tie-break, in request order), ip_hash, hash <key> [consistent], random,
+ * random two [least_conn].  Peer ids are global indices into the generation's peer table
+ * (upstreams in sorted-name order, servers in config order; gm_peer_address names them).
+ *
+ * The balancing state nginx keeps per peer (active connections, current_weight, down) is a
+ * caller-owned device array of gm_stats_t.n_peers gm_peer_state entries, so several
+ * independent balancers (e.g. one per worker) can share one ctx.  gm_select_peers reads it at
+ * the start of the batch, applies the batch's picks in request order (conns += picks,
+ * current_weight as nginx would leave it) and gm_release_peers ends connections.  Calls that
+ * share a state array must be ordered on one stream. */
+typedef struct gm_peer_state {
+    uint32_t conns;           /* active connections (nginx peer->conns)                   */
+    int32_t  current_weight;  /* smooth-WRR / least_conn tie-break state                  */
+    uint32_t flags;           /* GM_PEER_DOWN: unavailable (down, or max_fails reached)   */
+    uint32_t reserved;
+} gm_peer_state;
+#define GM_PEER_DOWN   0x1u
+#define GM_PEER_DEFER  0xFFFFFFFEu  /* peer_out: the engine does not model this upstream / stale gen */
+/* peer_out: GM_NONE = no peer (not a proxied verdict, or no live peer: nginx's 502) */
+
+/* (Re)initialise a state array for the live generation: conns 0, current_weight 0, DOWN for
+ * `server ... down`.  n_peers must equal gm_stats_t.n_peers.  Device pointer, async. */
+int         gm_peers_init(gm_ctx *ctx, gm_peer_state *state, uint32_t n_peers, void *stream);
+/* peer_out[i] = the peer of verdicts[i] (proxied verdicts of the live generation only).  `in` is
+ * the batch the verdicts came from (device pointers: hash keys read its variables).  Async. */
+int         gm_select_peers(gm_ctx *ctx, const gm_batch *in, const gm_verdict *verdicts, gm_peer_state *state,
+                            uint32_t n_peers, uint32_t *peer_out, void *stream);
+/* conns -= 1 for each peer id in peer_ids[0 .. n) (GM_NONE / GM_PEER_DEFER skipped).  Async. */
+int         gm_release_peers(gm_ctx *ctx, const uint32_t *peer_ids, uint32_t n, gm_peer_state *state,
+                             uint32_t n_peers, void *stream);
+/* Host: the `server` address of a peer id ("10.0.0.1:8080") and its upstream id. */
+int         gm_peer_address(gm_ctx *ctx, uint32_t peer, char *buf, size_t cap, uint32_t *upstream_id);
 
 int         gm_stats(gm_ctx *ctx, gm_stats_t *out);
 /* Message of the calling thread's last failing call (thread-local; ctx is not consulted). */

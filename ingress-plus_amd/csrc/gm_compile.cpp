@@ -149,8 +149,19 @@ struct MapIR {
 };
 struct SplitIR { std::string src, var; std::vector<std::pair<std::string, std::string>> parts; };
 
+// an `upstream` block (version1/nginx.ingress.tmpl:2-8, version2/nginx.virtualserver.tmpl:2-10)
+struct UpstreamIR {
+    std::string name;
+    uint32_t method = UM_RR;
+    std::string key;                 // hash / hash consistent key (complex value)
+    bool defer = false;              // a construct the engine does not model
+    struct Peer { std::string addr; bool down = false; };
+    std::vector<Peer> peers;
+};
+
 struct Model {
     std::vector<Server> servers;
+    std::vector<UpstreamIR> upstream_defs;
     std::vector<Loc> locs;
     std::map<std::string, MapIR> maps;
     std::map<std::string, SplitIR> splits;
@@ -273,6 +284,45 @@ struct Builder {
         M.servers.push_back(std::move(S));
     }
 
+    // Balancing method and peers of an upstream block.  The method directive nginx applies is
+    // the last one (a second one only warns "load balancing method redefined"); `server`
+    // parameters other than the ones the templates emit (max_fails, fail_timeout; slow_start is
+    // Plus) and an explicit weight=1 / max_conns=0 make the upstream UM_DEFER.
+    void upstream(const Dir &d) {
+        UpstreamIR U;
+        U.name = d.a[1];
+        for (const Dir &k : d.body) {
+            if (k.a.empty()) continue;
+            const std::string &m = k.a[0];
+            if (m == "server" && k.a.size() >= 2) {
+                UpstreamIR::Peer p;
+                p.addr = k.a[1];
+                for (size_t q = 2; q < k.a.size(); q++) {
+                    const std::string &a = k.a[q];
+                    if (a == "down") p.down = true;
+                    else if (a.rfind("max_fails=", 0) == 0 || a.rfind("fail_timeout=", 0) == 0 ||
+                             a.rfind("slow_start=", 0) == 0 || a == "weight=1" || a == "max_conns=0") {}
+                    else U.defer = true;   // weight, backup, max_conns, resolve, service, route
+                }
+                U.peers.push_back(p);
+            } else if (m == "least_conn" && k.a.size() == 1) U.method = UM_LEAST_CONN;
+            else if (m == "ip_hash" && k.a.size() == 1) U.method = UM_IP_HASH;
+            else if (m == "hash" && (k.a.size() == 2 || (k.a.size() == 3 && k.a[2] == "consistent"))) {
+                U.method = k.a.size() == 3 ? UM_CHASH : UM_HASH;
+                U.key = k.a[1];
+            } else if (m == "random") {
+                if (k.a.size() == 1) U.method = UM_RANDOM;
+                else if (k.a[1] == "two" && (k.a.size() == 2 || (k.a.size() == 3 && k.a[2] == "least_conn")))
+                    U.method = UM_RANDOM2;
+                else U.defer = true;   // random two least_time=... (Plus)
+            } else if (m == "least_time" || m == "sticky" || m == "queue" || m == "ntlm" || m == "hash") {
+                U.defer = true;
+            }
+            // keepalive, zone, keepalive_timeout / _requests: connection reuse, not the choice
+        }
+        M.upstream_defs.push_back(std::move(U));
+    }
+
     void http(const std::vector<Dir> &body) {
         for (const Dir &d : body) {
             if (d.a.empty()) continue;
@@ -283,6 +333,7 @@ struct Builder {
                 M.http_waf = waf_mode(d.a[1]);
             } else if (n == "upstream" && d.block && d.a.size() == 2) {
                 M.upstreams.push_back(d.a[1]);
+                upstream(d);
             } else if (n == "map" && d.block && d.a.size() == 3) {
                 MapIR m;
                 m.src = d.a[1]; m.var = lower(d.a[2].substr(1));
@@ -1023,6 +1074,116 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     ups.erase(std::unique(ups.begin(), ups.end()), ups.end());
     st.n_upstreams = (uint32_t)ups.size();
 
+    // ---- upstream peers (§8 f3): one DUpstream per sorted name (first block of a name wins;
+    // nginx rejects a duplicate upstream outright)
+    std::vector<DUpstream> dups(ups.size());
+    std::vector<DKeyPart> key_parts;
+    std::vector<DPoint> points;
+    std::vector<uint32_t> peer_init;
+    R.peer_addrs.clear(); R.peer_ups.clear();
+    {
+        std::map<std::string, const UpstreamIR *> defs;
+        for (const UpstreamIR &U : M.upstream_defs) defs.emplace(U.name, &U);
+        for (size_t u = 0; u < ups.size(); u++) {
+            DUpstream &D = dups[u];
+            memset(&D, 0, sizeof D);
+            D.first_peer = (uint32_t)peer_init.size();
+            const UpstreamIR *U = defs.count(ups[u]) ? defs[ups[u]] : nullptr;
+            if (!U) { D.method = UM_DEFER; st.n_upstreams_deferred++; continue; }
+            D.method = U->method;
+            D.n_peers = (uint32_t)U->peers.size();
+            for (const auto &p : U->peers) {
+                peer_init.push_back(p.down ? GM_PEER_DOWN : 0u);
+                R.peer_addrs.push_back(p.addr);
+                R.peer_ups.push_back((uint32_t)u);
+            }
+            bool defer = U->defer;
+            if ((D.method == UM_RR || D.method == UM_LEAST_CONN) && D.n_peers > SEQ_PEERS_MAX) defer = true;
+            if (D.method == UM_HASH || D.method == UM_CHASH) {
+                // key = literal text and $variables; the engine's variables except $host (nginx's
+                // $host is the validated name or the server_name, not the raw header)
+                D.first_part = (uint32_t)key_parts.size();
+                const std::string &k = U->key;
+                size_t i = 0;
+                while (i < k.size() && !defer) {
+                    if (k[i] == '$') {
+                        size_t j = i + 1, e;
+                        std::string nm;
+                        if (j < k.size() && k[j] == '{') {
+                            e = k.find('}', j);
+                            if (e == std::string::npos) { defer = true; break; }
+                            nm = k.substr(j + 1, e - j - 1); e++;
+                        } else {
+                            e = j;
+                            while (e < k.size() && (isalnum((unsigned char)k[e]) || k[e] == '_')) e++;
+                            nm = k.substr(j, e - j);
+                        }
+                        const int sid = lower(nm) == "host" ? -1 : C.src("$" + nm);
+                        if (sid < 0) { defer = true; break; }
+                        key_parts.push_back(DKeyPart{(uint32_t)sid, KEY_PART_VAR});
+                        i = e;
+                    } else {
+                        size_t e = k.find('$', i);
+                        if (e == std::string::npos) e = k.size();
+                        key_parts.push_back(DKeyPart{C.put_bytes(k.substr(i, e - i)), (uint32_t)(e - i)});
+                        i = e;
+                    }
+                }
+                D.n_parts = (uint32_t)key_parts.size() - D.first_part;
+                // chash: two server lines with one address would share ring points (nginx then
+                // round-robins between them): not modelled
+                std::set<std::string> seen;
+                for (const auto &p : U->peers) if (!seen.insert(p.addr).second && D.method == UM_CHASH) defer = true;
+            }
+            if (D.method == UM_CHASH && !defer) {
+                // ngx_http_upstream_update_chash: per server, 160 * weight points; the base CRC over
+                // host, one NUL byte and port (split at the last ':' followed by digits only; "unix:"
+                // paths have no port), each point = final(base + the previous point's 4 LE bytes)
+                static constexpr Crc32Table T = make_crc32_table();
+                auto upd = [&](uint32_t c, const uint8_t *p, size_t n) {
+                    for (size_t q = 0; q < n; q++) c = T.t[(c ^ p[q]) & 0xFF] ^ (c >> 8);
+                    return c;
+                };
+                std::vector<DPoint> ring;
+                for (uint32_t j = 0; j < D.n_peers; j++) {
+                    const std::string &sv = U->peers[j].addr;
+                    std::string host = sv, port;
+                    if (sv.size() >= 5 && lower(sv.substr(0, 5)) == "unix:") host = sv.substr(5);
+                    else {
+                        for (size_t q = 0; q < sv.size(); q++) {
+                            const char c = sv[sv.size() - q - 1];
+                            if (c == ':') { host = sv.substr(0, sv.size() - q - 1); port = sv.substr(sv.size() - q); break; }
+                            if (c < '0' || c > '9') break;
+                        }
+                    }
+                    uint32_t base = 0xFFFFFFFFu;
+                    base = upd(base, (const uint8_t *)host.data(), host.size());
+                    const uint8_t nul = 0;
+                    base = upd(base, &nul, 1);
+                    base = upd(base, (const uint8_t *)port.data(), port.size());
+                    uint32_t prev = 0;
+                    for (int q = 0; q < 160; q++) {
+                        const uint8_t pb[4] = {(uint8_t)prev, (uint8_t)(prev >> 8), (uint8_t)(prev >> 16), (uint8_t)(prev >> 24)};
+                        const uint32_t h = upd(base, pb, 4) ^ 0xFFFFFFFFu;
+                        ring.push_back(DPoint{h, j});
+                        prev = h;
+                    }
+                }
+                // sorted by hash; equal hashes keep one point (nginx keeps the first after an
+                // unstable sort -- here the lowest peer index)
+                std::sort(ring.begin(), ring.end(), [](const DPoint &a, const DPoint &b) {
+                    return a.hash != b.hash ? a.hash < b.hash : a.peer < b.peer;
+                });
+                D.first_point = (uint32_t)points.size();
+                for (size_t q = 0; q < ring.size(); q++)
+                    if (q == 0 || ring[q].hash != ring[q - 1].hash) points.push_back(ring[q]);
+                D.n_points = (uint32_t)points.size() - D.first_point;
+            }
+            if (defer) { D.method = UM_DEFER; st.n_upstreams_deferred++; }
+        }
+    }
+    st.n_peers = (uint32_t)peer_init.size();
+
     // ---- ports
     std::vector<DPort> ports;
     std::map<int, int> port_idx;
@@ -1461,6 +1622,10 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_always = I.put(always);
     h.n_rk_cap = rkcap; h.n_rk_ids = (uint32_t)rk_ids.size(); h.n_rk_ents_keys = (uint32_t)rk_lists.size();
     h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_rk_ents = I.put(rk_ents); h.off_rk_bloom = I.put(rk_bloom);
+    h.n_ups = (uint32_t)dups.size(); h.n_peers = (uint32_t)peer_init.size();
+    h.n_key_parts = (uint32_t)key_parts.size(); h.n_points = (uint32_t)points.size();
+    h.off_ups = I.put(dups); h.off_key_parts = I.put(key_parts); h.off_points = I.put(points);
+    h.off_peer_init = I.put(peer_init);
     C.bytes.resize(C.bytes.size() + 64, 0);   // slack: vector compares may over-read
     h.off_bytes = I.put(C.bytes);
     I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
@@ -1514,6 +1679,11 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.name_bytes = b + h.off_name_bytes;
     t.hot_base = b + h.off_ports;
     t.hot_len = h.off_hot_end - h.off_ports <= ROUTE_STAGE_BYTES ? (uint32_t)(h.off_hot_end - h.off_ports) : 0u;
+    t.ups = (const DUpstream *)(b + h.off_ups);
+    t.key_parts = (const DKeyPart *)(b + h.off_key_parts);
+    t.points = (const DPoint *)(b + h.off_points);
+    t.peer_init = (const uint32_t *)(b + h.off_peer_init);
+    t.n_ups = h.n_ups; t.n_peers = h.n_peers;
     t.n_ports = h.n_ports;
     t.names_mask = h.n_names_cap - 1; t.wild_head_mask = h.n_wild_head_cap - 1; t.wild_tail_mask = h.n_wild_tail_cap - 1;
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;

@@ -17,6 +17,8 @@ struct CompileResult {
     std::vector<uint8_t> image;   // TabHeader at offset 0, sections at hdr.off_*
     TabHeader hdr{};
     gm_stats_t stats{};
+    std::vector<std::string> peer_addrs;   // per global peer id: the `server` address
+    std::vector<uint32_t> peer_ups;        // per global peer id: its upstream id
 };
 
 CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen);

@@ -971,6 +971,8 @@ struct Generation {
     GTab tab{};
     gm_stats_t stats{};
     std::vector<uint8_t> host_image;   // kept for host-side introspection (gpumatch_debug.h)
+    std::vector<std::string> peer_addrs;   // gm_peer_address
+    std::vector<uint32_t> peer_ups;
     ~Generation() {
         for (void *p : {(void *)d_image, (void *)d_counters, (void *)d_counters_sum})
             if (p) (void)hipFree(p);
@@ -1000,10 +1002,16 @@ struct Scratch {
     uint8_t *d_stage = nullptr; size_t cap_stage = 0;            // GM_BATCH_HOST staging
     uint64_t *d_wsize = nullptr, *d_wbase = nullptr; size_t cap_wsize = 0, cap_wbase = 0;   // wire parser
     uint8_t *d_wtemp = nullptr; size_t cap_wtemp = 0;
+    uint32_t *d_pk = nullptr; size_t cap_pk = 0;     // peer selection: keys, values (x2: sorted),
+    uint32_t *d_pseg = nullptr; size_t cap_pseg = 0; // per-upstream ranges, periodic programs
+    uint4 *d_pprog = nullptr; size_t cap_pprog = 0;
+    uint32_t *d_ppat = nullptr; size_t cap_ppat = 0;
+    uint8_t *d_ptemp = nullptr; size_t cap_ptemp = 0;
     ~Scratch() {
         for (void *p : {(void *)d_status, (void *)d_blk2rec, (void *)d_cand, (void *)d_surv, (void *)d_pairs,
                         (void *)d_jobs, (void *)d_set, (void *)d_cnt, (void *)d_start, (void *)d_ccnt,
-                        (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp})
+                        (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp,
+                        (void *)d_pk, (void *)d_pseg, (void *)d_pprog, (void *)d_ppat, (void *)d_ptemp})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
         for (auto &e : ev) if (e) (void)hipEventDestroy(e);
@@ -1135,6 +1143,8 @@ int gm_load_generation(gm_ctx *c, const void *blob, size_t len, uint32_t gen) {
     g->hdr = R.hdr;
     g->host_image = R.image;
     g->stats = R.stats;
+    g->peer_addrs = std::move(R.peer_addrs);
+    g->peer_ups = std::move(R.peer_ups);
     if (!(c->flags & GM_CREATE_COMPILE_ONLY)) {
         HIPCHK(c, hipSetDevice(c->dev));
         HIPCHK(c, hipMalloc((void **)&g->d_image, R.image.size()));
@@ -1658,6 +1668,7 @@ __global__ __launch_bounds__(256) void k_uri_normalize(const uint8_t *A, const u
 }
 
 #include "gm_wire.inc"
+#include "gm_peers.inc"
 }  // namespace
 
 extern "C" int gm_normalize_uris(gm_ctx *c, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
@@ -1716,4 +1727,103 @@ extern "C" int gm_debug_wire_sizes(gm_ctx *c, void *stream, uint64_t *out, size_
     HIPCHK(c, hipStreamSynchronize((hipStream_t)stream));
     HIPCHK(c, hipMemcpy(out, S->d_wsize, std::min(n, S->cap_wsize) * 8, hipMemcpyDeviceToHost));
     return GM_OK;
+}
+
+// ---------------------------------------------------------------- upstream peer selection (§8 f3)
+extern "C" int gm_peers_init(gm_ctx *c, gm_peer_state *state, uint32_t n_peers, void *stream) {
+    if (!c) return fail(c, GM_E_INVAL, "null ctx");
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
+    HIPCHK(c, hipSetDevice(c->dev));
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    const Generation *g = c->gen;
+    if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
+    if (n_peers != g->tab.n_peers) return fail(c, GM_E_INVAL, "n_peers differs from the generation's peer count");
+    if (n_peers == 0) return GM_OK;
+    if (!state) return fail(c, GM_E_INVAL, "null state");
+    k_peers_init<<<std::min<uint32_t>((n_peers + 255) / 256, 1024), 256, 0, (hipStream_t)stream>>>(g->tab, state);
+    HIPCHK(c, hipGetLastError());
+    return GM_OK;
+}
+
+extern "C" int gm_select_peers(gm_ctx *c, const gm_batch *in, const gm_verdict *verdicts, gm_peer_state *state,
+                               uint32_t n_peers, uint32_t *peer_out, void *stream) {
+    if (!c || !in) return fail(c, GM_E_INVAL, "null argument");
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
+    if (in->flags & GM_BATCH_HOST) return fail(c, GM_E_INVAL, "gm_select_peers takes device buffers");
+    const uint32_t n = in->n;
+    if (n && (!verdicts || !peer_out || !in->reqs)) return fail(c, GM_E_INVAL, "null argument");
+    if (((uintptr_t)verdicts & 15) || ((uintptr_t)in->reqs & 15)) return fail(c, GM_E_INVAL, "verdicts / reqs must be 16-byte aligned");
+    HIPCHK(c, hipSetDevice(c->dev));
+    hipStream_t s = (hipStream_t)stream;
+    Scratch *S = scratch_for(c, s);
+    if (!S) return fail(c, GM_E_NOMEM, t_err);
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    const Generation *g = c->gen;
+    if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
+    const GTab &t = g->tab;
+    if (n_peers != t.n_peers) return fail(c, GM_E_INVAL, "n_peers differs from the generation's peer count");
+    if (t.n_peers && !state) return fail(c, GM_E_INVAL, "null state");
+    if (n == 0) return GM_OK;
+    const uint32_t nu = std::max<uint32_t>(t.n_ups, 1);
+    int e;
+    if ((e = grow(c, s, S->d_pk, S->cap_pk, (size_t)n * 4))) return e;
+    if ((e = grow(c, s, S->d_pseg, S->cap_pseg, (size_t)nu * 2))) return e;
+    if ((e = grow(c, s, S->d_pprog, S->cap_pprog, (size_t)nu))) return e;
+    if ((e = grow(c, s, S->d_ppat, S->cap_ppat, (size_t)std::max<uint32_t>(t.n_peers, 1) * 2))) return e;
+    uint32_t *keys = S->d_pk, *vals = keys + n, *ks = vals + n, *vs = ks + n;
+    const int bits = t.n_ups ? 32 - __builtin_clz(t.n_ups) : 1;   // keys <= n_ups (the sentinel)
+    size_t tb = 0;
+    HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, ks, vals, vs, (int)n, 0, bits, s));
+    if ((e = grow(c, s, S->d_ptemp, S->cap_ptemp, tb))) return e;
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8));
+    k_peer_pick<<<blocks, 256, 0, s>>>(in->reqs, in->arena, verdicts, n, t, state, peer_out, keys, vals);
+    HIPCHK(c, hipGetLastError());
+    if (t.n_ups) {
+        HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(S->d_ptemp, tb, keys, ks, vals, vs, (int)n, 0, bits, s));
+        HIPCHK(c, hipMemsetAsync(S->d_pseg, 0, (size_t)nu * 2 * 4, s));
+        k_peer_segs<<<blocks, 256, 0, s>>>(ks, n, t.n_ups, S->d_pseg, S->d_pseg + nu);
+        HIPCHK(c, hipGetLastError());
+        k_peer_seq<<<t.n_ups, 64, 0, s>>>(t, state, S->d_pseg, S->d_pseg + nu, vs, peer_out, S->d_ppat, S->d_pprog);
+        HIPCHK(c, hipGetLastError());
+        k_peer_fill<<<blocks, 256, 0, s>>>(ks, vs, n, t, S->d_pseg, S->d_pprog, S->d_ppat, peer_out);
+        HIPCHK(c, hipGetLastError());
+    }
+    if (t.n_peers) {
+        k_peer_count<<<blocks, 256, 0, s>>>(peer_out, n, state, t.n_peers, 1);
+        HIPCHK(c, hipGetLastError());
+    }
+    return GM_OK;
+}
+
+extern "C" int gm_release_peers(gm_ctx *c, const uint32_t *peer_ids, uint32_t n, gm_peer_state *state,
+                                uint32_t n_peers, void *stream) {
+    if (!c) return fail(c, GM_E_INVAL, "null ctx");
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
+    HIPCHK(c, hipSetDevice(c->dev));
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    const Generation *g = c->gen;
+    if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
+    if (n_peers != g->tab.n_peers) return fail(c, GM_E_INVAL, "n_peers differs from the generation's peer count");
+    if (n == 0 || n_peers == 0) return GM_OK;
+    if (!peer_ids || !state) return fail(c, GM_E_INVAL, "null argument");
+    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8));
+    k_peer_count<<<blocks, 256, 0, (hipStream_t)stream>>>(peer_ids, n, state, n_peers, -1);
+    HIPCHK(c, hipGetLastError());
+    return GM_OK;
+}
+
+extern "C" int gm_peer_address(gm_ctx *c, uint32_t peer, char *buf, size_t cap, uint32_t *upstream_id) {
+    if (!c) return fail(c, GM_E_INVAL, "null ctx");
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    const Generation *g = c->gen;
+    if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
+    if (peer >= g->peer_addrs.size()) return fail(c, GM_E_INVAL, "peer id out of range");
+    const std::string &a = g->peer_addrs[peer];
+    if (buf && cap) {
+        const size_t m = std::min(cap - 1, a.size());
+        memcpy(buf, a.data(), m);
+        buf[m] = 0;
+    }
+    if (upstream_id) *upstream_id = g->peer_ups[peer];
+    return (int)a.size();
 }

@@ -195,6 +195,49 @@ struct DSigRegex {
                              // factor, every request; PREFIX = verified inline in k_waf_verify
 };
 
+// ---- upstream peer selection ---------------------------------------------
+// One DUpstream per entry of the sorted upstream-name table (the verdict's upstream_id), its
+// `server` lines as peers [first_peer, first_peer + n_peers) in config order (global peer ids).
+// Methods follow the upstream block the templates render (version1/nginx.ingress.tmpl:2-8,
+// version2/nginx.virtualserver.tmpl:2-10) from LBMethod (config_params.go:123, ParseLBMethod
+// parsing_helpers.go:89-161).  UM_DEFER: a construct the engine does not model (weights, backup,
+// max_conns, Plus-only methods, hash keys over unsupported variables) -- the data plane asks nginx.
+enum : uint32_t { UM_RR = 0, UM_LEAST_CONN = 1, UM_IP_HASH = 2, UM_HASH = 3, UM_CHASH = 4, UM_RANDOM = 5,
+                  UM_RANDOM2 = 6, UM_DEFER = 7 };
+struct DUpstream {
+    uint32_t first_peer, n_peers;
+    uint32_t method;         // UM_*
+    uint32_t first_part, n_parts;    // hash key: DKeyPart list (literal text and variables)
+    uint32_t first_point, n_points;  // UM_CHASH: sorted, de-duplicated DPoint ring
+    uint32_t pad;
+};
+constexpr uint32_t KEY_PART_VAR = 0xFFFFFFFFu;
+struct DKeyPart { uint32_t off; uint32_t len; };   // len KEY_PART_VAR: off = DSrc index
+struct DPoint { uint32_t hash; uint32_t peer; };    // peer: index within the upstream
+// the sequential methods (RR, least_conn) hold an upstream's peer state in LDS on the device
+constexpr uint32_t SEQ_PEERS_MAX = 1024;
+
+// nginx ngx_crc32 (CRC-32/IEEE, reflected 0xEDB88320): hash keys and the consistent-hash ring
+struct Crc32Table { uint32_t t[256]; };
+constexpr Crc32Table make_crc32_table() {
+    Crc32Table r{};
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+        r.t[i] = c;
+    }
+    return r;
+}
+// $request_id-keyed draw j for `random` / `random two` (nginx draws ngx_random(); the engine
+// draws reproducibly from the request's own random id): splitmix64 finaliser
+__host__ __device__ inline uint32_t peer_draw(uint64_t lo, uint64_t hi, uint32_t j) {
+    uint64_t x = lo ^ (hi * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)(j + 1) * 0xD1B54A32D192ED03ull);
+    x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27; x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return (uint32_t)(x >> 32);
+}
+
 struct TabHeader {
     uint32_t magic, version;
     uint32_t n_ports, n_names_cap, n_wild_head_cap, n_wild_tail_cap;
@@ -218,6 +261,8 @@ struct TabHeader {
     uint64_t off_rk_bloom;         // RK_BLOOM_WORDS: one bit per (server, key), top bits of rk_hash
     uint64_t off_name_bytes;       // server-name strings (DName.name_off), 64 B of slack
     uint64_t off_hot_end;          // [off_ports, off_hot_end): the route's hot tables, contiguous
+    uint32_t n_ups, n_peers, n_key_parts, n_points;
+    uint64_t off_ups, off_key_parts, off_points, off_peer_init;   // peer_init: u32 GM_PEER_DOWN per peer
 };
 // The route's hot tables -- ports, the three name tables, servers, server ifs, small-location
 // lists, locations and the name strings -- are laid out first and contiguously in the image;
@@ -238,6 +283,8 @@ struct GTab {                // device pointers, built on host from the image ba
     const uint32_t *rk_bloom; uint32_t rk_keys;
     const uint8_t *name_bytes;
     const uint8_t *hot_base; uint32_t hot_len;   // the hot prefix (hot_len 0: larger than ROUTE_STAGE_BYTES)
+    const DUpstream *ups; const DKeyPart *key_parts; const DPoint *points; const uint32_t *peer_init;
+    uint32_t n_ups, n_peers;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
     uint32_t gen;

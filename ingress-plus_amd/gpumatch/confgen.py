@@ -89,6 +89,44 @@ def _as_bool(v):
     return None  # GetMapKeyAsBool error -> ignored (annotations.go logs and keeps default)
 
 
+# --------------------------------------------------------------------------- load balancing
+
+_LB_VALID = {"least_conn", "ip_hash", "random", "random two", "random two least_conn"}   # parsing_helpers.go:109-115
+_LB_VALID_PLUS = _LB_VALID | {"random two least_time=header", "random two least_time=last_byte",
+                              "least_time header", "least_time last_byte", "least_time header inflight",
+                              "least_time last_byte inflight"}                          # :117-129
+
+
+def _validate_hash_lb_method(method: str) -> str:
+    """parsing_helpers.go:152-161: "hash <key>" or "hash <key> consistent" (split on single spaces)."""
+    kw = method.split(" ")
+    if kw[0] == "hash" and (len(kw) == 2 or (len(kw) == 3 and kw[2] == "consistent")):
+        return method
+    raise ValueError(f"Invalid load balancing method: {method!r}")
+
+
+def parse_lb_method(method: str, plus: bool = False) -> str:
+    """ParseLBMethod / ParseLBMethodForPlus (parsing_helpers.go:89-150): the directive the upstream
+    block renders ("" = nginx's default round robin); ValueError for an invalid method."""
+    method = method.strip(" \t\n\r\v\f")   # strings.TrimSpace
+    if method == "round_robin":
+        return ""
+    if method.startswith("hash"):
+        return _validate_hash_lb_method(method)
+    if method in (_LB_VALID_PLUS if plus else _LB_VALID):
+        return method
+    raise ValueError(f"Invalid load balancing method: {method!r}")
+
+
+_GO_INT = re.compile(r"[+-]?[0-9]+")
+
+
+def _go_atoi(v):
+    """strconv.Atoi / ParseInt(s, 10, 64) (GetMapKeyAsInt / GetMapKeyAsInt64): None on error."""
+    s = str(v)
+    return int(s) if _GO_INT.fullmatch(s) else None
+
+
 def parse_annotations(ing: dict, base: dict) -> dict:
     """annotations.go:57-333, restricted to keys that change the request verdict:
     redirect-to-https (:176-182), ssl-redirect (:184-190), listen ports (:266-273),
@@ -103,6 +141,21 @@ def parse_annotations(ing: dict, base: dict) -> dict:
         b = _as_bool(ann["ingress.kubernetes.io/ssl-redirect"])
         if b is not None:
             p["SSLRedirect"] = b
+    if "nginx.org/lb-method" in ann:   # annotations.go:60-74 (OSS: ParseLBMethod; errors keep the base)
+        try:
+            p["LBMethod"] = parse_lb_method(str(ann["nginx.org/lb-method"]), plus=False)
+        except ValueError:
+            pass
+    if "nginx.org/keepalive" in ann:   # annotations.go:275-281
+        v = _go_atoi(ann["nginx.org/keepalive"])
+        if v is not None:
+            p["Keepalive"] = v
+    if "nginx.org/max-fails" in ann:   # annotations.go:283-289
+        v = _go_atoi(ann["nginx.org/max-fails"])
+        if v is not None:
+            p["MaxFails"] = v
+    if "nginx.org/fail-timeout" in ann:   # annotations.go:291-293
+        p["FailTimeout"] = ann["nginx.org/fail-timeout"]
     if "nginx.org/client-max-body-size" in ann:
         p["ClientMaxBodySize"] = ann["nginx.org/client-max-body-size"]
     for key, field in (("nginx.org/listen-ports", "Ports"), ("nginx.org/listen-ports-ssl", "SSLPorts")):

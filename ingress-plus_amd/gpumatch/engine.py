@@ -32,7 +32,8 @@ STATS_FIELDS64 = ["table_bytes", "lds_bytes_scan", "last_candidates", "last_pair
 
 
 STATS_FIELDS_MS = ["last_ms_route", "last_ms_scan", "last_ms_verify", "last_ms_tail"]
-STATS_FIELDS_WAF = ["n_waf_keys", "bloom_pk", "bloom_fp_ppm", "last_ctx_pass", "last_jobs", "reserved0"]
+STATS_FIELDS_WAF = ["n_waf_keys", "bloom_pk", "bloom_fp_ppm", "last_ctx_pass", "last_jobs", "n_peers",
+                    "n_upstreams_deferred", "reserved1"]
 GM_CREATE_PROFILE = 0x2
 GM_CREATE_SERIAL = 0x4
 
@@ -50,7 +51,13 @@ class GmBatch(ctypes.Structure):
 
 EXPORTS = ["gm_create", "gm_destroy", "gm_abi_version", "gm_load_generation", "gm_match_batch", "gm_sync",
            "gm_counters", "gm_counters_reset", "gm_comm_unique_id", "gm_comm_init", "gm_counters_allreduce",
-           "gm_stats", "gm_last_error", "gm_normalize_uris", "gm_counters_global", "gm_parse_requests"]
+           "gm_stats", "gm_last_error", "gm_normalize_uris", "gm_counters_global", "gm_parse_requests",
+           "gm_peers_init", "gm_select_peers", "gm_release_peers", "gm_peer_address"]
+
+# gm_peer_state (include/gpumatch.h)
+PEER_STATE_DTYPE = np.dtype([("conns", "<u4"), ("current_weight", "<i4"), ("flags", "<u4"), ("reserved", "<u4")])
+GM_PEER_DOWN = 0x1
+GM_PEER_DEFER = 0xFFFFFFFE
 
 _lib = None
 
@@ -81,6 +88,13 @@ def lib():
         L.gm_parse_requests.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                         ctypes.c_void_p]
+        L.gm_peers_init.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+        L.gm_select_peers.argtypes = [ctypes.c_void_p, ctypes.POINTER(GmBatch), ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        L.gm_release_peers.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                       ctypes.c_uint32, ctypes.c_void_p]
+        L.gm_peer_address.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t,
+                                      ctypes.c_void_p]
         L.gm_last_error.restype = ctypes.c_char_p
         L.gm_last_error.argtypes = [ctypes.c_void_p]
         _lib = L
@@ -157,6 +171,28 @@ class Engine:
         """gm_parse_requests on device pointers (HTTP/1.x wire bytes -> gm_req records + arena)."""
         self._chk(lib().gm_parse_requests(self.h, wire_ptr, msgs_ptr, n, reqs_ptr, arena_ptr, arena_cap,
                                           arena_len_dev_ptr, stream))
+
+    def peers_init_ptr(self, state_ptr, n_peers, stream=0):
+        """gm_peers_init: the generation's initial balancer state into a device gm_peer_state array."""
+        self._chk(lib().gm_peers_init(self.h, state_ptr, n_peers, stream))
+
+    def select_peers_ptr(self, reqs_ptr, arena_ptr, arena_len, n, verdicts_ptr, state_ptr, n_peers, out_ptr,
+                         stream=0):
+        """gm_select_peers on device pointers: the peer of every proxied verdict (async)."""
+        b = GmBatch(reqs_ptr, arena_ptr, arena_len, n, 0, None)
+        self._chk(lib().gm_select_peers(self.h, ctypes.byref(b), verdicts_ptr, state_ptr, n_peers, out_ptr, stream))
+
+    def release_peers_ptr(self, ids_ptr, n, state_ptr, n_peers, stream=0):
+        self._chk(lib().gm_release_peers(self.h, ids_ptr, n, state_ptr, n_peers, stream))
+
+    def peer_address(self, peer: int):
+        """(address, upstream id) of a global peer id."""
+        buf = ctypes.create_string_buffer(512)
+        up = ctypes.c_uint32(0)
+        rc = lib().gm_peer_address(self.h, peer, buf, 512, ctypes.byref(up))
+        if rc < 0:
+            self._chk(rc)
+        return buf.value.decode(), up.value
 
     def normalize_uris_ptr(self, arena_ptr, off_ptr, len_ptr, n, out_ptr, out_len_ptr, stream=0):
         """gm_normalize_uris on device pointers (nginx $uri normalisation, include/gpumatch.h)."""

@@ -1,0 +1,123 @@
+"""Upstream peer-selection workloads.
+
+The upstream blocks the templates render (``version1/nginx.ingress.tmpl:2-8``,
+``version2/nginx.virtualserver.tmpl:2-10``): ``server <ip>:<port> max_fails=.. fail_timeout=..``
+lines from the endpoints (``ingress.go:277-301``) behind every LBMethod ``ParseLBMethod`` accepts
+(``parsing_helpers.go:89-161``; default ``random two least_conn``, ``config_params.go:123``), plus
+the shapes the engine leaves to nginx (Plus-only methods, weights, ``$host`` keys).  Requests
+vary what the balancers read: ``$remote_addr`` (IPv4, IPv6, unix), ``$request_uri``, ``$arg_*``,
+``$cookie_*``, ``$http_*`` and ``$request_id``.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from . import blob, records
+
+# (method directive, number of servers); "" = round robin
+UPSTREAMS = [
+    ("", 3), ("", 70), ("", 1), ("least_conn", 4), ("least_conn", 67), ("least_conn", 1),
+    ("ip_hash", 5), ("ip_hash", 1), ("hash $request_uri", 6), ("hash $arg_user consistent", 7),
+    ("hash $cookie_session$remote_addr", 4), ("hash ${http_x_user}-k consistent", 5),
+    ("hash $request_id consistent", 64), ("random", 5), ("random two", 6), ("random two least_conn", 9),
+    ("random two least_conn", 2), ("random", 1), ("random two", 1),
+    ("hash $host", 3), ("least_time header", 3), ("hash $arg_user", 1), ("least_conn", 2),
+]
+# servers marked `down` in config: (upstream index, server index)
+DOWN = {(0, 1), (3, 0), (6, 2), (9, 3), (13, 4), (15, 0), (4, 5), (4, 66)}
+DEFER_WEIGHT = len(UPSTREAMS)   # one more upstream with weight=2: deferred
+
+
+def _addr(u, j):
+    if u == 2:
+        return "unix:/var/run/nginx-502-server.sock"
+    if u == 7:
+        return "127.0.0.1:8181"
+    return f"10.{u}.{j // 250}.{j % 250 + 1}:{8080 + (j % 3)}"
+
+
+def conf_text() -> str:
+    L = []
+    names = []
+    for u, (m, k) in enumerate(UPSTREAMS):
+        name = f"default-peers-u{u:02d}-svc-80"
+        names.append(name)
+        L.append(f"upstream {name} {{")
+        if m:
+            L.append(f"\t{m};")
+        for j in range(k):
+            down = " down" if (u, j) in DOWN else ""
+            L.append(f"\tserver {_addr(u, j)} max_fails=1 fail_timeout=10s{down};")
+        L.append("\tkeepalive 32;")
+        L.append("}")
+    name = f"default-peers-u{DEFER_WEIGHT:02d}-svc-80"
+    names.append(name)
+    L.append(f"upstream {name} {{\n\tserver 10.99.0.1:80 weight=2;\n\tserver 10.99.0.2:80;\n}}")
+    for u, name in enumerate(names):
+        L.append(f"server {{\n\tlisten 80;\n\tserver_name u{u}.peers.example.com;\n"
+                 f"\tlocation / {{\n\t\tproxy_pass http://{name};\n\t}}\n"
+                 f"\tlocation /static/ {{\n\t\treturn 200;\n\t}}\n}}")
+    return "\n".join(L) + "\n"
+
+
+def peers_blob() -> bytes:
+    main = ("http {\n\tserver {\n\t\tlisten 80 default_server;\n\t\tserver_name _;\n"
+            "\t\tlocation / {\n\t\t\treturn 404;\n\t\t}\n\t}\n\tinclude /etc/nginx/conf.d/*.conf;\n}\n")
+    return blob.make_blob(main, {"default-peers": conf_text()})
+
+
+def _raddrs(rng, m):
+    out = []
+    for _ in range(m):
+        r = rng.random()
+        if r < 0.6:
+            out.append("%d.%d.%d.%d" % tuple(rng.integers(1, 255, 4)))
+        elif r < 0.85:
+            g = ["%x" % x for x in rng.integers(0, 65536, 8)]
+            z = int(rng.integers(0, 4))
+            out.append(":".join(g) if z == 0 else ":".join(g[:z]) + "::" + ":".join(g[z + 3:]))
+        elif r < 0.9:
+            out.append("::ffff:%d.%d.%d.%d" % tuple(rng.integers(1, 255, 4)))
+        elif r < 0.95:
+            out.append("unix:")
+        else:
+            out.append(["01.2.3.4", "1.2.3", "1:2::3::4", "::", "256.1.1.1", "fe80::1", ""][int(rng.integers(0, 7))])
+    return out
+
+
+def gen_requests(n: int, seed: int = records.SEED_BASE + 40, hot: tuple = ()):
+    """n requests over the peers config.  ``hot``: upstream indices that get most of the traffic
+    (long sequential runs for round robin / least_conn)."""
+    rng = np.random.default_rng(seed)
+    nu = len(UPSTREAMS) + 1
+    w = np.ones(nu)
+    for h in hot:
+        w[h] = 40.0 * nu
+    w /= w.sum()
+    ui = rng.choice(nu, size=n, p=w)
+    hosts = [f"u{u}.peers.example.com" for u in range(nu)]
+    uris = [f"/api/v{k}/item/{k * 7 % 13}" for k in range(40)] + ["/", "/static/x.css"]
+    args = [""] + [f"user={k}" for k in range(25)] + [f"a=1&user=u{k}&b=2" for k in range(10)]
+    ras = _raddrs(rng, 400)
+    hdr_pool = []
+    for k in range(60):
+        h = b""
+        if k % 3:
+            h += f"Cookie: theme=dark; session=s{k % 17}\r\n".encode()
+        if k % 4:
+            h += f"X-User: user-{k % 11}\r\n".encode()
+        if k % 7 == 0:
+            h += b"Cookie: session=second\r\n"
+        hdr_pool.append(h + b"Accept: */*\r\n")
+    fields = {
+        "uri": [records.choice_seg(uris, rng.integers(0, len(uris), n))],
+        "args": [records.choice_seg(args, rng.integers(0, len(args), n))],
+        "hdrs": [records.choice_seg(hdr_pool, rng.integers(0, len(hdr_pool), n))],
+        "host": [records.choice_seg(hosts, ui)],
+        "method": [records.const_seg("GET", n)],
+        "raddr": [records.choice_seg(ras, rng.integers(0, len(ras), n))],
+    }
+    rid = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+    return records.build(n, fields, np.full(n, 80), np.zeros(n, np.uint8), rid=rid,
+                         remote_port=rng.integers(1024, 65535, n))

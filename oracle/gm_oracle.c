@@ -43,6 +43,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <arpa/inet.h>
 
 #include "../include/gpumatch.h"
 
@@ -184,8 +185,21 @@ typedef struct { char *src; char *var; int np; part_t *p; } split_t;
 
 typedef struct { int kind; int nocase; int zones; uint8_t *lit; int len; pcre *re; pcre_extra *ex; } sig_t;
 
+/* an upstream block (version1/nginx.ingress.tmpl:2-8, version2/nginx.virtualserver.tmpl:2-10) */
+enum { OM_RR, OM_LEAST_CONN, OM_IP_HASH, OM_HASH, OM_CHASH, OM_RANDOM, OM_RANDOM2, OM_DEFER };
+typedef struct { uint32_t hash; int peer; } opoint_t;
+typedef struct {
+    char *name; dir_t *d;
+    int method; char *key;
+    int npeers; char **addr; int *down;
+    int first_peer;
+    opoint_t *ring; int nring;
+} oups_t;
+
 typedef struct orc_ctx {
     uint32_t gen;
+    oups_t *udef; int nudef;        /* upstream blocks in config order */
+    oups_t **uby; int total_peers;  /* per sorted upstream id (NULL: no block) */
     srv_t *srv; int nsrv;
     loc_t *loc; int nloc;
     map_t *map; int nmap;
@@ -317,6 +331,10 @@ static void walk_http(build_t *B, dir_t *h) {
         } else if (!strcmp(n, "upstream") && d->nargs == 2 && d->block) {
             c->ups = realloc(c->ups, sizeof(char *) * (c->nups + 1));
             c->ups[c->nups++] = strdup(d->args[1]);
+            c->udef = realloc(c->udef, sizeof(oups_t) * (c->nudef + 1));
+            memset(&c->udef[c->nudef], 0, sizeof(oups_t));
+            c->udef[c->nudef].name = strdup(d->args[1]); c->udef[c->nudef].d = d;
+            c->nudef++;
         } else if (!strcmp(n, "map") && d->nargs == 3 && d->block) {
             map_t m; memset(&m, 0, sizeof m);
             m.src = strdup(d->args[1]); m.var = strdup(d->args[2] + 1);
@@ -581,6 +599,134 @@ static void build_ac(orc_ctx *c) {
 }
 
 /* ------------------------------------------------------------------ public: create */
+/* ------------------------------------------------------------------ upstream balancers (§8 f3)
+ * nginx 1.17.3's ngx_http_upstream_round_robin / least_conn / ip_hash / hash / random modules,
+ * restated request by request (the engine's k_peer_* kernels batch the same algorithms).  What the
+ * engine does not model defers (GM_PEER_DEFER): server parameters beyond max_fails /
+ * fail_timeout / slow_start / down, Plus-only methods, hash keys with $host or variables outside
+ * the engine's set, a consistent-hash upstream naming one address twice, more than 1024 peers
+ * under round robin / least_conn. */
+static int is_var_ch(char ch);
+static uint32_t crc32_bytes(uint32_t c, const void *p, size_t n) {   /* bitwise CRC-32/IEEE, running */
+    const uint8_t *b = p;
+    for (size_t i = 0; i < n; i++) {
+        c ^= b[i];
+        for (int k = 0; k < 8; k++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1u)));
+    }
+    return c;
+}
+uint32_t orc_crc32(const void *p, size_t n) { return crc32_bytes(0xFFFFFFFFu, p, n) ^ 0xFFFFFFFFu; }
+
+static int cmp_point(const void *a, const void *b) {
+    const opoint_t *x = a, *y = b;
+    if (x->hash != y->hash) return x->hash < y->hash ? -1 : 1;
+    return x->peer - y->peer;
+}
+
+/* the engine's variable set for hash keys (gm_compile.cpp Compiler::src, minus $host) */
+static int key_var_ok(const char *nm, int n) {
+    static const char *vars[] = {"scheme", "https", "http2", "request_method", "args", "query_string", "uri",
+                                 "document_uri", "request_uri", "request", "request_body", "remote_addr",
+                                 "remote_port", "server_port", "request_id", NULL};
+    char b[128];
+    if (n <= 0 || n >= (int)sizeof b) return 0;
+    for (int i = 0; i < n; i++) b[i] = (char)lc((unsigned char)nm[i]);
+    b[n] = 0;
+    for (int i = 0; vars[i]; i++) if (!strcmp(b, vars[i])) return 1;
+    if ((!strncmp(b, "http_", 5) && n > 5) || (!strncmp(b, "cookie_", 7) && n > 7) || (!strncmp(b, "arg_", 4) && n > 4)) return 1;
+    return 0;
+}
+
+static void build_upstreams(orc_ctx *c) {
+    c->uby = calloc(c->nups ? c->nups : 1, sizeof(oups_t *));
+    c->total_peers = 0;
+    for (int u = 0; u < c->nups; u++) {
+        oups_t *U = NULL;
+        for (int k = 0; k < c->nudef && !U; k++) if (!strcmp(c->udef[k].name, c->ups[u])) U = &c->udef[k];
+        c->uby[u] = U;
+        if (!U) continue;
+        dir_t *d = U->d;
+        U->method = OM_RR;
+        int defer = 0;
+        for (int i = 0; i < d->nkids; i++) {
+            dir_t *k = &d->kids[i];
+            if (!k->nargs) continue;
+            const char *m = k->args[0];
+            if (!strcmp(m, "server") && k->nargs >= 2) {
+                U->addr = realloc(U->addr, sizeof(char *) * (U->npeers + 1));
+                U->down = realloc(U->down, sizeof(int) * (U->npeers + 1));
+                U->addr[U->npeers] = strdup(k->args[1]); U->down[U->npeers] = 0;
+                for (int q = 2; q < k->nargs; q++) {
+                    const char *a = k->args[q];
+                    if (!strcmp(a, "down")) U->down[U->npeers] = 1;
+                    else if (!strncmp(a, "max_fails=", 10) || !strncmp(a, "fail_timeout=", 13) ||
+                             !strncmp(a, "slow_start=", 11) || !strcmp(a, "weight=1") || !strcmp(a, "max_conns=0")) {}
+                    else defer = 1;
+                }
+                U->npeers++;
+            } else if (!strcmp(m, "least_conn") && k->nargs == 1) U->method = OM_LEAST_CONN;
+            else if (!strcmp(m, "ip_hash") && k->nargs == 1) U->method = OM_IP_HASH;
+            else if (!strcmp(m, "hash") && (k->nargs == 2 || (k->nargs == 3 && !strcmp(k->args[2], "consistent")))) {
+                U->method = k->nargs == 3 ? OM_CHASH : OM_HASH;
+                U->key = strdup(k->args[1]);
+            } else if (!strcmp(m, "random")) {
+                if (k->nargs == 1) U->method = OM_RANDOM;
+                else if (!strcmp(k->args[1], "two") && (k->nargs == 2 || (k->nargs == 3 && !strcmp(k->args[2], "least_conn"))))
+                    U->method = OM_RANDOM2;
+                else defer = 1;
+            } else if (!strcmp(m, "least_time") || !strcmp(m, "sticky") || !strcmp(m, "queue") ||
+                       !strcmp(m, "ntlm") || !strcmp(m, "hash")) defer = 1;
+        }
+        U->first_peer = c->total_peers;
+        c->total_peers += U->npeers;
+        if ((U->method == OM_RR || U->method == OM_LEAST_CONN) && U->npeers > 1024) defer = 1;
+        if (U->method == OM_HASH || U->method == OM_CHASH) {
+            for (const char *p = U->key; *p && !defer; p++) {
+                if (*p != '$') continue;
+                const char *st; int n;
+                p++;
+                if (*p == '{') { st = ++p; while (*p && *p != '}') p++; if (!*p) { defer = 1; break; } n = (int)(p - st); }
+                else { st = p; while (is_var_ch(*p)) p++; n = (int)(p - st); p--; }
+                if (!key_var_ok(st, n)) defer = 1;
+            }
+            if (U->method == OM_CHASH)
+                for (int a = 0; a < U->npeers; a++)
+                    for (int b = 0; b < a; b++) if (!strcmp(U->addr[a], U->addr[b])) defer = 1;
+        }
+        if (U->method == OM_CHASH && !defer) {
+            /* ngx_http_upstream_update_chash: 160 points per server */
+            U->ring = malloc(sizeof(opoint_t) * 160 * (U->npeers ? U->npeers : 1));
+            int np = 0;
+            for (int j = 0; j < U->npeers; j++) {
+                const char *sv = U->addr[j]; int sl = (int)strlen(sv);
+                const char *host = sv, *port = ""; int hl = sl, pl = 0;
+                if (sl >= 5 && !strncasecmp(sv, "unix:", 5)) { host = sv + 5; hl = sl - 5; }
+                else {
+                    for (int q = sl - 1; q >= 0; q--) {
+                        if (sv[q] == ':') { hl = q; port = sv + q + 1; pl = sl - q - 1; break; }
+                        if (sv[q] < '0' || sv[q] > '9') break;
+                    }
+                }
+                uint32_t base = crc32_bytes(0xFFFFFFFFu, host, hl);
+                base = crc32_bytes(base, "", 1);
+                base = crc32_bytes(base, port, pl);
+                uint32_t prev = 0;
+                for (int q = 0; q < 160; q++) {
+                    uint8_t pb[4] = {(uint8_t)prev, (uint8_t)(prev >> 8), (uint8_t)(prev >> 16), (uint8_t)(prev >> 24)};
+                    uint32_t h = crc32_bytes(base, pb, 4) ^ 0xFFFFFFFFu;
+                    U->ring[np].hash = h; U->ring[np].peer = j; np++;
+                    prev = h;
+                }
+            }
+            qsort(U->ring, np, sizeof(opoint_t), cmp_point);
+            int m = 0;
+            for (int q = 0; q < np; q++) if (q == 0 || U->ring[q].hash != U->ring[m - 1].hash) U->ring[m++] = U->ring[q];
+            U->nring = m;
+        }
+        if (defer) U->method = OM_DEFER;
+    }
+}
+
 orc_ctx *orc_create(const void *blob, size_t len, uint32_t gen) {
     const uint8_t *b = blob;
     if (len < 8) { seterr("short blob", NULL); return NULL; }
@@ -614,6 +760,7 @@ orc_ctx *orc_create(const void *blob, size_t len, uint32_t gen) {
     int u = 0;
     for (int i = 0; i < c->nups; i++) if (u == 0 || strcmp(c->ups[u - 1], c->ups[i])) c->ups[u++] = c->ups[i];
     c->nups = u;
+    build_upstreams(c);
     for (int i = 0; i < c->nloc; i++) {
         loc_t *L = &c->loc[i];
         if (!L->has_proxy) continue;
@@ -1567,4 +1714,176 @@ int64_t orc_parse_requests(const uint8_t *wire, const gm_wire_msg *msgs, uint32_
     }
     free(uri.p); free(hdrs.p); free(body.p);
     return rc < 0 ? -1 : (int64_t)o;
+}
+
+/* ------------------------------------------------------------------ peer selection (§8 f3) */
+static uint32_t orc_draw(const uint8_t rid[16], uint32_t j) {
+    uint64_t lo = 0, hi = 0;
+    for (int i = 7; i >= 0; i--) { lo = lo << 8 | rid[i]; hi = hi << 8 | rid[8 + i]; }
+    uint64_t x = lo ^ (hi * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)(j + 1) * 0xD1B54A32D192ED03ull);
+    x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27; x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    return (uint32_t)(x >> 32);
+}
+
+#define LIVE(j) (!(st[U->first_peer + (j)].flags & GM_PEER_DOWN))
+
+/* ngx_http_upstream_get_round_robin_peer (weights 1): single peer, else smooth WRR */
+static int orc_rr(oups_t *U, gm_peer_state *st) {
+    int n = U->npeers;
+    if (n == 1) return LIVE(0) ? 0 : -1;
+    int best = -1, total = 0;
+    for (int j = 0; j < n; j++) {
+        if (!LIVE(j)) continue;
+        gm_peer_state *e = &st[U->first_peer + j];
+        e->current_weight += 1; total += 1;
+        if (best < 0 || e->current_weight > st[U->first_peer + best].current_weight) best = j;
+    }
+    if (best < 0) return -1;
+    st[U->first_peer + best].current_weight -= total;
+    return best;
+}
+
+/* ngx_http_upstream_get_least_conn_peer (weights 1) */
+static int orc_lc(oups_t *U, gm_peer_state *st) {
+    int n = U->npeers, best = -1, many = 0;
+    for (int j = 0; j < n; j++) {
+        if (!LIVE(j)) continue;
+        if (best < 0 || st[U->first_peer + j].conns < st[U->first_peer + best].conns) { best = j; many = 0; }
+        else if (st[U->first_peer + j].conns == st[U->first_peer + best].conns) many = 1;
+    }
+    if (best < 0) return -1;
+    if (many) {
+        int b = best, total = 0;
+        for (int j = best; j < n; j++) {
+            if (!LIVE(j) || st[U->first_peer + j].conns != st[U->first_peer + b].conns) continue;
+            st[U->first_peer + j].current_weight += 1; total += 1;
+            if (st[U->first_peer + j].current_weight > st[U->first_peer + b].current_weight) b = j;
+        }
+        st[U->first_peer + b].current_weight -= total;
+        best = b;
+    }
+    return best;
+}
+
+/* -1: round robin, -2: defer; st conns are the batch-start snapshot for random two */
+static int orc_stateless(orc_ctx *c, oups_t *U, const gm_req *r, const uint8_t *arena, gm_peer_state *st,
+                         const uint32_t *snap_conns, scratch_t *sc) {
+    int n = U->npeers;
+    if (U->method == OM_RANDOM) {
+        for (uint32_t tries = 0;;) {
+            int x = (int)(orc_draw(r->rid, tries) % (uint32_t)n);
+            if (LIVE(x)) return x;
+            if (++tries > 20) return -1;
+        }
+    }
+    if (U->method == OM_RANDOM2) {
+        if (n < 2) return -1;
+        int first = -1; uint32_t tries = 0;
+        for (uint32_t j = 0;; j++) {
+            int x = (int)(orc_draw(r->rid, j) % (uint32_t)n);
+            if (LIVE(x) && x != first) {
+                if (first < 0) { first = x; continue; }
+                return snap_conns[U->first_peer + first] < snap_conns[U->first_peer + x] ? first : x;
+            }
+            if (++tries > 20) return -1;
+        }
+    }
+    if (n == 1) return -1;
+    rq_t q; rq_init(&q, r, arena);
+    if (U->method == OM_IP_HASH) {
+        uint8_t b[16] = {0}; int alen = 3;
+        char t[64];
+        if (q.raddr.n < (int)sizeof t) {
+            memcpy(t, q.raddr.p, q.raddr.n); t[q.raddr.n] = 0;
+            uint8_t a6[16];
+            if (inet_pton(AF_INET, t, b) == 1) alen = 3;
+            else if (inet_pton(AF_INET6, t, a6) == 1) { memcpy(b, a6, 16); alen = 16; }
+            else memset(b, 0, sizeof b);
+        }
+        uint32_t hash = 89;
+        for (uint32_t tries = 0;;) {
+            for (int i = 0; i < alen; i++) hash = (hash * 113 + b[i]) % 6271;
+            int w = (int)(hash % (uint32_t)n);
+            if (LIVE(w)) return w;
+            if (++tries > 20) return -1;
+        }
+    }
+    ev_t E = {c, &q, sc, 0, NULL, NULL};
+    sv key = eval_complex(&E, U->key);
+    if (key.n == 0) return -1;
+    if (U->method == OM_CHASH) {
+        uint32_t h = orc_crc32(key.p, key.n);
+        int lo = 0, hi = U->nring;   /* ngx_http_upstream_find_chash_point */
+        while (lo < hi) {
+            int k = (lo + hi) / 2;
+            if (h > U->ring[k].hash) lo = k + 1; else if (h < U->ring[k].hash) hi = k; else { lo = k; break; }
+        }
+        for (uint32_t tries = 0;; lo++) {
+            int j = U->ring[lo % U->nring].peer;
+            if (LIVE(j)) return j;
+            if (++tries > 20) return -1;
+        }
+    }
+    /* hash: ((crc32([REHASH] KEY) >> 16) & 0x7fff) + PREV_HASH */
+    uint32_t acc = 0;
+    for (uint32_t tries = 0, rehash = 0;;) {
+        uint32_t cr = 0xFFFFFFFFu;
+        if (rehash > 0) { char d[16]; int dn = snprintf(d, sizeof d, "%u", rehash); cr = crc32_bytes(cr, d, dn); }
+        cr = crc32_bytes(cr, key.p, key.n) ^ 0xFFFFFFFFu;
+        acc += (cr >> 16) & 0x7FFF;
+        rehash++;
+        int w = (int)(acc % (uint32_t)n);
+        if (LIVE(w)) return w;
+        if (++tries > 20) return -1;
+    }
+}
+
+/* Select peers for n verdicts in request order, updating st (gm_peer_state per peer: conns +=
+ * picks, current_weight).  Returns 0, or -1 if n_peers differs from the generation's. */
+int orc_select_peers(orc_ctx *c, const gm_req *reqs, const uint8_t *arena, const gm_verdict *v, uint32_t n,
+                     gm_peer_state *st, uint32_t n_peers, uint32_t *out) {
+    if ((int)n_peers != c->total_peers) return -1;
+    uint32_t *snap = malloc(sizeof(uint32_t) * (n_peers ? n_peers : 1));
+    for (uint32_t j = 0; j < n_peers; j++) snap[j] = st[j].conns;
+    uint32_t *picks = calloc(n_peers ? n_peers : 1, sizeof(uint32_t));
+    scratch_t sc = {NULL};
+    for (uint32_t i = 0; i < n; i++) {
+        out[i] = GM_NONE;
+        if (v[i].action != GM_ACT_PROXY || v[i].upstream_id == GM_NONE) continue;
+        if (v[i].gen != c->gen || (int)v[i].upstream_id >= c->nups) { out[i] = GM_PEER_DEFER; continue; }
+        oups_t *U = c->uby[v[i].upstream_id];
+        if (!U || U->method == OM_DEFER) { out[i] = GM_PEER_DEFER; continue; }
+        if (U->npeers == 0) continue;
+        int p;
+        if (U->method == OM_LEAST_CONN) {
+            p = orc_lc(U, st);
+            if (p >= 0) st[U->first_peer + p].conns++;   /* least_conn sees its own picks at once */
+        } else {
+            p = U->method == OM_RR ? -1 : orc_stateless(c, U, &reqs[i], arena, st, snap, &sc);
+            if (p == -2) { out[i] = GM_PEER_DEFER; continue; }
+            if (p == -1) p = orc_rr(U, st);
+            if (p >= 0) picks[U->first_peer + p]++;
+        }
+        sc_reset(&sc);
+        if (p >= 0) out[i] = (uint32_t)(U->first_peer + p);
+    }
+    for (uint32_t j = 0; j < n_peers; j++) st[j].conns += picks[j];
+    free(snap); free(picks); sc_reset(&sc); free(sc.head);
+    return 0;
+}
+
+int orc_n_peers(orc_ctx *c) { return c->total_peers; }
+
+/* the initial state of a generation (gm_peers_init) */
+int orc_peers_init(orc_ctx *c, gm_peer_state *st, uint32_t n_peers) {
+    if ((int)n_peers != c->total_peers) return -1;
+    memset(st, 0, sizeof(gm_peer_state) * n_peers);
+    for (int u = 0; u < c->nups; u++) {
+        oups_t *U = c->uby[u];
+        if (!U) continue;
+        for (int j = 0; j < U->npeers; j++) st[U->first_peer + j].flags = U->down[j] ? GM_PEER_DOWN : 0;
+    }
+    return 0;
 }

@@ -85,3 +85,45 @@ def parse_requests(wire: np.ndarray, msgs: np.ndarray):
     if tot < 0:
         raise RuntimeError("oracle parse: arena capacity")
     return reqs, arena[:tot]
+
+
+def crc32(b: bytes) -> int:
+    """nginx ngx_crc32 (the oracle's bitwise CRC-32/IEEE)."""
+    L = lib()
+    L.orc_crc32.restype = ctypes.c_uint32
+    L.orc_crc32.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+    return int(L.orc_crc32(b, len(b)))
+
+
+class Balancer:
+    """The oracle's upstream balancers (orc_select_peers): nginx's peer choice, request by request."""
+
+    def __init__(self, oracle: Oracle):
+        from gpumatch.engine import PEER_STATE_DTYPE
+        L = lib()
+        L.orc_n_peers.restype = ctypes.c_int
+        L.orc_n_peers.argtypes = [ctypes.c_void_p]
+        L.orc_peers_init.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+        L.orc_select_peers.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+        self.o = oracle
+        self.n_peers = int(L.orc_n_peers(oracle.h))
+        self.state = np.zeros(max(self.n_peers, 1), dtype=PEER_STATE_DTYPE)[:self.n_peers]
+        L.orc_peers_init(oracle.h, self.state.ctypes.data, self.n_peers)
+
+    def select(self, reqs: np.ndarray, arena: np.ndarray, verdicts: np.ndarray) -> np.ndarray:
+        n = len(reqs)
+        out = np.zeros(n, dtype=np.uint32)
+        reqs = np.ascontiguousarray(reqs)
+        arena = np.ascontiguousarray(arena) if len(arena) else np.zeros(16, np.uint8)
+        verdicts = np.ascontiguousarray(verdicts)
+        rc = lib().orc_select_peers(self.o.h, reqs.ctypes.data, arena.ctypes.data, verdicts.ctypes.data, n,
+                                    self.state.ctypes.data, self.n_peers, out.ctypes.data)
+        if rc != 0:
+            raise RuntimeError("oracle: peer count mismatch")
+        return out
+
+    def release(self, ids: np.ndarray):
+        for p in ids:
+            if p < self.n_peers:
+                self.state["conns"][p] -= 1
