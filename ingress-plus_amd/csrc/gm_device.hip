@@ -1776,7 +1776,9 @@ extern "C" int gm_select_peers(gm_ctx *c, const gm_batch *in, const gm_verdict *
     HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, ks, vals, vs, (int)n, 0, bits, s));
     if ((e = grow(c, s, S->d_ptemp, S->cap_ptemp, tb))) return e;
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8));
-    k_peer_pick<<<blocks, 256, 0, s>>>(in->reqs, in->arena, verdicts, n, t, state, peer_out, keys, vals);
+    // one lane per request, no grid-stride loop: every request's dependent loads (verdict ->
+    // record -> draws -> peer state) in flight at once
+    k_peer_pick<<<(n + 255) / 256, 256, 0, s>>>(in->reqs, in->arena, verdicts, n, t, state, peer_out, keys, vals);
     HIPCHK(c, hipGetLastError());
     if (t.n_ups) {
         HIPCHK(c, hipcub::DeviceRadixSort::SortPairs(S->d_ptemp, tb, keys, ks, vals, vs, (int)n, 0, bits, s));
@@ -1789,7 +1791,9 @@ extern "C" int gm_select_peers(gm_ctx *c, const gm_batch *in, const gm_verdict *
         HIPCHK(c, hipGetLastError());
     }
     if (t.n_peers) {
-        k_peer_count<<<blocks, 256, 0, s>>>(peer_out, n, state, t.n_peers, 1);
+        // histogram blocks: enough to stream the picks, few enough that the flush stays small
+        k_peer_count<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 4095) / 4096, (uint32_t)c->cu_count * 2)), 256, 0, s>>>(
+            peer_out, n, state, t.n_peers, 1);
         HIPCHK(c, hipGetLastError());
     }
     return GM_OK;
@@ -1806,8 +1810,8 @@ extern "C" int gm_release_peers(gm_ctx *c, const uint32_t *peer_ids, uint32_t n,
     if (n_peers != g->tab.n_peers) return fail(c, GM_E_INVAL, "n_peers differs from the generation's peer count");
     if (n == 0 || n_peers == 0) return GM_OK;
     if (!peer_ids || !state) return fail(c, GM_E_INVAL, "null argument");
-    const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8));
-    k_peer_count<<<blocks, 256, 0, (hipStream_t)stream>>>(peer_ids, n, state, n_peers, -1);
+    k_peer_count<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 4095) / 4096, (uint32_t)c->cu_count * 2)), 256, 0,
+                   (hipStream_t)stream>>>(peer_ids, n, state, n_peers, -1);
     HIPCHK(c, hipGetLastError());
     return GM_OK;
 }

@@ -58,6 +58,7 @@ EXPORTS = ["gm_create", "gm_destroy", "gm_abi_version", "gm_load_generation", "g
 PEER_STATE_DTYPE = np.dtype([("conns", "<u4"), ("current_weight", "<i4"), ("flags", "<u4"), ("reserved", "<u4")])
 GM_PEER_DOWN = 0x1
 GM_PEER_DEFER = 0xFFFFFFFE
+GM_NONE = 0xFFFFFFFF
 
 _lib = None
 

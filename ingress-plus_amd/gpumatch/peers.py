@@ -37,10 +37,12 @@ def _addr(u, j):
     return f"10.{u}.{j // 250}.{j % 250 + 1}:{8080 + (j % 3)}"
 
 
-def conf_text() -> str:
+def conf_text(method: str | None = None) -> str:
+    """``method``: one LBMethod for every upstream (e.g. the default "random two least_conn")."""
     L = []
     names = []
     for u, (m, k) in enumerate(UPSTREAMS):
+        m = m if method is None else method
         name = f"default-peers-u{u:02d}-svc-80"
         names.append(name)
         L.append(f"upstream {name} {{")
@@ -61,10 +63,10 @@ def conf_text() -> str:
     return "\n".join(L) + "\n"
 
 
-def peers_blob() -> bytes:
+def peers_blob(method: str | None = None) -> bytes:
     main = ("http {\n\tserver {\n\t\tlisten 80 default_server;\n\t\tserver_name _;\n"
             "\t\tlocation / {\n\t\t\treturn 404;\n\t\t}\n\t}\n\tinclude /etc/nginx/conf.d/*.conf;\n}\n")
-    return blob.make_blob(main, {"default-peers": conf_text()})
+    return blob.make_blob(main, {"default-peers": conf_text(method)})
 
 
 def _raddrs(rng, m):
