@@ -182,8 +182,21 @@ typedef struct gm_stats_t {
     uint32_t last_ctx_pass, last_jobs;
     uint32_t n_peers;             /* upstream `server` peers: gm_peer_state entries     */
     uint32_t n_upstreams_deferred;/* upstreams whose balancing the engine leaves to nginx */
-    uint32_t reserved1;
+    uint32_t decoders;            /* request parsers the signature set runs (GM_DEC_*)  */
 } gm_stats_t;
+
+/* Request parsers (Wallarm's) a signature set can declare ("@decoders" line of
+ * the GM_ENTRY_SIGS text); wallarm_parser_disable <name> (annotations.go:320-329,
+ * nginx.ingress.tmpl:26,111) turns one off for a server or location.  Their decoded views of
+ * $args and the body are scanned by the same WAF stages (hits count for the request):
+ *   percent   %XX -> byte in $args (and a form body)
+ *   urlenc    '+' -> ' ' in $args and an application/x-www-form-urlencoded body
+ *   json_doc  JSON string escapes (\" \\ \/ \b \f \n \r \t \uXXXX -> UTF-8) of a "json" body
+ *   base64    every run of >= 16 base64 characters in $args / the body, decoded */
+#define GM_DEC_PERCENT 0x1u
+#define GM_DEC_URLENC  0x2u
+#define GM_DEC_JSON    0x4u
+#define GM_DEC_BASE64  0x8u
 
 typedef struct gm_ctx gm_ctx;
 
@@ -268,6 +281,20 @@ typedef struct gm_wire_msg {
 int         gm_parse_requests(gm_ctx *ctx, const uint8_t *wire, const gm_wire_msg *msgs, uint32_t n,
                               gm_req *reqs, uint8_t *arena, uint64_t arena_cap, uint64_t *arena_len_dev,
                               void *stream);
+
+/* ---------------------------------------------------------------- upstream request URI
+ * (nginx.org/rewrites.)  The URI a proxied request is sent upstream with, as
+ * ngx_http_proxy_create_request builds it: a location whose proxy_pass has a URI part (the
+ * template's {{$location.Rewrite}}, version1/nginx.ingress.tmpl:194-196, from nginx.org/rewrites
+ * "serviceName=<svc> rewrite=<uri>", annotations.go:347-361,526-544) sends <uri> + the rest of
+ * $uri after the location's prefix (%-escaped when the request's path held a '%' the parser saw
+ * before any "/.", "//", '?' or '#') + "?" $args; any other proxying location sends $request_uri
+ * unchanged.  out_len[i] = the length at out[out_off[i]]; GM_NONE for a verdict that is not a
+ * proxy (or past out_cap: gm_sync then reports GM_E_OVERFLOW), GM_PEER_DEFER for a proxy_pass
+ * with variables or of an older generation.  out_cap >= sum over requests of (longest URI part +
+ * 3 * uri_len + args_len + ruri_len + 1) always suffices.  Device pointers, asynchronous. */
+int         gm_upstream_uris(gm_ctx *ctx, const gm_batch *in, const gm_verdict *verdicts, uint8_t *out,
+                             uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, void *stream);
 
 /* ---------------------------------------------------------------- upstream peer selection
  * (the step after the path.)  The upstream blocks the templates render

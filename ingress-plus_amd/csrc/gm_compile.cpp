@@ -123,18 +123,32 @@ bool parse_body(Tokenizer &T, std::vector<Dir> &out, bool nested) {
 
 // ============================================================================ IR
 enum LocKind { PFX, EXACT, NOREGEX, RX, RXI, NAMED };
+// Wallarm parser names (wallarm_parser_disable, annotations.go:320-329) -> DEC_* bits
+uint32_t decoder_bit(const std::string &name) {
+    if (name == "percent") return DEC_PERCENT;
+    if (name == "urlenc") return DEC_URLENC;
+    if (name == "json_doc" || name == "json") return DEC_JSON;
+    if (name == "base64") return DEC_BASE64;
+    return 0;
+}
+
 struct Loc {
     int id = 0, server = 0;
     LocKind kind = PFX;
     std::string path;
     bool has_proxy = false, has_return = false, nested = false;
     std::string ups, err418;
+    std::string pass_uri;        // the URI part of proxy_pass (nginx.org/rewrites), "" none
+    uint32_t parser_off = 0;     // wallarm_parser_disable in the location (DEC_* bits)
+    bool has_pd = false;
+    bool pass_vars = false, grpc = false;
     int code = 0;
     int waf = -1;
 };
 struct SIf { std::string var; int op = 0; std::string val; int code = 0; bool ret_only = false; };
 struct Server {
     int id = 0, waf = GM_WAF_OFF;
+    uint32_t parser_off = 0;     // server-level wallarm_parser_disable (DEC_* bits)
     std::vector<std::pair<int, int>> listens;   // port, flags (1 ssl, 2 default)
     std::vector<std::string> names;
     std::vector<SIf> ifs;
@@ -207,6 +221,9 @@ struct Builder {
                 u = p == std::string::npos ? u : u.substr(p + 3);
                 size_t e = u.find_first_of("/$");
                 L.ups = u.substr(0, e); L.has_proxy = true;
+                L.pass_vars = u.find('$') != std::string::npos;
+                L.pass_uri = e != std::string::npos && u[e] == '/' ? u.substr(e) : std::string();
+                L.grpc = n == "grpc_pass";
             } else if (n == "return" && k.a.size() >= 2) {
                 L.has_return = true;
                 L.code = isdigit((unsigned char)k.a[1][0]) ? atoi(k.a[1].c_str()) : 302;
@@ -214,6 +231,8 @@ struct Builder {
                 L.err418 = k.a[3];
             } else if (n == "wallarm_mode" && k.a.size() == 2) {
                 L.waf = waf_mode(k.a[1]);
+            } else if (n == "wallarm_parser_disable" && k.a.size() == 2) {
+                L.parser_off |= decoder_bit(k.a[1]); L.has_pd = true;
             } else if (n == "location" || n == "if" || n == "rewrite") {
                 L.nested = true;
             }
@@ -227,8 +246,10 @@ struct Builder {
         Server S;
         S.id = (int)M.servers.size();
         S.waf = M.http_waf;
-        for (const Dir &k : d.body)
+        for (const Dir &k : d.body) {
             if (k.a.size() == 2 && k.a[0] == "wallarm_mode") S.waf = waf_mode(k.a[1]);
+            if (k.a.size() == 2 && k.a[0] == "wallarm_parser_disable") S.parser_off |= decoder_bit(k.a[1]);
+        }
         for (const Dir &k : d.body) {
             if (k.a.empty()) continue;
             const std::string &n = k.a[0];
@@ -701,7 +722,13 @@ struct Compiler {
 // ============================================================================ signatures
 struct SigRule { bool lit; bool nocase; int zones; std::string pat; };
 
-bool parse_sigs(const char *t, size_t n, std::vector<SigRule> &out) {
+static int hexv(char c) {
+    return c >= '0' && c <= '9' ? c - '0' : (c | 0x20) >= 'a' && (c | 0x20) <= 'f' ? (c | 0x20) - 'a' + 10 : -1;
+}
+
+// One rule per line: "lit|re <i|-> <zones> <hex literal | regex>"; "@decoders a,b,..." names the
+// request parsers whose decoded views the set's rules are written against (DEC_*).
+bool parse_sigs(const char *t, size_t n, std::vector<SigRule> &out, uint32_t &decoders) {
     size_t i = 0;
     while (i < n) {
         size_t e = i;
@@ -712,6 +739,20 @@ bool parse_sigs(const char *t, size_t n, std::vector<SigRule> &out) {
         size_t s = line.find_first_not_of(" \t");
         if (s == std::string::npos || line[s] == '#') continue;
         line = line.substr(s);
+        if (line.rfind("@decoders", 0) == 0) {
+            std::string v = line.substr(9);
+            size_t a = 0;
+            while (a < v.size()) {
+                size_t b = v.find(',', a);
+                if (b == std::string::npos) b = v.size();
+                std::string nm = v.substr(a, b - a);
+                nm.erase(0, nm.find_first_not_of(" \t"));
+                nm.erase(nm.find_last_not_of(" \t") + 1);
+                decoders |= decoder_bit(nm);
+                a = b + 1;
+            }
+            continue;
+        }
         std::string f[3];
         size_t p = 0;
         for (int k = 0; k < 3; k++) {
@@ -730,7 +771,11 @@ bool parse_sigs(const char *t, size_t n, std::vector<SigRule> &out) {
         std::string pat = line.substr(p);
         if (r.lit) {
             if (pat.size() % 2) return false;
-            for (size_t k = 0; k < pat.size(); k += 2) r.pat.push_back((char)std::stoi(pat.substr(k, 2), nullptr, 16));
+            for (size_t k = 0; k < pat.size(); k += 2) {
+                const int hi = hexv(pat[k]), lo = hexv(pat[k + 1]);
+                if (hi < 0 || lo < 0) return false;
+                r.pat.push_back((char)(hi * 16 + lo));
+            }
         } else r.pat = pat;
         out.push_back(r);
     }
@@ -1056,6 +1101,11 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         else confd.push_back(std::move(body));
     }
 
+    std::vector<SigRule> sig;
+    uint32_t decoders = 0;
+    if (sig_text && !parse_sigs(sig_text, sig_len, sig, decoders)) { R.code = GM_E_PARSE; R.err = "signature set parse error"; return R; }
+    st.decoders = decoders;
+
     Model M;
     Builder B(M, confd);
     if (have_main) {
@@ -1259,6 +1309,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
 
     // ---- locations, tries, regex locations, server ifs
     std::vector<DLoc> dlocs(M.locs.size());
+    std::vector<DLocUri> dluri(M.locs.size());
     std::vector<DNode> nodes;
     std::vector<std::pair<uint32_t, uint32_t>> edge_list;   // key, child
     std::map<std::pair<uint32_t, uint8_t>, uint32_t> edge_map;
@@ -1329,6 +1380,9 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             Loc &L = M.locs[lid];
             DLoc &dl = dlocs[lid];
             dl.waf_mode = (uint8_t)(L.waf >= 0 ? L.waf : S.waf);
+            // the request parsers this location runs: the signature set's, minus
+            // wallarm_parser_disable (a location's own list replaces the server's, nginx's array merge)
+            dluri[lid].flags |= (decoders & ~(L.has_pd ? L.parser_off : S.parser_off)) << LOCURI_DEC_SHIFT;
             dl.upstream = GM_NONE;
             dl.noregex = L.kind == NOREGEX;
             dl.is_named = L.kind == NAMED;
@@ -1350,6 +1404,19 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 dl.kind = LK_PROXY;
                 auto it = std::lower_bound(ups.begin(), ups.end(), L.ups);
                 if (it != ups.end() && *it == L.ups) dl.upstream = (uint32_t)(it - ups.begin());
+                // the upstream request URI (ngx_http_proxy_create_request): a URI part replaces
+                // the matched location prefix of $uri; variables, a URI part under a regex / named
+                // location (a config error in nginx) or on grpc_pass are left to nginx
+                DLocUri &du = dluri[lid];
+                du.flags &= ~(LOCURI_REWRITE | LOCURI_DEFER);
+                if (L.pass_vars || (!L.pass_uri.empty() && (L.grpc || L.kind == RX || L.kind == RXI || L.kind == NAMED)))
+                    du.flags |= LOCURI_DEFER;
+                else if (!L.pass_uri.empty()) {
+                    du.flags |= LOCURI_REWRITE;
+                    du.off = C.put_bytes(L.pass_uri);
+                    du.len = (uint32_t)L.pass_uri.size();
+                    du.loc_len = (uint32_t)L.path.size();
+                }
             } else dl.kind = LK_NONE;
 
             if (L.kind == PFX || L.kind == NOREGEX || L.kind == EXACT) {
@@ -1472,9 +1539,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         rk_ents.insert(rk_ents.end(), kv.second.begin(), kv.second.end());   // ascending k: pushed in k order
     }
 
-    // ---- signatures
-    std::vector<SigRule> sig;
-    if (sig_text && !parse_sigs(sig_text, sig_len, sig)) { R.code = GM_E_PARSE; R.err = "signature set parse error"; return R; }
+    // ---- signatures (parsed up front: the set's decoders shape the location tables)
+
     struct LitE { uint32_t key; DLit lit; std::string bytes; };
     std::vector<LitE> lits;
     std::vector<DSigRegex> sregex;
@@ -1626,6 +1692,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.n_key_parts = (uint32_t)key_parts.size(); h.n_points = (uint32_t)points.size();
     h.off_ups = I.put(dups); h.off_key_parts = I.put(key_parts); h.off_points = I.put(points);
     h.off_peer_init = I.put(peer_init);
+    h.off_loc_uri = I.put(dluri);
+    h.decoders = decoders;
     C.bytes.resize(C.bytes.size() + 64, 0);   // slack: vector compares may over-read
     h.off_bytes = I.put(C.bytes);
     I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
@@ -1684,6 +1752,8 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.points = (const DPoint *)(b + h.off_points);
     t.peer_init = (const uint32_t *)(b + h.off_peer_init);
     t.n_ups = h.n_ups; t.n_peers = h.n_peers;
+    t.loc_uri = (const DLocUri *)(b + h.off_loc_uri);
+    t.decoders = h.decoders;
     t.n_ports = h.n_ports;
     t.names_mask = h.n_names_cap - 1; t.wild_head_mask = h.n_wild_head_cap - 1; t.wild_tail_mask = h.n_wild_tail_cap - 1;
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;

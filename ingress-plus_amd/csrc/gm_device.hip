@@ -955,6 +955,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
 }
 
 #include "gm_waf.inc"
+#include "gm_decode.inc"
 
 }  // namespace
 
@@ -1007,11 +1008,20 @@ struct Scratch {
     uint4 *d_pprog = nullptr; size_t cap_pprog = 0;
     uint32_t *d_ppat = nullptr; size_t cap_ppat = 0;
     uint8_t *d_ptemp = nullptr; size_t cap_ptemp = 0;
+    uint64_t *d_usize = nullptr; size_t cap_usize = 0;   // upstream URIs: sizes
+    gm_req *d_sreqs = nullptr; size_t cap_sreqs = 0;     // decoded views: shadow records, arena,
+    uint8_t *d_sarena = nullptr; size_t cap_sarena = 0;  // block map, sizes / bases, scan temp
+    uint32_t *d_sblk = nullptr; size_t cap_sblk = 0;
+    uint64_t *d_ssize = nullptr, *d_sbase = nullptr; size_t cap_ssize = 0, cap_sbase = 0;
+    uint8_t *d_stemp = nullptr; size_t cap_stemp = 0;
+    uint8_t *d_utemp = nullptr; size_t cap_utemp = 0;
     ~Scratch() {
         for (void *p : {(void *)d_status, (void *)d_blk2rec, (void *)d_cand, (void *)d_surv, (void *)d_pairs,
                         (void *)d_jobs, (void *)d_set, (void *)d_cnt, (void *)d_start, (void *)d_ccnt,
                         (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp,
-                        (void *)d_pk, (void *)d_pseg, (void *)d_pprog, (void *)d_ppat, (void *)d_ptemp})
+                        (void *)d_pk, (void *)d_pseg, (void *)d_pprog, (void *)d_ppat, (void *)d_ptemp,
+                        (void *)d_usize, (void *)d_utemp, (void *)d_sreqs, (void *)d_sarena, (void *)d_sblk,
+                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
         for (auto &e : ev) if (e) (void)hipEventDestroy(e);
@@ -1239,13 +1249,15 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         S->epoch = 0;
         HIPCHK(c, hipMemsetAsync(S->d_set, 0, S->cap_set * 8, s));
     }
-    if (++S->epoch > 255) {   // epoch wrap: every slot becomes free again
+    // one epoch per batch (two with decoders: the decoded pass's jobs take epoch + 1)
+    S->epoch += t.decoders ? 2 : 1;
+    if (S->epoch + (t.decoders ? 1 : 0) > 255) {   // epoch wrap: every slot becomes free again
         S->epoch = 1;
         HIPCHK(c, hipMemsetAsync(S->d_set, 0, S->cap_set * 8, s));
     }
     const uint32_t wcap = (uint32_t)std::min<size_t>(S->cap_cand / 4 / W, 0xFFFFFFFFu);   // records per wave
     u32x4 *cand = reinterpret_cast<u32x4 *>(S->d_cand);
-    Dedup dd{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, out, S->d_cnt, S->d_status};
+    Dedup dd{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, out, S->d_cnt, S->d_status};
 
     // ---- fork: k_route on the side stream, beside the WAF scan (independent inputs; its waves
     // fit beside the scan's one workgroup per CU; issued after the scan so the scan claims the
@@ -1304,8 +1316,56 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         HIPCHK(c, hipGetLastError());
     }
     if (t.n_always) {
-        k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(A, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd);
+        k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(A, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, false);
         HIPCHK(c, hipGetLastError());
+    }
+    if (t.decoders) {
+        // ---- the request parsers' decoded views (gm_decode.inc): shadow records, same indices,
+        // then the WAF stages once more over them; hits land in the same dedupe set and counts
+        const size_t scap = 2 * (size_t)alen + 32 * (size_t)n + 4096;   // a view <= 2x its zones
+        const uint32_t snblk = (uint32_t)((scap >> BLK_SHIFT) + 1);
+        if ((e = grow(c, s, S->d_sreqs, S->cap_sreqs, (size_t)n))) return e;
+        if ((e = grow(c, s, S->d_sarena, S->cap_sarena, scap))) return e;
+        if ((e = grow(c, s, S->d_sblk, S->cap_sblk, snblk))) return e;
+        if ((e = grow(c, s, S->d_ssize, S->cap_ssize, (size_t)n + 2))) return e;
+        if ((e = grow(c, s, S->d_sbase, S->cap_sbase, (size_t)n + 2))) return e;
+        size_t dtmp = 0;
+        HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, dtmp, S->d_ssize, S->d_sbase, (int)n + 1, s));
+        if ((e = grow(c, s, S->d_stemp, S->cap_stemp, dtmp))) return e;
+        const uint32_t dblocks = (n + 255) / 256;
+        k_dec_size<<<dblocks, 256, 0, s>>>(reqs, A, n, t, out, S->d_ssize);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_stemp, dtmp, S->d_ssize, S->d_sbase, (int)n + 1, s));
+        uint64_t *slen = S->d_sbase + n + 1;   // the shadow arena's length, on the device
+        k_dec_emit<<<dblocks, 256, 0, s>>>(reqs, A, n, t, out, S->d_sbase, S->d_sreqs, S->d_sarena, scap,
+                                           S->d_sblk, snblk, slen, S->d_status);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemsetAsync(S->d_status + 2, 0, 4, s));   // the job list restarts (pairs continue)
+        Dedup dd2 = dd;
+        dd2.jepoch = S->epoch + 1;
+        const uint8_t *SA = S->d_sarena;
+        const gm_req *SR = S->d_sreqs;
+        if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen);
+        else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen);
+        else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen);
+        else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen);
+        HIPCHK(c, hipGetLastError());
+        k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, S->d_ccnt, W, t, S->d_surv, bcap, S->d_ccnt + W,
+                                                    S->d_status);
+        HIPCHK(c, hipGetLastError());
+        k_waf_exact<<<scan_blocks * EXACT_SUB, 256, 0, s>>>(SA, scap, SR, n, S->d_sblk, t, S->d_surv, bcap,
+                                                             S->d_ccnt + W, EXACT_SUB, S->d_pairs, (uint32_t)S->cap_pairs,
+                                                             S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, dd2, slen);
+        HIPCHK(c, hipGetLastError());
+        if (t.n_sig_regex) {
+            k_waf_regex<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(SA, SR, t, S->d_jobs, (uint32_t)S->cap_jobs, S->d_pairs,
+                                                                   (uint32_t)S->cap_pairs, dd2);
+            HIPCHK(c, hipGetLastError());
+        }
+        if (t.n_always) {
+            k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(SA, SR, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd2, true);
+            HIPCHK(c, hipGetLastError());
+        }
     }
     // ---- hit emission: offsets by an exclusive scan of the per-request counts (request order)
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_temp, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
@@ -1386,6 +1446,7 @@ int gm_sync(gm_ctx *c, void *stream) {
     }
     const uint32_t ov = S->h_status[3];
     if (S->h_status[PARSE_STATUS_WORD + 3]) return fail(c, GM_E_OVERFLOW, "gm_parse_requests: arena capacity exceeded");
+    if (S->h_status[UPURI_STATUS_WORD]) return fail(c, GM_E_OVERFLOW, "gm_upstream_uris: output capacity exceeded");
     if (ov & 2u) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded");
     if (ov) return fail(c, GM_E_OVERFLOW, "WAF candidate / survivor / pair / job capacity exceeded");
     return GM_OK;
@@ -1669,6 +1730,7 @@ __global__ __launch_bounds__(256) void k_uri_normalize(const uint8_t *A, const u
 
 #include "gm_wire.inc"
 #include "gm_peers.inc"
+#include "gm_upuri.inc"
 }  // namespace
 
 extern "C" int gm_normalize_uris(gm_ctx *c, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
@@ -1700,7 +1762,7 @@ extern "C" int gm_parse_requests(gm_ctx *c, const uint8_t *wire, const gm_wire_m
     hipStream_t s = (hipStream_t)stream;
     Scratch *S = scratch_for(c, s);
     if (!S) return fail(c, GM_E_NOMEM, t_err);
-    HIPCHK(c, hipMemsetAsync(S->d_status + PARSE_STATUS_WORD, 0, (STATUS_WORDS - PARSE_STATUS_WORD) * 4, s));
+    HIPCHK(c, hipMemsetAsync(S->d_status + PARSE_STATUS_WORD, 0, (UPURI_STATUS_WORD - PARSE_STATUS_WORD) * 4, s));
     if (n == 0) { HIPCHK(c, hipMemsetAsync(arena_len_dev, 0, 8, s)); return GM_OK; }
     size_t tmp = 0;
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, S->d_wsize, S->d_wbase, (int)n + 1, s));
@@ -1830,4 +1892,38 @@ extern "C" int gm_peer_address(gm_ctx *c, uint32_t peer, char *buf, size_t cap, 
     }
     if (upstream_id) *upstream_id = g->peer_ups[peer];
     return (int)a.size();
+}
+
+// ---------------------------------------------------------------- upstream request URIs (§8 f1)
+extern "C" int gm_upstream_uris(gm_ctx *c, const gm_batch *in, const gm_verdict *verdicts, uint8_t *out,
+                                uint64_t out_cap, uint64_t *out_off, uint32_t *out_len, void *stream) {
+    if (!c || !in) return fail(c, GM_E_INVAL, "null argument");
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
+    if (in->flags & GM_BATCH_HOST) return fail(c, GM_E_INVAL, "gm_upstream_uris takes device buffers");
+    const uint32_t n = in->n;
+    if (n && (!verdicts || !out_off || !out_len || !in->reqs || !in->arena || (!out && out_cap)))
+        return fail(c, GM_E_INVAL, "null argument");
+    if (((uintptr_t)verdicts & 15) || ((uintptr_t)in->reqs & 15)) return fail(c, GM_E_INVAL, "verdicts / reqs must be 16-byte aligned");
+    HIPCHK(c, hipSetDevice(c->dev));
+    hipStream_t s = (hipStream_t)stream;
+    Scratch *S = scratch_for(c, s);
+    if (!S) return fail(c, GM_E_NOMEM, t_err);
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    const Generation *g = c->gen;
+    if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
+    HIPCHK(c, hipMemsetAsync(S->d_status + UPURI_STATUS_WORD, 0, 4, s));
+    if (n == 0) return GM_OK;
+    int e;
+    if ((e = grow(c, s, S->d_usize, S->cap_usize, (size_t)n))) return e;
+    size_t tb = 0;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tb, S->d_usize, out_off, (int)n, s));
+    if ((e = grow(c, s, S->d_utemp, S->cap_utemp, tb))) return e;
+    const uint32_t blocks = (n + 255) / 256;
+    k_upuri_size<<<blocks, 256, 0, s>>>(in->reqs, in->arena, verdicts, n, g->tab, S->d_usize);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_utemp, tb, S->d_usize, out_off, (int)n, s));
+    k_upuri_emit<<<blocks, 256, 0, s>>>(in->reqs, in->arena, verdicts, n, g->tab, out_off, out, out_cap, out_len,
+                                        S->d_status + UPURI_STATUS_WORD);
+    HIPCHK(c, hipGetLastError());
+    return GM_OK;
 }

@@ -107,6 +107,19 @@ struct DLoc {
     uint32_t route;          // DSplit / DRules index for IRLs
 };
 
+// The upstream request URI of a proxying location (§8 f1, nginx.org/rewrites: the URI part of
+// proxy_pass, annotations.go:347-361, version1/nginx.ingress.tmpl:194-196), indexed like DLoc.
+enum : uint32_t { LOCURI_REWRITE = 1, LOCURI_DEFER = 2 };
+// flags bits 8..11: the request parsers (Wallarm's, §8 f4) the location runs before the WAF
+// stages -- the signature set's "@decoders" minus wallarm_parser_disable
+constexpr uint32_t LOCURI_DEC_SHIFT = 8;
+enum : uint32_t { DEC_PERCENT = 1, DEC_URLENC = 2, DEC_JSON = 4, DEC_BASE64 = 8 };
+struct DLocUri {
+    uint32_t off, len;       // the URI part (bytes pool)
+    uint32_t loc_len;        // the location's prefix length: $uri[loc_len:] follows the URI part
+    uint32_t flags;          // 0: the request's own $request_uri goes upstream unchanged
+};
+
 // ---- request variables ---------------------------------------------------------------
 enum : uint8_t { SRC_HTTP = 1, SRC_COOKIE = 2, SRC_ARG = 3, SRC_VAR = 4 };
 enum : uint8_t { V_SCHEME = 1, V_HTTPS, V_HTTP2, V_METHOD, V_ARGS, V_URI, V_REQUEST_URI, V_REQUEST,
@@ -263,6 +276,8 @@ struct TabHeader {
     uint64_t off_hot_end;          // [off_ports, off_hot_end): the route's hot tables, contiguous
     uint32_t n_ups, n_peers, n_key_parts, n_points;
     uint64_t off_ups, off_key_parts, off_points, off_peer_init;   // peer_init: u32 GM_PEER_DOWN per peer
+    uint64_t off_loc_uri;          // DLocUri per location
+    uint32_t decoders, pad_dec;    // the signature set's request parsers (DEC_*)
 };
 // The route's hot tables -- ports, the three name tables, servers, server ifs, small-location
 // lists, locations and the name strings -- are laid out first and contiguously in the image;
@@ -285,6 +300,8 @@ struct GTab {                // device pointers, built on host from the image ba
     const uint8_t *hot_base; uint32_t hot_len;   // the hot prefix (hot_len 0: larger than ROUTE_STAGE_BYTES)
     const DUpstream *ups; const DKeyPart *key_parts; const DPoint *points; const uint32_t *peer_init;
     uint32_t n_ups, n_peers;
+    const DLocUri *loc_uri;
+    uint32_t decoders;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
     uint32_t gen;

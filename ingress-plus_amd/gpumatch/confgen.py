@@ -227,11 +227,41 @@ def _create_upstream(ing_ex, name, backend, p):
     return ups
 
 
-def _create_location(path, upstream, p):
-    """ingress.go:233-252."""
+def parse_rewrites(service: str):
+    """annotations.go:526-544 parseRewrites: "serviceName=<svc> rewrite=<path>" -> (svc, path);
+    ValueError on any other shape (strings.TrimSpace, SplitN(" ", 2), Split("="))."""
+    parts = service.strip(" \t\n\r\v\f").split(" ", 1)
+    if len(parts) != 2:
+        raise ValueError(f"Invalid rewrite format: {service}")
+    svc = parts[0].split("=")
+    if len(svc) != 2:
+        raise ValueError(f"Invalid rewrite format: {svc}")
+    rw = parts[1].split("=")
+    if len(rw) != 2:
+        raise ValueError(f"Invalid rewrite format: {rw}")
+    return svc[1], rw[1]
+
+
+def get_rewrites(ing: dict) -> dict:
+    """annotations.go:347-361 getRewrites: nginx.org/rewrites, ';'-separated; invalid entries are
+    logged and skipped."""
+    ann = (ing.get("metadata") or {}).get("annotations") or {}
+    out = {}
+    if "nginx.org/rewrites" in ann:
+        for svc in str(ann["nginx.org/rewrites"]).split(";"):
+            try:
+                name, rw = parse_rewrites(svc)
+            except ValueError:
+                continue
+            out[name] = rw
+    return out
+
+
+def _create_location(path, upstream, p, rewrite=""):
+    """ingress.go:233-252 (Rewrite: the URI part of proxy_pass, version1/nginx.ingress.tmpl:194-196)."""
     return {"Path": path, "Upstream": upstream, "ProxyConnectTimeout": p["ProxyConnectTimeout"],
             "ProxyReadTimeout": p["ProxyReadTimeout"], "ClientMaxBodySize": p["ClientMaxBodySize"],
-            "Rewrite": "", "SSL": False, "GRPC": False, "Websocket": False,
+            "Rewrite": rewrite, "SSL": False, "GRPC": False, "Websocket": False,
             "ProxyBuffering": p["ProxyBuffering"], "Wallarm": None, "MinionIngress": None}
 
 
@@ -239,6 +269,7 @@ def generate_nginx_cfg(ing_ex: dict, pems: dict, is_minion: bool, base: dict) ->
     """ingress.go:47-231 generateNginxCfg (OSS, no JWT/health-check/grpc paths)."""
     ing = ing_ex["Ingress"]
     p = parse_annotations(ing, base)
+    rewrites = get_rewrites(ing)   # ingress.go:51
     spec = ing.get("spec") or {}
     upstreams = {}
     default_backend = spec.get("backend")
@@ -270,13 +301,15 @@ def generate_nginx_cfg(ing_ex: dict, pems: dict, is_minion: bool, base: dict) ->
             ups_name = get_name_for_upstream(ing, host, be)
             if ups_name not in upstreams:
                 upstreams[ups_name] = _create_upstream(ing_ex, ups_name, be, p)
-            loc = _create_location(path_or_default(path.get("path", "")), upstreams[ups_name], p)
+            loc = _create_location(path_or_default(path.get("path", "")), upstreams[ups_name], p,
+                                   rewrites.get(be["serviceName"], ""))
             locations.append(loc)
             if loc["Path"] == "/":
                 root = True
         if not root and default_backend is not None:
             ups_name = get_name_for_upstream(ing, "", default_backend)
-            locations.append(_create_location("/", upstreams[ups_name], p))
+            locations.append(_create_location("/", upstreams[ups_name], p,
+                                              rewrites.get(default_backend["serviceName"], "")))
         server["Locations"] = locations
         servers.append(server)
     ns, name = _meta(ing)

@@ -33,7 +33,7 @@ STATS_FIELDS64 = ["table_bytes", "lds_bytes_scan", "last_candidates", "last_pair
 
 STATS_FIELDS_MS = ["last_ms_route", "last_ms_scan", "last_ms_verify", "last_ms_tail"]
 STATS_FIELDS_WAF = ["n_waf_keys", "bloom_pk", "bloom_fp_ppm", "last_ctx_pass", "last_jobs", "n_peers",
-                    "n_upstreams_deferred", "reserved1"]
+                    "n_upstreams_deferred", "decoders"]
 GM_CREATE_PROFILE = 0x2
 GM_CREATE_SERIAL = 0x4
 
@@ -52,7 +52,7 @@ class GmBatch(ctypes.Structure):
 EXPORTS = ["gm_create", "gm_destroy", "gm_abi_version", "gm_load_generation", "gm_match_batch", "gm_sync",
            "gm_counters", "gm_counters_reset", "gm_comm_unique_id", "gm_comm_init", "gm_counters_allreduce",
            "gm_stats", "gm_last_error", "gm_normalize_uris", "gm_counters_global", "gm_parse_requests",
-           "gm_peers_init", "gm_select_peers", "gm_release_peers", "gm_peer_address"]
+           "gm_peers_init", "gm_select_peers", "gm_release_peers", "gm_peer_address", "gm_upstream_uris"]
 
 # gm_peer_state (include/gpumatch.h)
 PEER_STATE_DTYPE = np.dtype([("conns", "<u4"), ("current_weight", "<i4"), ("flags", "<u4"), ("reserved", "<u4")])
@@ -96,6 +96,8 @@ def lib():
                                        ctypes.c_uint32, ctypes.c_void_p]
         L.gm_peer_address.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t,
                                       ctypes.c_void_p]
+        L.gm_upstream_uris.argtypes = [ctypes.c_void_p, ctypes.POINTER(GmBatch), ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.gm_last_error.restype = ctypes.c_char_p
         L.gm_last_error.argtypes = [ctypes.c_void_p]
         _lib = L
@@ -185,6 +187,13 @@ class Engine:
 
     def release_peers_ptr(self, ids_ptr, n, state_ptr, n_peers, stream=0):
         self._chk(lib().gm_release_peers(self.h, ids_ptr, n, state_ptr, n_peers, stream))
+
+    def upstream_uris_ptr(self, reqs_ptr, arena_ptr, arena_len, n, verdicts_ptr, out_ptr, out_cap, off_ptr, len_ptr,
+                          stream=0):
+        """gm_upstream_uris on device pointers: the URI each proxied request goes upstream with."""
+        b = GmBatch(reqs_ptr, arena_ptr, arena_len, n, 0, None)
+        self._chk(lib().gm_upstream_uris(self.h, ctypes.byref(b), verdicts_ptr, out_ptr, out_cap, off_ptr, len_ptr,
+                                         stream))
 
     def peer_address(self, peer: int):
         """(address, upstream id) of a global peer id."""

@@ -35,11 +35,17 @@ class Rule:
 
 
 class SigSet:
-    def __init__(self, rules):
+    """``decoders``: the request parsers (Wallarm's names: percent, urlenc, json_doc, base64) whose
+    decoded views of $args / the body the rules also scan ("@decoders" line, gm_decode.inc)."""
+
+    def __init__(self, rules, decoders=()):
         self.rules = list(rules)
+        self.decoders = list(decoders)
 
     def to_text(self) -> str:
         out = ["# gpumatch signature set v1"]
+        if self.decoders:
+            out.append("@decoders " + ",".join(self.decoders))
         for r in self.rules:
             fl = "i" if r.nocase else "-"
             if r.kind == "lit":
@@ -50,17 +56,20 @@ class SigSet:
 
     @staticmethod
     def from_text(text: str) -> "SigSet":
-        rules = []
+        rules, dec = [], []
         for line in text.splitlines():
             s = line.strip()
             if not s or s.startswith("#"):
+                continue
+            if s.startswith("@decoders"):
+                dec += [x.strip() for x in s[9:].split(",") if x.strip()]
                 continue
             kind, fl, zones, pat = s.split(" ", 3)
             if kind == "lit":
                 rules.append(Rule("lit", fl == "i", zones, bytes.fromhex(pat)))
             else:
                 rules.append(Rule("re", fl == "i", zones, pat))
-        return SigSet(rules)
+        return SigSet(rules, dec)
 
 
 # --------------------------------------------------------------------------- C4 generator

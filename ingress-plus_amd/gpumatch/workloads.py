@@ -89,11 +89,13 @@ def c4_sample(sigset: sigs.SigSet, n: int = 2000, seed: int = records.SEED_BASE 
     return b"".join(parts)
 
 
-def c4_blob(sigset: sigs.SigSet, mode: str = "block", sample: bytes | None = None) -> bytes:
+def c4_blob(sigset: sigs.SigSet, mode: str = "block", sample: bytes | None = None, parser_disable: str = "") -> bytes:
     base = confgen.default_config_params()
     base["MainEnableWallarm"] = True
     ing = copy.deepcopy(CAFE_INGRESS)
     ing["metadata"]["annotations"] = {"wallarm.com/mode": mode}
+    if parser_disable:
+        ing["metadata"]["annotations"]["wallarm.com/parser-disable"] = parser_disable
     files = confgen.ingress_files([ing], base=base, secrets=("cafe-secret",))
     return blob.make_blob(confgen.render_main(base), files, sigset.to_text(), sample)
 

@@ -160,6 +160,9 @@ typedef struct {
     int id, server;
     int auto_redirect;
     char *proxy_ups; int upstream_id; int has_proxy;
+    char *pass_uri;           /* proxy_pass URI part (nginx.org/rewrites), NULL none */
+    int pass_defer;           /* variables in proxy_pass, or a URI part nginx rejects */
+    int pd_mask, has_pd;      /* wallarm_parser_disable in the location (DEC bits) */
     int has_return; int ret_code;
     char *err418;             /* error_page 418 = <complex value> */
     int waf_mode;
@@ -172,6 +175,7 @@ typedef struct { char *var; int op; char *val; pcre *re; int code; char *text; i
 
 typedef struct {
     int id; int nports; int ports[16]; int ssl[16]; int def[16];
+    int pd_mask;              /* server-level wallarm_parser_disable */
     int nnames; char **names; int *nlen; pcre **nre;
     int nifs; sif_t *ifs;
     int nlocs; int *locs;
@@ -207,6 +211,7 @@ typedef struct orc_ctx {
     char **ups; int nups;
     int http_waf;
     sig_t *sig; int nsig;
+    int decoders;             /* the signature set's "@decoders" (DEC bits) */
     /* Aho-Corasick over case-folded bytes */
     int32_t *ac_next; int ac_states; int32_t *ac_out; int32_t *ac_dict; int32_t *ac_pat_next; int *ac_pat;
 } orc_ctx;
@@ -217,6 +222,15 @@ static int waf_mode_of(const char *s) {
     if (!strcmp(s, "safe_blocking")) return GM_WAF_SAFE_BLOCKING;
     if (!strcmp(s, "block")) return GM_WAF_BLOCK;
     return GM_WAF_OFF;
+}
+
+/* Wallarm parser names -> the engine's decoder bits (include/gpumatch.h GM_DEC_*) */
+static int dec_bit(const char *nm) {
+    if (!strcmp(nm, "percent")) return GM_DEC_PERCENT;
+    if (!strcmp(nm, "urlenc")) return GM_DEC_URLENC;
+    if (!strcmp(nm, "json_doc") || !strcmp(nm, "json")) return GM_DEC_JSON;
+    if (!strcmp(nm, "base64")) return GM_DEC_BASE64;
+    return 0;
 }
 
 static pcre *re_compile(const char *pat, int caseless) {
@@ -422,6 +436,10 @@ static void add_location(build_t *B, srv_t *S, dir_t *d, int srv_waf) {
             const char *p = strstr(u, "://"); p = p ? p + 3 : u;
             int n = 0; while (p[n] && p[n] != '/' && p[n] != '$') n++;
             L.proxy_ups = xstrndup(p, n); L.has_proxy = 1;
+            L.pass_uri = p[n] == '/' ? strdup(p + n) : NULL;
+            L.pass_defer = strchr(u, '$') != NULL ||
+                           (L.pass_uri && (!strcmp(k->args[0], "grpc_pass") || L.kind == LK_REGEX ||
+                                           L.kind == LK_REGEX_I || L.kind == LK_NAMED));
         } else if (!strcmp(k->args[0], "return") && k->nargs >= 2) {
             L.has_return = 1; L.ret_code = atoi(k->args[1]);
             if (!isdigit((unsigned char)k->args[1][0])) L.ret_code = 302;
@@ -430,6 +448,8 @@ static void add_location(build_t *B, srv_t *S, dir_t *d, int srv_waf) {
             L.err418 = strdup(k->args[3]);
         } else if (!strcmp(k->args[0], "wallarm_mode") && k->nargs == 2) {
             L.waf_mode = waf_mode_of(k->args[1]);
+        } else if (!strcmp(k->args[0], "wallarm_parser_disable") && k->nargs == 2) {
+            L.pd_mask |= dec_bit(k->args[1]); L.has_pd = 1;
         } else if (!strcmp(k->args[0], "location") || !strcmp(k->args[0], "if") || !strcmp(k->args[0], "rewrite")) {
             L.nested = 1;   /* nested location / if / rewrite: outside the restated subset */
         }
@@ -448,6 +468,7 @@ static void add_server(build_t *B, dir_t *s, int http_waf) {
     for (int i = 0; i < s->nkids; i++) {
         dir_t *d = &s->kids[i];
         if (d->nargs == 2 && !strcmp(d->args[0], "wallarm_mode")) S.waf_mode = waf_mode_of(d->args[1]);
+        if (d->nargs == 2 && !strcmp(d->args[0], "wallarm_parser_disable")) S.pd_mask |= dec_bit(d->args[1]);
     }
     c->srv = realloc(c->srv, sizeof(srv_t) * (c->nsrv + 1)); c->nsrv++;
     for (int i = 0; i < s->nkids; i++) {
@@ -533,6 +554,16 @@ static int load_sigs(orc_ctx *c, const char *t, int n) {
         int le = e; while (le > ls && (t[le - 1] == '\r' || t[le - 1] == ' ' || t[le - 1] == '\t')) le--;
         i = e + 1;
         if (ls >= le || t[ls] == '#') continue;
+        if (le - ls >= 9 && !strncmp(t + ls, "@decoders", 9)) {
+            int p = ls + 9;
+            while (p < le) {
+                while (p < le && (t[p] == ' ' || t[p] == ',' || t[p] == '\t')) p++;
+                int q = p; while (q < le && t[q] != ',' && t[q] != ' ' && t[q] != '\t') q++;
+                if (q > p) { char nm[32] = {0}; memcpy(nm, t + p, (size_t)(q - p < 31 ? q - p : 31)); c->decoders |= dec_bit(nm); }
+                p = q;
+            }
+            continue;
+        }
         char kind[8] = {0}, fl[8] = {0}, zs[8] = {0};
         int p = ls, f = 0;
         char *dst[3] = {kind, fl, zs};
@@ -1183,9 +1214,9 @@ static void hb_push(hitbuf_t *h, uint32_t v) {
     h->ids[h->n++] = v;
 }
 
-static void waf_scan(orc_ctx *c, rq_t *q, uint8_t *mark, hitbuf_t *out) {
-    sv zones[4] = {q->uri, q->args, q->hdrs, q->body};
-    size_t first = out->n;
+/* literal (Aho-Corasick) and regex signatures over four zones; skip_empty: regexes only on
+ * non-empty zones (the decoded views' pass) */
+static void waf_zones(orc_ctx *c, const sv *zones, uint8_t *mark, hitbuf_t *out, int skip_empty) {
     for (int z = 0; z < 4; z++) {
         sv Z = zones[z];
         int s = 0;
@@ -1209,11 +1240,131 @@ static void waf_scan(orc_ctx *c, rq_t *q, uint8_t *mark, hitbuf_t *out) {
         if (g->kind != 1 || !g->re || mark[p]) continue;
         for (int z = 0; z < 4; z++) {
             if (!(g->zones & (1 << z))) continue;
+            if (skip_empty && zones[z].n == 0) continue;
             int ov[30];
             if (pcre_exec(g->re, g->ex, zones[z].p ? zones[z].p : "", zones[z].n, 0, 0, ov, 30) >= 0) {
                 mark[p] = 1; hb_push(out, (uint32_t)p); break;
             }
         }
+    }
+}
+
+/* ------------------------------------------------------------------ request parsers (§8 f4)
+ * The decoded views gm_decode.inc builds, restated: $args -> [percent / urlenc transform if it
+ * changes a byte, '\n'] [each base64 run (>= 16 of [A-Za-z0-9+/]) decoded, '\n']; body -> the
+ * form transform of an application/x-www-form-urlencoded body or the JSON unescape of a "json"
+ * body (if it changes a byte, then '\n'), then the body's base64 runs. */
+typedef struct { uint8_t *p; size_t n, cap; } dbuf_t;
+static void db_put(dbuf_t *b, uint8_t ch) {
+    if (b->n == b->cap) { b->cap = b->cap ? 2 * b->cap : 256; b->p = realloc(b->p, b->cap); }
+    b->p[b->n++] = ch;
+}
+static int hexd(int c) { return c >= '0' && c <= '9' ? c - '0' : (c | 0x20) >= 'a' && (c | 0x20) <= 'f' ? (c | 0x20) - 'a' + 10 : -1; }
+static int b64d(int c) {
+    if (c >= 'A' && c <= 'Z') return c - 'A';
+    if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+    if (c >= '0' && c <= '9') return c - '0' + 52;
+    return c == '+' ? 62 : c == '/' ? 63 : -1;
+}
+static void dv_form(sv s, int mask, dbuf_t *o) {
+    size_t st = o->n; int chg = 0;
+    for (int i = 0; i < s.n; i++) {
+        unsigned char ch = (unsigned char)s.p[i];
+        if ((mask & GM_DEC_PERCENT) && ch == '%' && i + 2 < s.n && hexd((unsigned char)s.p[i + 1]) >= 0 &&
+            hexd((unsigned char)s.p[i + 2]) >= 0) {
+            ch = (unsigned char)(hexd((unsigned char)s.p[i + 1]) * 16 + hexd((unsigned char)s.p[i + 2])); i += 2; chg = 1;
+        } else if ((mask & GM_DEC_URLENC) && ch == '+') { ch = ' '; chg = 1; }
+        db_put(o, ch);
+    }
+    if (chg) db_put(o, '\n'); else o->n = st;
+}
+static void utf8(dbuf_t *o, unsigned cp) {
+    if (cp < 0x80) db_put(o, (uint8_t)cp);
+    else if (cp < 0x800) { db_put(o, (uint8_t)(0xC0 | cp >> 6)); db_put(o, (uint8_t)(0x80 | (cp & 63))); }
+    else if (cp < 0x10000) { db_put(o, (uint8_t)(0xE0 | cp >> 12)); db_put(o, (uint8_t)(0x80 | (cp >> 6 & 63))); db_put(o, (uint8_t)(0x80 | (cp & 63))); }
+    else { db_put(o, (uint8_t)(0xF0 | cp >> 18)); db_put(o, (uint8_t)(0x80 | (cp >> 12 & 63))); db_put(o, (uint8_t)(0x80 | (cp >> 6 & 63))); db_put(o, (uint8_t)(0x80 | (cp & 63))); }
+}
+static int u4(sv s, int i) {
+    if (i + 4 > s.n) return -1;
+    int v = 0;
+    for (int k = 0; k < 4; k++) { int h = hexd((unsigned char)s.p[i + k]); if (h < 0) return -1; v = v * 16 + h; }
+    return v;
+}
+static void dv_json(sv s, dbuf_t *o) {
+    size_t st = o->n; int chg = 0;
+    for (int i = 0; i < s.n; i++) {
+        unsigned char ch = (unsigned char)s.p[i];
+        if (ch != '\\' || i + 1 >= s.n) { db_put(o, ch); continue; }
+        char e = s.p[i + 1];
+        const char *from = "\"\\/bfnrt", *to = "\"\\/\b\f\n\r\t";
+        const char *f = strchr(from, e);
+        if (e && f) { db_put(o, (uint8_t)to[f - from]); i++; chg = 1; continue; }
+        if (e == 'u') {
+            int cp = u4(s, i + 2);
+            if (cp >= 0) {
+                int adv = 5;
+                if (cp >= 0xD800 && cp <= 0xDBFF) {
+                    int lo = (i + 7 < s.n && s.p[i + 6] == '\\' && s.p[i + 7] == 'u') ? u4(s, i + 8) : -1;
+                    if (lo >= 0xDC00 && lo <= 0xDFFF) { cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00); adv = 11; }
+                    else cp = 0xFFFD;
+                } else if (cp >= 0xDC00 && cp <= 0xDFFF) cp = 0xFFFD;
+                utf8(o, (unsigned)cp); i += adv; chg = 1;
+                continue;
+            }
+        }
+        db_put(o, ch);
+    }
+    if (chg) db_put(o, '\n'); else o->n = st;
+}
+static void dv_b64(sv s, dbuf_t *o) {
+    int i = 0;
+    while (i < s.n) {
+        if (b64d((unsigned char)s.p[i]) < 0) { i++; continue; }
+        int j = i; while (j < s.n && b64d((unsigned char)s.p[j]) >= 0) j++;
+        int L = j - i;
+        if (L >= 16) {
+            for (int q = i; q + 4 <= i + (L & ~3); q += 4) {
+                unsigned v = (unsigned)b64d((unsigned char)s.p[q]) << 18 | (unsigned)b64d((unsigned char)s.p[q + 1]) << 12 |
+                             (unsigned)b64d((unsigned char)s.p[q + 2]) << 6 | (unsigned)b64d((unsigned char)s.p[q + 3]);
+                db_put(o, (uint8_t)(v >> 16)); db_put(o, (uint8_t)(v >> 8)); db_put(o, (uint8_t)v);
+            }
+            db_put(o, '\n');
+        }
+        i = j;
+    }
+}
+/* 1 form, 2 json, 0 other: the first Content-Type line */
+static int orc_body_kind(rq_t *q) {
+    int pos = 0; sv hn, vv;
+    while (hdr_next(q->hdrs, &pos, &hn, &vv)) {
+        if (!hdr_name_match(hn, "content_type", 12)) continue;
+        if (vv.n >= 33 && !strncasecmp(vv.p, "application/x-www-form-urlencoded", 33)) return 1;
+        for (int k = 0; k + 4 <= vv.n; k++) if (!strncasecmp(vv.p + k, "json", 4)) return 2;
+        return 0;
+    }
+    return 0;
+}
+static void decoded_views(rq_t *q, int mask, dbuf_t *a, dbuf_t *b) {
+    if (mask & (GM_DEC_PERCENT | GM_DEC_URLENC)) dv_form(q->args, mask, a);
+    if (mask & GM_DEC_BASE64) dv_b64(q->args, a);
+    int kind = (mask & (GM_DEC_PERCENT | GM_DEC_URLENC | GM_DEC_JSON)) ? orc_body_kind(q) : 0;
+    if (kind == 1 && (mask & (GM_DEC_PERCENT | GM_DEC_URLENC))) dv_form(q->body, mask, b);
+    else if (kind == 2 && (mask & GM_DEC_JSON)) dv_json(q->body, b);
+    if (mask & GM_DEC_BASE64) dv_b64(q->body, b);
+}
+
+static void waf_scan(orc_ctx *c, rq_t *q, uint8_t *mark, hitbuf_t *out, int dec_mask) {
+    sv zones[4] = {q->uri, q->args, q->hdrs, q->body};
+    size_t first = out->n;
+    waf_zones(c, zones, mark, out, 0);
+    if (dec_mask) {
+        dbuf_t a = {0}, b = {0};
+        decoded_views(q, dec_mask, &a, &b);
+        if (a.n || b.n) {
+            sv dz[4] = {{"", 0}, {(const char *)a.p, (int)a.n}, {"", 0}, {(const char *)b.p, (int)b.n}};
+            waf_zones(c, dz, mark, out, 1);
+        }
+        free(a.p); free(b.p);
     }
     /* sort this request's ids ascending, clear marks */
     for (size_t i = first + 1; i < out->n; i++) {
@@ -1304,7 +1455,10 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
     v->waf_mode = (uint16_t)F->waf_mode;
     if (F->waf_mode != GM_WAF_OFF && c->nsig) {
         size_t before = hits->n;
-        waf_scan(c, &q, mark, hits);
+        /* the request parsers of the URI-selected location (its own wallarm_parser_disable list,
+         * else its server's) */
+        int dmask = c->decoders & ~(L->has_pd ? L->pd_mask : S->pd_mask);
+        waf_scan(c, &q, mark, hits, dmask);
         *nh = (uint32_t)(hits->n - before);
         v->n_hits = (uint16_t)*nh;
         if (*nh && F->waf_mode == GM_WAF_BLOCK) { v->action = GM_ACT_BLOCK; v->status = 403; }
@@ -1886,4 +2040,70 @@ int orc_peers_init(orc_ctx *c, gm_peer_state *st, uint32_t n_peers) {
         for (int j = 0; j < U->npeers; j++) st[U->first_peer + j].flags = U->down[j] ? GM_PEER_DOWN : 0;
     }
     return 0;
+}
+
+/* ------------------------------------------------------------------ upstream request URI (§8 f1)
+ * ngx_http_proxy_create_request restated: proxy_pass without a URI part sends the unparsed
+ * $request_uri; with one (nginx.org/rewrites) the URI part + $uri after the location prefix
+ * (ngx_escape_uri NGX_ESCAPE_URI when r->quoted_uri) + "?" $args.  r->quoted_uri: the request-line
+ * parser (ngx_http_parse_request_line) met '%' in sw_check_uri / sw_after_slash_in_uri, i.e.
+ * before any '?', '#', "/." or "//" moved it to sw_uri. */
+static int orc_quoted(const char *p, int n) {
+    int slash = 0;
+    for (int i = 0; i < n; i++) {
+        char c = p[i];
+        if (c == '%') return 1;
+        if (c == '?' || c == '#') return 0;
+        if (slash && (c == '.' || c == '/')) return 0;
+        slash = c == '/';
+    }
+    return 0;
+}
+
+static int orc_esc(unsigned char c) {   /* ngx_escape_uri's NGX_ESCAPE_URI table */
+    static const uint32_t uri[] = {0xffffffff, 0x80000029, 0x00000000, 0x80000000,
+                                   0xffffffff, 0xffffffff, 0xffffffff, 0xffffffff};
+    return (uri[c >> 5] >> (c & 0x1f)) & 1;
+}
+
+/* out_off[i] = running offset; out_len[i] = length, GM_NONE (not proxied / past cap) or
+ * GM_PEER_DEFER.  Returns the total bytes, or -1 if cap was exceeded. */
+int64_t orc_upstream_uris(orc_ctx *c, const gm_req *reqs, const uint8_t *arena, const gm_verdict *v, uint32_t n,
+                          uint8_t *out, uint64_t cap, uint64_t *out_off, uint32_t *out_len) {
+    uint64_t off = 0; int over = 0;
+    static const char hex[] = "0123456789ABCDEF";
+    for (uint32_t i = 0; i < n; i++) {
+        out_off[i] = off; out_len[i] = GM_NONE;
+        if (v[i].action != GM_ACT_PROXY || v[i].location_id == GM_NONE) continue;
+        if (v[i].gen != c->gen || (int)v[i].location_id >= c->nloc) { out_len[i] = GM_PEER_DEFER; continue; }
+        loc_t *L = &c->loc[v[i].location_id];
+        if (L->pass_defer) { out_len[i] = GM_PEER_DEFER; continue; }
+        rq_t q; rq_init(&q, &reqs[i], arena);
+        uint8_t *buf = malloc(3 * (size_t)q.uri.n + q.args.n + q.ruri.n + (L->pass_uri ? strlen(L->pass_uri) : 0) + 8);
+        size_t k = 0;
+        if (!L->pass_uri) {
+            if (q.ruri.n) { memcpy(buf, q.ruri.p, q.ruri.n); k = q.ruri.n; }
+            else {
+                memcpy(buf, q.uri.p, q.uri.n); k = q.uri.n;
+                if (q.args.n) { buf[k++] = '?'; memcpy(buf + k, q.args.p, q.args.n); k += q.args.n; }
+            }
+        } else {
+            size_t rl = strlen(L->pass_uri);
+            memcpy(buf, L->pass_uri, rl); k = rl;
+            int esc = q.ruri.n ? orc_quoted(q.ruri.p, q.ruri.n) : orc_quoted(q.uri.p, q.uri.n);
+            int t0 = L->plen < q.uri.n ? L->plen : q.uri.n;
+            for (int j = t0; j < q.uri.n; j++) {
+                unsigned char ch = (unsigned char)q.uri.p[j];
+                if (esc && orc_esc(ch)) { buf[k++] = '%'; buf[k++] = hex[ch >> 4]; buf[k++] = hex[ch & 15]; }
+                else buf[k++] = ch;
+            }
+            if (q.args.n) { buf[k++] = '?'; memcpy(buf + k, q.args.p, q.args.n); k += q.args.n; }
+        }
+        if (off + k > cap) { over = 1; free(buf); continue; }
+        memcpy(out + off, buf, k);
+        out_len[i] = (uint32_t)k;
+        off += k;
+        free(buf);
+    }
+    return over ? -1 : (int64_t)off;
 }

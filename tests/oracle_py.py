@@ -127,3 +127,38 @@ class Balancer:
         for p in ids:
             if p < self.n_peers:
                 self.state["conns"][p] -= 1
+
+
+def upstream_uris(o: Oracle, reqs: np.ndarray, arena: np.ndarray, verdicts: np.ndarray):
+    """oracle orc_upstream_uris: (out bytes, offsets, lengths) of the URIs sent upstream."""
+    L = lib()
+    L.orc_upstream_uris.restype = ctypes.c_int64
+    L.orc_upstream_uris.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                    ctypes.c_void_p]
+    n = len(reqs)
+    reqs = np.ascontiguousarray(reqs)
+    arena = np.ascontiguousarray(arena) if len(arena) else np.zeros(16, np.uint8)
+    verdicts = np.ascontiguousarray(verdicts)
+    cap = int(4 * len(arena) + 4096 * n + 16)
+    out = np.zeros(cap, np.uint8)
+    off = np.zeros(n, np.uint64)
+    ln = np.zeros(n, np.uint32)
+    tot = L.orc_upstream_uris(o.h, reqs.ctypes.data, arena.ctypes.data, verdicts.ctypes.data, n, out.ctypes.data,
+                              cap, off.ctypes.data, ln.ctypes.data)
+    if tot < 0:
+        raise RuntimeError("oracle upstream URIs: capacity")
+    return out[:tot], off, ln
+
+
+def uri_list(out, off, ln):
+    """per request: bytes, or None (not proxied) / "defer" """
+    res = []
+    for o, k in zip(off, ln):
+        if k == 0xFFFFFFFF:
+            res.append(None)
+        elif k == 0xFFFFFFFE:
+            res.append("defer")
+        else:
+            res.append(bytes(out[int(o):int(o) + int(k)]))
+    return res
