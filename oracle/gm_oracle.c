@@ -187,7 +187,13 @@ typedef struct { char *src; char *var; int np; mparam_t *p; char *defval; int ho
 typedef struct { uint32_t bound; int star; char *val; } part_t;
 typedef struct { char *src; char *var; int np; part_t *p; } split_t;
 
-typedef struct { int kind; int nocase; int zones; uint8_t *lit; int len; pcre *re; pcre_extra *ex; } sig_t;
+typedef struct {
+    int kind; int nocase; int zones; uint8_t *lit; int len; pcre *re; pcre_extra *ex;
+    /* prefilter: literals one of which every match of the regex contains (lowercased), nfac 0:
+     * none (the regex runs on every zone) */
+    char fac[16][64]; int flen[16]; int nfac;
+    char *pattern_src;
+} sig_t;
 
 /* an upstream block (version1/nginx.ingress.tmpl:2-8, version2/nginx.virtualserver.tmpl:2-10) */
 enum { OM_RR, OM_LEAST_CONN, OM_IP_HASH, OM_HASH, OM_CHASH, OM_RANDOM, OM_RANDOM2, OM_DEFER };
@@ -212,6 +218,10 @@ typedef struct orc_ctx {
     int http_waf;
     sig_t *sig; int nsig;
     int decoders;             /* the signature set's "@decoders" (DEC bits) */
+    /* CPU-baseline engine (orc_set_prefilter): a regex runs on a zone only if its required factor
+     * occurs there (Aho-Corasick over the factors), as a competent CPU WAF would do */
+    int prefilter;
+    int32_t *fac_next; int32_t *fac_out; int32_t *fac_dict; int32_t *fac_pat_next; int32_t *fac_pat_re;
     /* Aho-Corasick over case-folded bytes */
     int32_t *ac_next; int ac_states; int32_t *ac_out; int32_t *ac_dict; int32_t *ac_pat_next; int *ac_pat;
 } orc_ctx;
@@ -581,13 +591,122 @@ static int load_sigs(orc_ctx *c, const char *t, int n) {
             s.kind = 1;
             char *pat = xstrndup(t + p, le - p);
             s.re = re_compile(pat, s.nocase);
-            free(pat);
+            s.pattern_src = pat;
             if (!s.re) { seterr("bad signature regex", NULL); return -1; }
             const char *er;
             s.ex = pcre_study(s.re, PCRE_STUDY_JIT_COMPILE, &er);
         }
         c->sig = realloc(c->sig, sizeof(sig_t) * (c->nsig + 1)); c->sig[c->nsig++] = s;
     }
+    return 0;
+}
+
+/* A literal that every match of a PCRE pattern contains, or 0: the longest run of plain
+ * characters at top level, each kept only if its quantifier has a minimum >= 1 (a '+' or {n,}
+ * quantifier ends the run after its character, '*' '?' {0,} drop it); groups, classes, escapes
+ * of letters and digits, '.', anchors end a run; a top-level '|', "(?" or \Q anywhere: no factor. */
+static int skip_quant(const char *p, int i, int *min) {
+    *min = 1;
+    if (p[i] == '*' || p[i] == '?') { *min = 0; i++; }
+    else if (p[i] == '+') { *min = 2; i++; }
+    else if (p[i] == '{') {
+        int j = i + 1, n = 0, dig = 0;
+        while (p[j] >= '0' && p[j] <= '9') { n = n * 10 + (p[j] - '0'); j++; dig = 1; }
+        if (!dig) return i;   /* a literal '{' */
+        while (p[j] && p[j] != '}') j++;
+        if (!p[j]) return i;
+        *min = n == 0 ? 0 : 2;
+        i = j + 1;
+    } else return i;
+    if (p[i] == '?' || p[i] == '+') i++;   /* lazy / possessive */
+    return i;
+}
+/* a group body that is an alternation of plain literals (escaped punctuation allowed): its
+ * alternatives, lowercased, into alts; 0 if any part is not a plain literal or is shorter than 3 */
+static int literal_alts(const char *p, int n, char alts[16][64], int *alen) {
+    int na = 0, cl = 0;
+    char cur[64];
+    for (int i = 0; i <= n; i++) {
+        if (i == n || p[i] == '|') {
+            if (cl < 3 || na == 16) return 0;
+            memcpy(alts[na], cur, cl); alen[na++] = cl; cl = 0;
+            continue;
+        }
+        char ch = p[i];
+        if (ch == '\\') {
+            if (i + 1 >= n || isalnum((unsigned char)p[i + 1])) return 0;
+            ch = p[++i];
+        } else if (strchr(".^$*+?{}[]()", ch)) return 0;
+        if (cl == 63) return 0;
+        cur[cl++] = (char)lc((unsigned char)ch);
+    }
+    return na;
+}
+
+static int extract_factor(const char *p, char alts[16][64], int *alen) {
+    int depth = 0, cls = 0;
+    for (int i = 0; p[i]; i++) {
+        if (p[i] == '\\' && p[i + 1] == 'Q') return 0;
+        if (p[i] == '\\' && p[i + 1]) { i++; continue; }
+        if (cls) { if (p[i] == ']') cls = 0; continue; }
+        if (p[i] == '[') { cls = 1; if (p[i + 1] == '^') i++; if (p[i + 1] == ']') i++; continue; }
+        if (p[i] == '(') { if (p[i + 1] == '?' && p[i + 2] != ':') return 0; depth++; }
+        else if (p[i] == ')') depth--;
+        else if (p[i] == '|' && depth == 0) return 0;
+    }
+    char cur[256], best[256]; int cl = 0, bl = 0, i = 0, min;
+    char galts[16][64]; int glen[16], gn = 0, gmin = 0;
+#define FLUSH() do { if (cl > bl) { memcpy(best, cur, cl); bl = cl; } cl = 0; } while (0)
+    while (p[i]) {
+        char c = p[i], lit;
+        if (c == '\\') {
+            char e = p[i + 1];
+            if (!e) break;
+            if (isalnum((unsigned char)e)) { FLUSH(); i = skip_quant(p, i + 2, &min); continue; }
+            lit = e; i += 2;
+        } else if (c == '[') {
+            int j = i + 1;
+            if (p[j] == '^') j++;
+            if (p[j] == ']') j++;
+            while (p[j] && p[j] != ']') { if (p[j] == '\\' && p[j + 1]) j++; j++; }
+            FLUSH(); i = skip_quant(p, p[j] ? j + 1 : j, &min); continue;
+        } else if (c == '(') {
+            int j = i, d = 0, k = 0;
+            for (; p[j]; j++) {
+                if (p[j] == '\\' && p[j + 1]) { j++; continue; }
+                if (k) { if (p[j] == ']') k = 0; continue; }
+                if (p[j] == '[') { k = 1; if (p[j + 1] == '^') j++; if (p[j + 1] == ']') j++; continue; }
+                if (p[j] == '(') d++;
+                else if (p[j] == ')' && --d == 0) break;
+            }
+            FLUSH();
+            const int body = i + ((p[i + 1] == '?') ? 3 : 1);   /* "(?:" or "(" */
+            i = skip_quant(p, p[j] ? j + 1 : j, &min);
+            if (min > 0 && !gn) {   /* a required group of literal alternatives */
+                char t[16][64]; int tl[16];
+                const int na = p[j] ? literal_alts(p + body, j - body, t, tl) : 0;
+                int mn = 64;
+                for (int q = 0; q < na; q++) mn = tl[q] < mn ? tl[q] : mn;
+                if (na) { memcpy(galts, t, sizeof t); memcpy(glen, tl, sizeof tl); gn = na; gmin = mn; }
+            }
+            continue;
+        } else if (c == '.' || c == '^' || c == '$' || c == '*' || c == '+' || c == '?' || c == '{' || c == ')') {
+            FLUSH(); i = skip_quant(p, i + 1, &min); continue;
+        } else { lit = c; i++; }
+        i = skip_quant(p, i, &min);
+        if (min == 0) { FLUSH(); continue; }
+        if (cl < 255) cur[cl++] = (char)lc((unsigned char)lit);
+        if (min == 2) FLUSH();
+    }
+    FLUSH();
+#undef FLUSH
+    /* the longest plain run, unless a literal-alternation group has longer shortest members */
+    if (bl >= 3 && (bl >= 4 || !gn || gmin <= bl)) {
+        if (bl > 63) bl = 63;
+        memcpy(alts[0], best, bl); alen[0] = bl;
+        return 1;
+    }
+    if (gn) { memcpy(alts, galts, sizeof galts); memcpy(alen, glen, sizeof glen); return gn; }
     return 0;
 }
 
@@ -627,6 +746,67 @@ static void build_ac(orc_ctx *c) {
     }
     free(q); free(fail);
     c->ac_next = nx; c->ac_states = ns; c->ac_out = out; c->ac_dict = dict; c->ac_pat_next = pnext;
+}
+
+static void build_fac_ac(orc_ctx *c) {
+    int total = 1, npat = 0;
+    for (int i = 0; i < c->nsig; i++) {
+        sig_t *g = &c->sig[i];
+        if (g->kind != 1) continue;
+        g->nfac = extract_factor(g->pattern_src ? g->pattern_src : "", g->fac, g->flen);
+        for (int k = 0; k < g->nfac; k++) { total += g->flen[k]; npat++; }
+    }
+    int32_t *nx = malloc(sizeof(int32_t) * 256 * (size_t)total);
+    for (size_t k = 0; k < 256 * (size_t)total; k++) nx[k] = -1;
+    int32_t *out = malloc(sizeof(int32_t) * total), *fail = calloc(total, sizeof(int32_t));
+    int32_t *dict = malloc(sizeof(int32_t) * total);
+    for (int k = 0; k < total; k++) { out[k] = -1; dict[k] = -1; }
+    int32_t *pnext = malloc(sizeof(int32_t) * (npat + 1)), *pre = malloc(sizeof(int32_t) * (npat + 1));
+    int ns = 1, pid = 0;
+    for (int i = 0; i < c->nsig; i++) {
+        sig_t *g = &c->sig[i];
+        if (g->kind != 1) continue;
+        for (int f = 0; f < g->nfac; f++, pid++) {
+            int s = 0;
+            for (int k = 0; k < g->flen[f]; k++) {
+                int b = (unsigned char)g->fac[f][k];
+                if (nx[(size_t)s * 256 + b] < 0) nx[(size_t)s * 256 + b] = ns++;
+                s = nx[(size_t)s * 256 + b];
+            }
+            pre[pid] = i; pnext[pid] = out[s]; out[s] = pid;
+        }
+    }
+    int32_t *q = malloc(sizeof(int32_t) * ns); int qh = 0, qt = 0;
+    for (int b = 0; b < 256; b++) {
+        int t = nx[b];
+        if (t < 0) nx[b] = 0; else { fail[t] = 0; q[qt++] = t; }
+    }
+    while (qh < qt) {
+        int s = q[qh++];
+        dict[s] = (out[fail[s]] >= 0) ? fail[s] : dict[fail[s]];
+        for (int b = 0; b < 256; b++) {
+            int t = nx[(size_t)s * 256 + b];
+            if (t < 0) nx[(size_t)s * 256 + b] = nx[(size_t)fail[s] * 256 + b];
+            else { fail[t] = nx[(size_t)fail[s] * 256 + b]; q[qt++] = t; }
+        }
+    }
+    free(q); free(fail);
+    c->fac_next = nx; c->fac_out = out; c->fac_dict = dict; c->fac_pat_next = pnext; c->fac_pat_re = pre;
+}
+
+/* switch the CPU-baseline prefilter on (1) or off (0, the checker's exhaustive PCRE runs) */
+int orc_set_prefilter(orc_ctx *c, int on) {
+    if (on && !c->fac_next) build_fac_ac(c);
+    c->prefilter = on;
+    return 0;
+}
+/* the prefilter literals of a regex, '|'-joined into out (>= 16 * 65 bytes); returns their count */
+int orc_factor(const char *pat, char *out) {
+    char a[16][64]; int l[16];
+    int n = extract_factor(pat, a, l), k = 0;
+    for (int i = 0; i < n; i++) { if (i) out[k++] = '|'; memcpy(out + k, a[i], l[i]); k += l[i]; }
+    out[k] = 0;
+    return n;
 }
 
 /* ------------------------------------------------------------------ public: create */
@@ -1235,12 +1415,27 @@ static void waf_zones(orc_ctx *c, const sv *zones, uint8_t *mark, hitbuf_t *out,
             }
         }
     }
+    uint8_t *cand = c->prefilter ? mark + c->nsig + 1 : NULL;
+    if (cand) {
+        for (int z = 0; z < 4; z++) {
+            sv Z = zones[z];
+            int s = 0;
+            for (int i = 0; i < Z.n; i++) {
+                s = c->fac_next[(size_t)s * 256 + lc((unsigned char)Z.p[i])];
+                for (int t = (c->fac_out[s] >= 0) ? s : c->fac_dict[s]; t > 0; t = c->fac_dict[t])
+                    for (int p = c->fac_out[t]; p >= 0; p = c->fac_pat_next[p]) cand[c->fac_pat_re[p]] |= (uint8_t)(1 << z);
+            }
+        }
+    }
     for (int p = 0; p < c->nsig; p++) {
         sig_t *g = &c->sig[p];
-        if (g->kind != 1 || !g->re || mark[p]) continue;
+        if (g->kind != 1 || !g->re || mark[p]) { if (cand) cand[p] = 0; continue; }
+        const int cz = cand ? cand[p] : 0;
+        if (cand) cand[p] = 0;
         for (int z = 0; z < 4; z++) {
             if (!(g->zones & (1 << z))) continue;
             if (skip_empty && zones[z].n == 0) continue;
+            if (cand && g->nfac && !(cz & (1 << z))) continue;   /* none of its factors is in the zone */
             int ov[30];
             if (pcre_exec(g->re, g->ex, zones[z].p ? zones[z].p : "", zones[z].n, 0, 0, ov, 30) >= 0) {
                 mark[p] = 1; hb_push(out, (uint32_t)p); break;
@@ -1473,7 +1668,7 @@ typedef struct {
 static void *worker(void *arg) {
     job_t *j = arg;
     scratch_t sc = {NULL};
-    uint8_t *mark = calloc(j->c->nsig + 1, 1);
+    uint8_t *mark = calloc(2 * (size_t)(j->c->nsig + 1), 1);   /* marks + prefilter candidate bits */
     for (size_t i = j->lo; i < j->hi; i++) {
         uint32_t nh;
         eval_one(j->c, &j->reqs[i], j->arena, &j->out[i], &sc, mark, &j->hits, &nh);

@@ -30,16 +30,22 @@ def lib():
         L.orc_murmur2.restype = ctypes.c_uint32
         L.orc_murmur2.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.orc_pcre_match.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.orc_set_prefilter.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.orc_factor.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         _lib = L
     return _lib
 
 
 class Oracle:
-    def __init__(self, blob: bytes, gen: int = 1):
+    def __init__(self, blob: bytes, gen: int = 1, prefilter: bool = False):
+        """prefilter: the CPU-baseline engine (regexes behind their required-factor prefilter);
+        off (the checker): every regex signature runs on every zone."""
         self._blob = blob
         self.h = lib().orc_create(blob, len(blob), gen)
         if not self.h:
             raise RuntimeError("oracle: " + lib().orc_error().decode())
+        if prefilter:
+            lib().orc_set_prefilter(ctypes.c_void_p(self.h), 1)
         info = np.zeros(4, dtype=np.uint32)
         lib().orc_info(self.h, info.ctypes.data)
         self.n_servers, self.n_locations, self.n_upstreams, self.n_sigs = (int(x) for x in info)
@@ -162,3 +168,10 @@ def uri_list(out, off, ln):
         else:
             res.append(bytes(out[int(o):int(o) + int(k)]))
     return res
+
+
+def regex_factor(pat: str) -> bytes:
+    """the oracle's prefilter literals of a regex (lowercased, '|'-joined), b"" if none"""
+    buf = ctypes.create_string_buffer(16 * 65 + 4)
+    lib().orc_factor(pat.encode(), buf)
+    return buf.value
