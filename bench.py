@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--pool", type=int, default=1_000_000)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--stress-requests", type=int, default=2_000_000,
+                    help="the C4 stress variant's batch (0: skip); reported under the line's 'stress' key")
     ap.add_argument("--serial", action="store_true",
                     help="measurement: the route stage alone before the scan (GM_CREATE_SERIAL)")
     args = ap.parse_args()
@@ -166,11 +168,75 @@ def main():
                      "algorithmic_bytes_per_launch": zone_bytes},
     }
     result["roofline"].update(pmc_traffic())
+    if world == 1 and args.stress_requests > 0:
+        del d_arena, d_reqs, d_out, d_hits
+        torch.cuda.empty_cache()
+        result["stress"] = stress_leg(torch, engine, records, workloads, args, local)
     if not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(ss, gblob, preqs, parena, args.cpu_seconds)
     if dist:
         dist.destroy_process_group()
     print(json.dumps(result), flush=True)
+
+
+def stress_leg(torch, engine, records, workloads, args, local):
+    """The C4 stress variant beside the headline: vocabulary literals that
+    benign SQL / HTML text also speaks, 10% factorless regexes (k_waf_always on every (request,
+    zone)) -- a 200k-request pool replicated to --stress-requests in HBM, K steps timed the same
+    way.  Not the headline: the headline config stays C4."""
+    ss, b = workloads.c4_stress_generation()
+    e = engine.Engine(local, profile=True)
+    e.load(b, 2)
+    n = args.stress_requests
+    preqs, parena = records.gen_c4(min(200_000, n), ss, seed=workloads.C4_STRESS_POOL_SEED, stress=True, pool_mb=8)
+    reqs, plen, reps, alen = workloads.replicate_pool(preqs, len(parena), n)
+    dev = torch.device("cuda", local)
+    d_pool = torch.from_numpy(np.ascontiguousarray(parena)).to(dev)
+    d_arena = torch.zeros(reps * plen + 1024, dtype=torch.uint8, device=dev)
+    for k in range(reps):
+        d_arena[k * plen:k * plen + len(parena)].copy_(d_pool)
+    d_reqs = torch.from_numpy(reqs.view(np.uint8).reshape(-1)).to(dev)
+    d_out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    cap = 4 * n + (1 << 20)
+    d_hits = torch.empty(cap, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        e.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), alen, n, d_out.data_ptr(), d_hits.data_ptr(), cap, s)
+        e.sync(s)
+    steps = max(1, min(args.steps, 5))
+    # warmup: a batch that overflows the stream's WAF buffers is void and grows them (gm_sync)
+    ok, tries = 0, 0
+    while ok < max(1, args.warmup) and tries < 12:
+        tries += 1
+        try:
+            step()
+            ok += 1
+        except engine.GmError as err:
+            if err.code != engine.GM_E_OVERFLOW:
+                raise
+            log(f"[stress] warmup batch overflowed the stream's buffers (grown): {err}")
+    torch.cuda.synchronize()
+    ms = {"route": [], "scan": [], "verify": [], "tail": []}
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+        st = e.stats()
+        for k in ms:
+            ms[k].append(st["last_ms_" + k])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st = e.stats()
+    log(f"[stress] {steps} steps of {n} requests in {dt:.3f}s; candidates {st['last_candidates']}, ctx-pass "
+        f"{st['last_ctx_pass']}, jobs {st['last_jobs']}, hits {st['last_hits']}")
+    return {"workload": "C4 stress: 8000 vocabulary literals (no random tails) + 2000 regexes, 10% without a "
+                        ">= 4-byte factor; benign text with SQL / HTML / shell vocabulary (gpumatch.sigs."
+                        "gen_waf_sigset_stress, records.gen_c4(stress=True))",
+            "requests": n, "value": n * steps / dt, "unit": "requests/s", "ms_per_step": dt / steps * 1e3,
+            "candidates_per_request": st["last_candidates"] / n, "ctx_pass_per_request": st["last_ctx_pass"] / n,
+            "jobs_per_request": st["last_jobs"] / n, "hits_per_request": st["last_hits"] / n,
+            "always_regexes": int(st["n_sig_regex_always"]),
+            "stage_ms": {k: float(np.mean(v)) for k, v in ms.items()}}
 
 
 # The PMC summary of this bench's C4 scan (scripts/pmc.sh on the same tree; bumped with each

@@ -214,7 +214,9 @@ int         gm_load_generation(gm_ctx *ctx, const void *blob, size_t len, uint32
  * intermediate counts -- they stay in device status words).  out[i] receives the verdict of
  * reqs[i]; the hit ids of request i are hit_ids[out[i].first_hit_off .. + n_hits), ascending,
  * requests in order.  gm_sync(ctx, stream) completes the stream's last batch and reports
- * capacity overflow (GM_E_OVERFLOW: the batch's verdicts are void).
+ * capacity overflow (GM_E_OVERFLOW: the batch's verdicts are void; an internal WAF buffer that
+ * overflowed is doubled for the stream's next batch, so a retry of the batch succeeds once the
+ * buffers fit the traffic).
  * Thread-safe per (ctx, stream) pair: each stream has its own scratch buffers, so batches on
  * different streams may be enqueued from different threads and run concurrently.  A scratch
  * buffer that a batch outgrows is replaced after its stream drains (the first large batches).

@@ -997,6 +997,10 @@ struct Scratch {
     unsigned long long *d_jobs = nullptr; size_t cap_jobs = 0;   // unique (request, regex, zone) jobs
     unsigned long long *d_set = nullptr; size_t cap_set = 0;     // dedupe set (power of two)
     uint32_t epoch = 0;                                          // dedupe epoch of the last batch
+    // capacity multipliers: a batch that overflowed a buffer (void, GM_E_OVERFLOW at gm_sync)
+    // doubles it for the stream's next batches -- traffic that passes the prefilter far more
+    // often than the default sizing assumes (e.g. the C4 stress variant) settles after a retry
+    uint32_t cand_mult = 1, surv_mult = 1, list_mult = 1;
     uint32_t *d_cnt = nullptr, *d_start = nullptr; size_t cap_cnt = 0, cap_start = 0;
     uint32_t *d_ccnt = nullptr; size_t cap_ccnt = 0;
     uint8_t *d_temp = nullptr; size_t cap_temp = 0;
@@ -1229,7 +1233,8 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     // truncated silently
     const uint32_t scan_blocks = (uint32_t)c->cu_count;
     const uint32_t W = scan_blocks * SCAN_WAVES;
-    const size_t ccap = 4 * (alen / 64 + 16384), pcap = (size_t)n * 2 + 65536, jcap = (size_t)n + 65536;
+    const size_t ccap = 4 * (alen / 64 + 16384) * S->cand_mult;
+    const size_t pcap = ((size_t)n * 2 + 65536) * S->list_mult, jcap = ((size_t)n + 65536) * S->list_mult;
     size_t set_need = 1;
     while (set_need < 2 * (pcap + jcap)) set_need <<= 1;
     size_t scan_tmp = 0;
@@ -1237,7 +1242,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     if ((e = grow(c, s, S->d_blk2rec, S->cap_blk, nblk))) return e;
     if ((e = grow(c, s, S->d_cand, S->cap_cand, std::max<size_t>(ccap, (size_t)W * 4096)))) return e;
     if ((e = grow(c, s, S->d_ccnt, S->cap_ccnt, W + scan_blocks))) return e;   // scan-wave + ctx-block counts
-    if ((e = grow(c, s, S->d_surv, S->cap_surv, std::min<size_t>(alen / 256 + 65536, 0xFFFFFFFFu)))) return e;
+    if ((e = grow(c, s, S->d_surv, S->cap_surv, std::min<size_t>((alen / 256 + 65536) * S->surv_mult, 0xFFFFFFFFu)))) return e;
     if ((e = grow(c, s, S->d_pairs, S->cap_pairs, pcap))) return e;
     if ((e = grow(c, s, S->d_jobs, S->cap_jobs, jcap))) return e;
     if ((e = grow(c, s, S->d_cnt, S->cap_cnt, (size_t)n + 1))) return e;
@@ -1445,10 +1450,15 @@ int gm_sync(gm_ctx *c, void *stream) {
         }
     }
     const uint32_t ov = S->h_status[3];
+    // the next batch on this stream gets twice the buffer that overflowed (bounded)
+    if ((ov & 4u) && S->cand_mult < 64) S->cand_mult *= 2;
+    if ((ov & 8u) && S->surv_mult < 64) S->surv_mult *= 2;
+    if ((ov & 17u) && S->list_mult < 64) S->list_mult *= 2;
     if (S->h_status[PARSE_STATUS_WORD + 3]) return fail(c, GM_E_OVERFLOW, "gm_parse_requests: arena capacity exceeded");
     if (S->h_status[UPURI_STATUS_WORD]) return fail(c, GM_E_OVERFLOW, "gm_upstream_uris: output capacity exceeded");
     if (ov & 2u) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded");
-    if (ov) return fail(c, GM_E_OVERFLOW, "WAF candidate / survivor / pair / job capacity exceeded");
+    if (ov) return fail(c, GM_E_OVERFLOW, "WAF candidate / survivor / pair / job capacity exceeded "
+                                          "(the stream's buffers are doubled for the next batch: retry it)");
     return GM_OK;
 }
 

@@ -202,10 +202,13 @@ _WORDS = ("the of and to in is it that for on with as was at by be this have fro
           "email address phone items quantity total shipping billing status created updated id").split()
 
 
-def text_pool(rng, size: int) -> np.ndarray:
-    """Benign mixed text (words, JSON-ish and form-encoded fragments), all printable ASCII."""
-    words = np.array(_WORDS)
-    seps = np.array([" ", " ", " ", ", ", ". ", "\": \"", "=", "&", "\n", "_", "-", "/", ":"])
+def text_pool(rng, size: int, vocab=()) -> np.ndarray:
+    """Benign mixed text (words, JSON-ish and form-encoded fragments), all printable ASCII.
+    ``vocab``: extra words drawn as often as all the plain words together (the C4 stress
+    variant's SQL / HTML / shell vocabulary)."""
+    words = np.array(list(_WORDS) + list(vocab) * max(1, len(_WORDS) // max(len(vocab), 1)) if vocab else _WORDS)
+    seps = np.array([" ", " ", " ", ", ", ". ", "\": \"", "=", "&", "\n", "_", "-", "/", ":"] +
+                    (["(", "'", " '", "<", "--"] if vocab else []))
     n = size // 5 + 16
     w = words[rng.integers(0, len(words), n)]
     s = seps[rng.integers(0, len(seps), n)]
@@ -362,11 +365,17 @@ def gen_c2(n: int, seed: int = SEED_BASE + 1):
 
 # --------------------------------------------------------------------------- C4 WAF
 
-def gen_c4(n: int, sigs, seed: int = SEED_BASE + 3, plant_rate: float = 0.01, pool_mb: int = 32):
+def gen_c4(n: int, sigs, seed: int = SEED_BASE + 3, plant_rate: float = 0.01, pool_mb: int = 32,
+           stress: bool = False):
     """C4: cafe host/paths + URI, args, 6-20 headers, body 50% 0 B / 40% U(1,2K) / 10% U(2K,8K);
-    ``plant_rate`` of requests carry one planted signature (rule chosen uniformly)."""
+    ``plant_rate`` of requests carry one planted signature (rule chosen uniformly).  ``stress``:
+    the benign text also speaks SQL / HTML / shell (gpumatch.sigs.VOCAB)."""
     rng = np.random.Generator(np.random.PCG64(seed))
-    tpool = text_pool(rng, pool_mb << 20)
+    if stress:
+        from .sigs import VOCAB
+        tpool = text_pool(rng, pool_mb << 20, VOCAB)
+    else:
+        tpool = text_pool(rng, pool_mb << 20)
     apool = alnum_pool(rng, 1 << 20)
     # TLS traffic: the cafe server redirects plain http (ssl-redirect) before the WAF phase
     https = rng.random(n) < 0.98

@@ -159,3 +159,66 @@ def gen_waf_sigset(n_lit: int = 8000, n_re: int = 2000, seed: int = 0xC0FFEE + 3
         rules.append(Rule("re", nocase, _zones(rng), pat, ex))
     order = rng.permutation(len(rules))
     return SigSet([rules[i] for i in order])
+
+
+# --------------------------------------------------------------------------- C4 stress variant
+# The headline C4 set keeps benign traffic nearly candidate-free (random literal tails, a random
+# required word in every regex).  The stress variant drops both: literals are plain SQL / HTML /
+# shell vocabulary (two or three words) that benign text (records.gen_c4(stress=True)) also
+# speaks, and 10% of the regexes have no >= 4-byte factor, so every (request, zone) runs them
+# (k_waf_always); the other regexes keep the headline's shapes.  The prefilter passes far more
+# windows, the exact stage verifies real matches, and the always-run DFAs carry the load.
+VOCAB = ("select", "from", "where", "union", "insert", "into", "update", "delete", "drop", "table", "order",
+         "group", "by", "having", "limit", "offset", "join", "inner", "outer", "left", "values", "set",
+         "script", "iframe", "img", "src", "href", "onload", "onerror", "onclick", "alert", "document",
+         "cookie", "window", "location", "eval", "function", "return", "var", "const", "style", "div",
+         "span", "form", "input", "button", "action", "method", "post", "get", "http", "https", "www",
+         "admin", "login", "password", "user", "passwd", "shadow", "etc", "bin", "bash", "cat", "echo",
+         "curl", "wget", "exec", "system", "cmd", "shell", "php", "include", "require", "file", "path",
+         "null", "true", "false", "and", "or", "not", "like", "count", "sum", "max", "min", "concat",
+         "char", "sleep", "benchmark", "version", "database", "schema", "information", "columns")
+_JOIN = (" ", "(", "=", "<", "/", "_", "'", " '", "--", ".")
+
+
+def gen_waf_sigset_stress(n_lit: int = 8000, n_re: int = 2000, seed: int = 0xC0FFEE + 13) -> SigSet:
+    rng = np.random.Generator(np.random.PCG64(seed ^ 0x5157))
+    rules, seen = [], set()
+    V = VOCAB
+    while len(rules) < n_lit:
+        k = int(rng.integers(2, 4))
+        parts = [V[int(i)] for i in rng.integers(0, len(V), k)]
+        s = parts[0]
+        for w in parts[1:]:
+            s += _JOIN[int(rng.integers(0, len(_JOIN)))] + w
+        if rng.random() < 0.3:
+            s = _JOIN[int(rng.integers(0, len(_JOIN)))] + s
+        if len(s) < 4 or len(s) > 32 or s in seen:
+            continue
+        seen.add(s)
+        nocase = rng.random() < 0.7
+        b = s.encode()
+        rules.append(Rule("lit", nocase, _zones(rng), b, b.upper() if nocase and rng.random() < 0.5 else b))
+    n_always = n_re // 10
+    for i in range(n_re):
+        nocase = rng.random() < 0.5
+        if i < n_always:   # no >= 4-byte factor: every (request, zone) runs it (k_waf_always)
+            t = int(rng.integers(0, 4))
+            k = int(rng.integers(2, 6))
+            a2 = "".join(chr(97 + int(x)) for x in rng.integers(0, 26, 2))
+            b2 = "".join(chr(97 + int(x)) for x in rng.integers(0, 26, 2))
+            if t == 0:
+                pat, ex = f"[0-9]{{{k},}}[a-f]x", "9" * k + "ax"
+            elif t == 1:
+                pat, ex = f"({a2}|{b2})[0-9]{{{k}}}--", a2 + "7" * k + "--"
+            elif t == 2:
+                pat, ex = f"=\\s*[0-9]{{{k}}}'\\s*or", "= " + "4" * k + "' or"
+            else:
+                pat, ex = f"<[a-z]{{1,3}}\\s+{a2}[a-z]{{{k}}}=", "<b " + a2 + "q" * k + "="
+            if nocase:
+                ex = ex.upper()
+            rules.append(Rule("re", nocase, _zones(rng), pat, ex.encode()))
+        else:
+            pat, ex = _regex_rule(rng, nocase)
+            rules.append(Rule("re", nocase, _zones(rng), pat, ex))
+    order = rng.permutation(len(rules))
+    return SigSet([rules[i] for i in order])

@@ -76,11 +76,11 @@ def c2_blob() -> bytes:
     return blob.make_blob(confgen.render_main(), files)
 
 
-def c4_sample(sigset: sigs.SigSet, n: int = 2000, seed: int = records.SEED_BASE + 33) -> bytes:
+def c4_sample(sigset: sigs.SigSet, n: int = 2000, seed: int = records.SEED_BASE + 33, stress: bool = False) -> bytes:
     """A benign traffic sample for the WAF prefilter tuning (GM_ENTRY_SAMPLE): C4 requests from a
     seed disjoint from every pool the tests and the bench match (a deployment samples its own
     recent traffic the same way); the zone bytes only."""
-    reqs, arena = records.gen_c4(n, sigset, seed=seed, plant_rate=0.0, pool_mb=2)
+    reqs, arena = records.gen_c4(n, sigset, seed=seed, plant_rate=0.0, pool_mb=2, stress=stress)
     parts = []
     for r in reqs:
         b = int(r["base"])
@@ -351,3 +351,14 @@ def gen_c3(n: int, regexes=None, seed: int = records.SEED_BASE + 2, pool: int = 
               "host": [records.const_seg(C3_HOST, n)],
               "method": [records.const_seg("GET", n)]}
     return records.build(n, fields, np.full(n, 80), np.zeros(n, dtype=np.int64))
+
+
+C4_STRESS_POOL_SEED = records.SEED_BASE + 23
+
+
+def c4_stress_generation():
+    """The C4 stress variant: gpumatch.sigs.gen_waf_sigset_stress on the same
+    cafe Ingress (wallarm_mode block), traffic from records.gen_c4(stress=True)."""
+    ss = sigs.gen_waf_sigset_stress()
+    smp = c4_sample(ss, seed=records.SEED_BASE + 43, stress=True)
+    return ss, c4_blob(ss, sample=smp)

@@ -70,6 +70,19 @@ def test_c4_waf_parity_10k_rules(eng, sample):
     assert (exp["action"] == 6).sum() > 100
 
 
+def test_c4_stress_variant_parity(eng):
+    """The C4 stress variant (workloads.c4_stress_generation): vocabulary literals that benign
+    traffic speaks, 10% factorless (always-run) regexes, SQL / HTML text -- 6000 requests
+    against the oracle."""
+    ss, b = workloads.c4_stress_generation()
+    reqs, arena = records.gen_c4(6_000, ss, seed=workloads.C4_STRESS_POOL_SEED, plant_rate=0.05, stress=True)
+    got, gh, exp, eh = run_both(eng, b, reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "C4-stress")
+    assert (exp["n_hits"] > 0).mean() > 0.2
+    st = eng.stats()
+    assert st["n_sig_regex_always"] == 200 and st["last_candidates"] > 10 * len(reqs)
+
+
 def test_waf_edge_cases(eng):
     rules = [sigs.Rule("lit", True, "uahb", b"evil"), sigs.Rule("lit", False, "b", b"CaseSensitive"),
              sigs.Rule("lit", True, "u", b"/tea/x"), sigs.Rule("re", True, "ah", r"sel\s*ect\d+"),
