@@ -1668,6 +1668,30 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.n_dfas = (uint32_t)C.dfas.size();
     h.n_lit_buckets_cap = lcap; h.n_lits = (uint32_t)dlits.size(); h.n_sig_regex = (uint32_t)sregex.size();
     h.n_always = (uint32_t)always.size(); h.n_sigs = st.n_sigs;
+    // the LDS pack of the always-run regexes (a prefix of `always` that fits ALWAYS_LDS_BYTES)
+    std::vector<DAlw> alw;
+    std::vector<uint8_t> alw_pack;
+    for (uint32_t ridx : always) {
+        const DSigRegex &sr = sregex[ridx];
+        const DDfa &d = C.dfas[sr.dfa];
+        const size_t tr_bytes = (size_t)d.n_states * d.n_classes * 2;
+        const size_t need = 256 + ((tr_bytes + 15) & ~size_t(15));
+        if (alw_pack.size() + need > ALWAYS_LDS_BYTES) break;
+        DAlw a{};
+        a.cls_off = (uint32_t)alw_pack.size();
+        alw_pack.insert(alw_pack.end(), C.dfa_cls.begin() + d.cls_off, C.dfa_cls.begin() + d.cls_off + 256);
+        a.tr_off = (uint32_t)alw_pack.size();
+        const uint8_t *tb = reinterpret_cast<const uint8_t *>(C.dfa_trans.data() + d.trans_off);
+        alw_pack.insert(alw_pack.end(), tb, tb + tr_bytes);
+        alw_pack.resize(a.cls_off + need, 0);
+        a.n_classes = d.n_classes;
+        a.acc1 = C.dfa_acc[d.acc_off + 1];
+        a.rule = sr.rule;
+        a.zones = sr.zones;
+        alw.push_back(a);
+    }
+    h.n_always_lds = (uint32_t)alw.size();
+    h.alw_pack_len = (uint32_t)alw_pack.size();
     // the route's hot tables first, contiguous (k_route stages them into LDS when they fit)
     h.off_ports = I.put(ports);
     h.off_names = I.put(tab_exact); h.off_wild_head = I.put(tab_head); h.off_wild_tail = I.put(tab_tail);
@@ -1686,6 +1710,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_waf_a = I.put(waf_a); h.off_waf_b = I.put(waf_b);
     h.off_lit_buckets = I.put(ltab); h.off_lits = I.put(dlits); h.off_sig_regex = I.put(sregex);
     h.off_always = I.put(always);
+    h.off_alw = I.put(alw); h.off_alw_pack = I.put(alw_pack);
     h.n_rk_cap = rkcap; h.n_rk_ids = (uint32_t)rk_ids.size(); h.n_rk_ents_keys = (uint32_t)rk_lists.size();
     h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_rk_ents = I.put(rk_ents); h.off_rk_bloom = I.put(rk_bloom);
     h.n_ups = (uint32_t)dups.size(); h.n_peers = (uint32_t)peer_init.size();
@@ -1754,6 +1779,9 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.n_ups = h.n_ups; t.n_peers = h.n_peers;
     t.loc_uri = (const DLocUri *)(b + h.off_loc_uri);
     t.decoders = h.decoders;
+    t.alw = (const DAlw *)(b + h.off_alw);
+    t.alw_pack = b + h.off_alw_pack;
+    t.n_always_lds = h.n_always_lds; t.alw_pack_len = h.alw_pack_len;
     t.n_ports = h.n_ports;
     t.names_mask = h.n_names_cap - 1; t.wild_head_mask = h.n_wild_head_cap - 1; t.wild_tail_mask = h.n_wild_tail_cap - 1;
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;

@@ -1126,6 +1126,10 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SCAN_LDS_BYTES) != hipSuccess) {
                 t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
             }
+        if (hipFuncSetAttribute((const void *)k_waf_always_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)ALWAYS_LDS_BYTES) != hipSuccess) {
+            t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
+        }
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
             c->cu_count = cus;
@@ -1320,8 +1324,14 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
                                                                (uint32_t)S->cap_pairs, dd);
         HIPCHK(c, hipGetLastError());
     }
-    if (t.n_always) {
-        k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(A, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, false);
+    if (t.n_always_lds) {
+        k_waf_always_lds<<<(uint32_t)c->cu_count, 1024, t.alw_pack_len, s>>>(A, alen, reqs, n, t, S->d_pairs,
+                                                                             (uint32_t)S->cap_pairs, dd, false, dlen);
+        HIPCHK(c, hipGetLastError());
+    }
+    if (t.n_always > t.n_always_lds) {
+        k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(A, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, false,
+                                                               t.n_always_lds);
         HIPCHK(c, hipGetLastError());
     }
     if (t.decoders) {
@@ -1367,8 +1377,14 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
                                                                    (uint32_t)S->cap_pairs, dd2);
             HIPCHK(c, hipGetLastError());
         }
-        if (t.n_always) {
-            k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(SA, SR, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd2, true);
+        if (t.n_always_lds) {
+            k_waf_always_lds<<<(uint32_t)c->cu_count, 1024, t.alw_pack_len, s>>>(SA, scap, SR, n, t, S->d_pairs,
+                                                                                 (uint32_t)S->cap_pairs, dd2, true, slen);
+            HIPCHK(c, hipGetLastError());
+        }
+        if (t.n_always > t.n_always_lds) {
+            k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(SA, SR, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd2, true,
+                                                                   t.n_always_lds);
             HIPCHK(c, hipGetLastError());
         }
     }

@@ -251,6 +251,18 @@ __host__ __device__ inline uint32_t peer_draw(uint64_t lo, uint64_t hi, uint32_t
     return (uint32_t)(x >> 32);
 }
 
+// Always-run signature regexes (RXM_ALWAYS, no >= 4-byte factor) whose DFAs fit together in LDS:
+// k_waf_always_lds stages the pack once per workgroup and runs a wave per request with a lane per
+// regex -- the zone's bytes are read once per 64 regexes and every transition is an LDS read.
+// Pack: per regex its 256-byte class map, then its transitions (u16, as dfa_trans), 16-B aligned.
+constexpr uint32_t ALWAYS_LDS_BYTES = 96 * 1024;
+struct DAlw {
+    uint32_t cls_off, tr_off;   // byte offsets in the pack
+    uint16_t n_classes, acc1;   // acc1: the start state's accept flags
+    uint32_t rule;
+    uint32_t zones;
+};
+
 struct TabHeader {
     uint32_t magic, version;
     uint32_t n_ports, n_names_cap, n_wild_head_cap, n_wild_tail_cap;
@@ -278,6 +290,8 @@ struct TabHeader {
     uint64_t off_ups, off_key_parts, off_points, off_peer_init;   // peer_init: u32 GM_PEER_DOWN per peer
     uint64_t off_loc_uri;          // DLocUri per location
     uint32_t decoders, pad_dec;    // the signature set's request parsers (DEC_*)
+    uint32_t n_always_lds, alw_pack_len;   // always[0, n_always_lds) are in the LDS pack
+    uint64_t off_alw, off_alw_pack;
 };
 // The route's hot tables -- ports, the three name tables, servers, server ifs, small-location
 // lists, locations and the name strings -- are laid out first and contiguously in the image;
@@ -302,6 +316,7 @@ struct GTab {                // device pointers, built on host from the image ba
     uint32_t n_ups, n_peers;
     const DLocUri *loc_uri;
     uint32_t decoders;
+    const DAlw *alw; const uint8_t *alw_pack; uint32_t n_always_lds, alw_pack_len;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
     uint32_t gen;
