@@ -345,19 +345,46 @@ __device__ bool dfa_run_bytes(const GTab &t, uint32_t dfa_id, const uint8_t *p, 
 // always list with dfa GM_NONE and "match" when reached.  Out of line: the route fast path
 // keeps its registers.
 constexpr int RK_K = 8;
+#ifndef GM_EXP_WPE
+#define GM_EXP_WPE 3
+#endif
+#ifndef GM_EXP_GRIDMUL
+#define GM_EXP_GRIDMUL 8
+#endif
+#ifdef GM_EXP_COUNT
+__device__ unsigned long long g_exp[8];
+#endif
 __device__ __noinline__ int32_t rloc_prefiltered(const GTab &t, const DServer &S, uint32_t sid, const uint8_t *u,
                                                  uint32_t ulen, const uint32_t *rkb) {
     auto run = [&](uint32_t k) -> bool {
         const DRegexLoc rl = t.rlocs[S.first_rloc + k];
+#ifdef GM_EXP_NO_DFA
+        return true;
+#endif
+#ifdef GM_EXP_COUNT
+        uint32_t steps = 0;
+        const uint64_t t0 = __builtin_readcyclecounter();
+        const bool m = rl.dfa == GM_NONE || dfa_run_bytes(t, rl.dfa, u, ulen, &steps);
+        atomicAdd(&g_exp[1], 1ull); atomicAdd(&g_exp[2], (unsigned long long)steps);
+        atomicAdd(&g_exp[3], (unsigned long long)(__builtin_readcyclecounter() - t0));
+        return m;
+#endif
         return rl.dfa == GM_NONE || dfa_run_bytes(t, rl.dfa, u, ulen);
     };
+#ifdef GM_EXP_COUNT
+    atomicAdd(&g_exp[0], 1ull);
+#endif
     uint32_t lo = 0, ai = 0;
     for (;;) {
         uint32_t c[RK_K];
 #pragma unroll
         for (int j = 0; j < RK_K; j++) c[j] = GM_NONE;
         uint32_t w = 0;
-        for (uint32_t i = 0; i < ulen; i++) {
+        uint32_t scan_len = ulen;
+#ifdef GM_EXP_NO_COLLECT
+        scan_len = 0;
+#endif
+        for (uint32_t i = 0; i < scan_len; i++) {
             w = (w >> 8) | ((uint32_t)u[i] << 24);
             if (i < 3) continue;
             const uint32_t key = fold4(w);
@@ -410,6 +437,14 @@ __device__ __noinline__ int32_t rloc_prefiltered(const GTab &t, const DServer &S
 // order whose DFA matches the URI (-1: none).  Out of line, like the other rarely taken steps.
 __device__ __noinline__ int32_t rloc_first_match(const GTab &t, const DServer &S, uint32_t sid, const uint8_t *u,
                                                  uint32_t ulen, const uint32_t *rkb) {
+#ifdef GM_EXP_COUNT
+    if (S.rk_on) {
+        const uint64_t t0 = __builtin_readcyclecounter();
+        const int32_t r = rloc_prefiltered(t, S, sid, u, ulen, rkb);
+        atomicAdd(&g_exp[4], (unsigned long long)(__builtin_readcyclecounter() - t0));
+        return r;
+    }
+#endif
     if (S.rk_on) return rloc_prefiltered(t, S, sid, u, ulen, rkb);
     for (uint32_t k = 0; k < S.n_rloc; k++) {
         const DRegexLoc rl = t.rlocs[S.first_rloc + k];
@@ -712,8 +747,17 @@ __device__ __forceinline__ void route_prefetch(const uint8_t *A, uint64_t alen, 
     load_span_n(A, f_uri, alen, min(r.uri_len, 32u), p.uw);
 }
 
+// k_rloc's tile shape: URIs up to RLOC_URI_CAP bytes staged in LDS, candidate bitmaps of
+// RLOC_BM_BITS regex locations (longer URIs / larger servers run rloc_prefiltered in the lane)
+constexpr uint32_t RLOC_URI_CAP = 256, RLOC_BM_BITS = 2048;
+constexpr uint32_t RLOC_STATUS_WORD = 16;   // batch status word: requests deferred to k_rloc
+// rk_in: RK_INLINE -- a prefiltered regex step runs here; RK_DEFER -- one that k_rloc can take
+// (URI <= RLOC_URI_CAP, n_rloc <= RLOC_BM_BITS) sets *pend and returns; >= -1 -- k_rloc's answer
+// (the location index, -1 none).  *sid_out: the server chosen (valid whenever *pend is set).
+constexpr int32_t RK_INLINE = -3, RK_DEFER = -2;
 __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const RoutePre &pre,
-                          const GTab &t, RouteOut &o, const uint32_t *rkb) {
+                          const GTab &t, RouteOut &o, const uint32_t *rkb, int32_t rk_in = RK_INLINE,
+                          bool *pend = nullptr) {
     o.server = GM_NONE; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0;
     o.action = GM_ACT_NO_LISTENER; o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF;
     const uint64_t f_uri = r.base, f_host = r.base + r.uri_len + r.args_len + r.hdr_len + r.body_len;
@@ -827,7 +871,11 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
     if (loc < 0) {
         if (best >= 0 && t.locs[best].noregex) loc = best;
         else {
-            loc = rloc_first_match(t, S, sid, u, r.uri_len, rkb);
+            if (S.rk_on && rk_in >= -1) loc = rk_in;
+            else if (S.rk_on && rk_in == RK_DEFER && r.uri_len <= RLOC_URI_CAP && S.n_rloc <= RLOC_BM_BITS) {
+                *pend = true;
+                return;
+            } else loc = rloc_first_match(t, S, sid, u, r.uri_len, rkb);
             if (loc < 0) loc = best;
         }
     }
@@ -869,14 +917,18 @@ constexpr uint32_t LDS_HIST_MAX = 512;
 
 // WPE: waves per SIMD the register allocation targets (beside the scan's workgroup, a CU has
 // room for route waves only when they are small)
-template <int WPE, bool RK = false>
+// RK: the generation has prefiltered regex locations -- their step is deferred to k_rloc when
+// q.list is set (requests appended to q.list as {index, server}); TAIL: the second pass over
+// q.list, finishing each deferred request with k_rloc's location (q.loc).
+struct RlocQ { uint2 *list; uint32_t *count; int32_t *loc; };
+template <int WPE, bool RK = false, bool TAIL = false>
 __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_route(const gm_req *__restrict__ reqs, uint32_t n,
                                                        const uint8_t *__restrict__ A, uint64_t arena_len,
                                                        GTab tg, gm_verdict *__restrict__ out,
                                                        unsigned long long *__restrict__ counters,
                                                        uint32_t *__restrict__ blk2rec, uint32_t nblk,
                                                        uint32_t *__restrict__ hcnt, int prio,
-                                                       const uint64_t *__restrict__ dlen) {
+                                                       const uint64_t *__restrict__ dlen, RlocQ q = RlocQ{}) {
     if (dlen) arena_len = *dlen;   // gm_batch.arena_len_dev: the length a producer wrote on the device
     // beside the WAF scan: issue priority over the scan's waves, so the route's short
     // latency-bound waves finish early instead of stretching past the scan (GM_ROUTE_PRIO)
@@ -907,12 +959,27 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
     __shared__ uint32_t rkb[RK ? RK_BLOOM_WORDS : 1];
     if (RK) for (uint32_t k = threadIdx.x; k < RK_BLOOM_WORDS; k += blockDim.x) rkb[k] = t.rk_bloom[k];
     __syncthreads();
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t nn = TAIL ? *q.count : n;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nn; x += gridDim.x * blockDim.x) {
+        const uint32_t i = TAIL ? q.list[x].x : x;
         const Rec r = load_rec(reqs + i);
         RoutePre pre;
         route_prefetch(A, arena_len, r, pre);
         RouteOut o;
-        route_one(A, arena_len, reqs + i, r, pre, t, o, RK ? rkb : nullptr);
+        bool pend = false;
+        route_one(A, arena_len, reqs + i, r, pre, t, o, RK ? rkb : nullptr,
+                  TAIL ? q.loc[x] : (RK && q.list ? RK_DEFER : RK_INLINE), &pend);
+        if (RK && !TAIL) {   // deferred to k_rloc: appended, one atomic per wave
+            const unsigned long long pm = __ballot(pend);
+            if (pm) {
+                const uint32_t lane = threadIdx.x & 63;
+                const int leader = __ffsll(pm) - 1;
+                uint32_t b = 0;
+                if (lane == (uint32_t)leader) b = atomicAdd(q.count, (uint32_t)__popcll(pm));
+                b = __shfl(b, leader);
+                if (pend) q.list[b + (uint32_t)__popcll(pm & ((1ull << lane) - 1))] = make_uint2(i, o.server);
+            }
+        }
         uint4 w0, w1;
         w0.x = t.gen; w0.y = o.server; w0.z = o.loc; w0.w = o.ups;
         w1.x = (uint32_t)o.action | ((uint32_t)o.kind << 8) | ((uint32_t)o.bucket << 16) | ((uint32_t)o.match << 24);
@@ -920,7 +987,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
         w1.z = 0;                 // first_hit_off
         w1.w = o.status;
         uint4 *dst = reinterpret_cast<uint4 *>(out + i);
-        dst[0] = w0; dst[1] = w1;
+        if (!pend) { dst[0] = w0; dst[1] = w1; }
         // per-location counter, aggregated over the wave: one atomic per distinct location
         unsigned long long todo = __ballot(o.loc != GM_NONE);
         while (todo) {
@@ -933,6 +1000,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
             }
             todo &= ~same;
         }
+        if (TAIL) continue;
         if (hcnt) {   // the WAF stages' per-request hit counts start the batch at zero
             hcnt[i] = 0;
             if (i + 1 == n) hcnt[n] = 0;
@@ -954,6 +1022,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
     }
 }
 
+#include "gm_rloc.inc"
 #include "gm_waf.inc"
 #include "gm_decode.inc"
 
@@ -1019,13 +1088,15 @@ struct Scratch {
     uint64_t *d_ssize = nullptr, *d_sbase = nullptr; size_t cap_ssize = 0, cap_sbase = 0;
     uint8_t *d_stemp = nullptr; size_t cap_stemp = 0;
     uint8_t *d_utemp = nullptr; size_t cap_utemp = 0;
+    uint2 *d_rq = nullptr; size_t cap_rq = 0;            // regex-location requests deferred to k_rloc
+    int32_t *d_rql = nullptr; size_t cap_rql = 0;        // and k_rloc's locations
     ~Scratch() {
         for (void *p : {(void *)d_status, (void *)d_blk2rec, (void *)d_cand, (void *)d_surv, (void *)d_pairs,
                         (void *)d_jobs, (void *)d_set, (void *)d_cnt, (void *)d_start, (void *)d_ccnt,
                         (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp,
                         (void *)d_pk, (void *)d_pseg, (void *)d_pprog, (void *)d_ppat, (void *)d_ptemp,
                         (void *)d_usize, (void *)d_utemp, (void *)d_sreqs, (void *)d_sarena, (void *)d_sblk,
-                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp})
+                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
         for (auto &e : ev) if (e) (void)hipEventDestroy(e);
@@ -1109,6 +1180,14 @@ static Scratch *scratch_for(gm_ctx *c, hipStream_t stream) {
     return p;
 }
 
+#ifdef GM_EXP_COUNT
+extern "C" int gm_exp_read(unsigned long long *out) {
+    hipMemcpyFromSymbol(out, HIP_SYMBOL(g_exp), sizeof(unsigned long long) * 8);
+    unsigned long long z[8] = {};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_exp), z, sizeof z);
+    return 0;
+}
+#endif
 extern "C" {
 
 uint32_t gm_abi_version(void) { return GM_ABI_VERSION; }
@@ -1222,12 +1301,31 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     HIPCHK(c, hipMemsetAsync(S->d_status, 0, BATCH_STATUS_WORDS * 4, s));
     if (mark(0)) return GM_E_HIP;
     const uint32_t route_blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
-                                                                           (uint32_t)c->cu_count * 8));
+                                                                           (uint32_t)c->cu_count * GM_EXP_GRIDMUL));
     unsigned long long *ctr = g->d_counters;
+    // prefiltered regex locations: k_route defers their step to k_rloc (a tile of requests per
+    // workgroup, gm_rloc.inc) and a second k_route pass over the deferred list finishes them
+    RlocQ q{};
+    if (t.rk_keys) {
+        int e2;
+        if ((e2 = grow(c, s, S->d_rq, S->cap_rq, n)) || (e2 = grow(c, s, S->d_rql, S->cap_rql, n))) return e2;
+        q = RlocQ{S->d_rq, S->d_status + RLOC_STATUS_WORD, S->d_rql};
+    }
+    auto launch_rloc = [&](hipStream_t rs, uint32_t tail_blocks) -> int {
+        k_rloc<<<(uint32_t)c->cu_count * 4, RLOC_BLOCK, 0, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen);
+        k_route<3, true, true><<<tail_blocks, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk,
+                                                                    nullptr, 0, dlen, q);
+        HIPCHK(c, hipGetLastError());
+        return GM_OK;
+    };
     if (!waf) {
-        if (t.rk_keys) k_route<3, true><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen);
+        if (t.rk_keys) k_route<3, true><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, q);
         else k_route<3><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen);
         HIPCHK(c, hipGetLastError());
+        if (t.rk_keys) {
+            const int e4 = launch_rloc(s, route_blocks);
+            if (e4) return e4;
+        }
         return mark(1) ? GM_E_HIP : GM_OK;
     }
     int e;
@@ -1287,10 +1385,12 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         // raised issue priority beside the scan: the route's short latency-bound waves finish
         // early instead of stretching past the scan
         if (t.rk_keys)
-            k_route<5, true><<<nb, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1, dlen);
+            k_route<5, true><<<nb, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1, dlen, q);
         else
             k_route<5><<<nb, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1, dlen);
         HIPCHK(c, hipGetLastError());
+        int e3;
+        if (t.rk_keys && (e3 = launch_rloc(rs, nb))) return e3;
         if (prof) HIPCHK(c, hipEventRecord(S->ev_route[1], rs));
         if (!serial) HIPCHK(c, hipEventRecord(S->ev_join, rs));
         S->route_side = true;

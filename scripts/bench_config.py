@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
     import torch
     from gpumatch import engine, workloads
@@ -86,6 +87,20 @@ def main():
             ms.append(eng.stats()["last_ms_route"])
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        rt = float(np.mean(ms))
+        try:
+            import ctypes
+            fn = ctypes.CDLL(engine.LIB_PATH).gm_exp_read
+            ex = (ctypes.c_ulonglong * 8)()
+            fn(ex)
+            print("exp counters (steps+warmup)", list(ex), flush=True)
+        except (AttributeError, OSError):
+            pass
+        if args.no_cpu:
+            print(json.dumps({"config": cfg, "requests": n, "ms_per_step": dt / args.steps * 1e3,
+                              "route_kernel_ms": rt, "value": n * args.steps / dt}), flush=True)
+            del d_arena, d_reqs, d_out, d_hits, d_pool, eng
+            continue
         # CPU oracle on a bounded sample of the pool
         cores = min(os.cpu_count() or 1, 16)
         o = Oracle(blob, 1)
