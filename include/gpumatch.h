@@ -183,6 +183,9 @@ typedef struct gm_stats_t {
     uint32_t n_peers;             /* upstream `server` peers: gm_peer_state entries     */
     uint32_t n_upstreams_deferred;/* upstreams whose balancing the engine leaves to nginx */
     uint32_t decoders;            /* request parsers the signature set runs (GM_DEC_*)  */
+    /* always-run regexes: union-DFA groups (one pass over a zone answers a group), their states,
+     * the LDS slices they are run in, and regexes left to the per-regex kernel (too big alone) */
+    uint32_t n_alw_groups, n_alw_states, n_alw_slices, n_alw_single;
 } gm_stats_t;
 
 /* Request parsers (Wallarm's) a signature set can declare ("@decoders" line of

@@ -1545,6 +1545,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     std::vector<LitE> lits;
     std::vector<DSigRegex> sregex;
     std::vector<uint32_t> always;
+    std::vector<Dfa> always_dfa;   // the always regexes' search DFAs (union groups, below)
+    std::vector<std::string> always_pat;
     // one prefilter pattern -> its key windows (stride-2 scan, see choose_keys)
     std::unordered_map<uint32_t, uint32_t> key_use;
     auto add_lit = [&](const std::string &pat, const std::string &bytes, uint32_t id, uint8_t flags, uint8_t zones,
@@ -1582,6 +1584,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             } else if (ri.min_factor < 4) {
                 sr.mode = RXM_ALWAYS;
                 always.push_back(ridx);
+                always_dfa.push_back(ri.dfa);
+                always_pat.push_back(g.pat);
                 st.n_sig_regex_always++;
             } else {
                 for (auto &f : ri.factors)
@@ -1668,30 +1672,114 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.n_dfas = (uint32_t)C.dfas.size();
     h.n_lit_buckets_cap = lcap; h.n_lits = (uint32_t)dlits.size(); h.n_sig_regex = (uint32_t)sregex.size();
     h.n_always = (uint32_t)always.size(); h.n_sigs = st.n_sigs;
-    // the LDS pack of the always-run regexes (a prefix of `always` that fits ALWAYS_LDS_BYTES)
-    std::vector<DAlw> alw;
+    // the always-run regexes in union-DFA groups.  Ordered by (zone set, pattern text) -- the
+    // same shapes side by side, whose unions stay small -- a regex joins the open group while the
+    // minimised union's tables stay within ALW_GROUP_BYTES (and ALW_GROUP_MAX members, one zone
+    // set); a regex whose DFA cannot form a group even alone stays with the per-regex kernel.
+    // Groups are then packed into LDS slices.  `always` is reordered: grouped regexes first (group
+    // order), then the rest.
+    std::vector<DAlwGroup> alw;
+    std::vector<DAlwSlice> alw_slices;
     std::vector<uint8_t> alw_pack;
-    for (uint32_t ridx : always) {
-        const DSigRegex &sr = sregex[ridx];
-        const DDfa &d = C.dfas[sr.dfa];
-        const size_t tr_bytes = (size_t)d.n_states * d.n_classes * 2;
-        const size_t need = 256 + ((tr_bytes + 15) & ~size_t(15));
-        if (alw_pack.size() + need > ALWAYS_LDS_BYTES) break;
-        DAlw a{};
-        a.cls_off = (uint32_t)alw_pack.size();
-        alw_pack.insert(alw_pack.end(), C.dfa_cls.begin() + d.cls_off, C.dfa_cls.begin() + d.cls_off + 256);
-        a.tr_off = (uint32_t)alw_pack.size();
-        const uint8_t *tb = reinterpret_cast<const uint8_t *>(C.dfa_trans.data() + d.trans_off);
-        alw_pack.insert(alw_pack.end(), tb, tb + tr_bytes);
-        alw_pack.resize(a.cls_off + need, 0);
-        a.n_classes = d.n_classes;
-        a.acc1 = C.dfa_acc[d.acc_off + 1];
-        a.rule = sr.rule;
-        a.zones = sr.zones;
-        alw.push_back(a);
+    std::vector<uint32_t> alw_rule, always_grouped, always_single;
+    {
+        std::vector<uint32_t> ord(always.size());
+        for (uint32_t i = 0; i < ord.size(); i++) ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+            const uint16_t zx = sregex[always[x]].zones, zy = sregex[always[y]].zones;
+            return zx != zy ? zx < zy : always_pat[x] < always_pat[y];
+        });
+        auto tab_bytes = [](const MultiDfa &m) {   // the group's rows (gm_tables.hpp DAlwGroup)
+            return (size_t)m.n_states * ((size_t)m.n_classes + (m.n_classes & 1) + 4) * 2;
+        };
+        std::vector<std::vector<uint32_t>> gmem;   // members (indices into always)
+        std::vector<MultiDfa> gdfa;
+        std::vector<uint32_t> cur;
+        MultiDfa cur_m;
+        auto close = [&]() {
+            if (!cur.empty()) { gmem.push_back(cur); gdfa.push_back(std::move(cur_m)); }
+            cur.clear();
+        };
+        for (uint32_t x : ord) {
+            const uint16_t zx = sregex[always[x]].zones;
+            if (!cur.empty() && sregex[always[cur[0]]].zones == zx && cur.size() < ALW_GROUP_MAX) {
+                std::vector<const Dfa *> comps;
+                for (uint32_t y : cur) comps.push_back(&always_dfa[y]);
+                comps.push_back(&always_dfa[x]);
+                MultiDfa m;
+                if (build_multi(comps, (int)ALW_BUILD_STATES, m) && tab_bytes(m) <= ALW_GROUP_BYTES) {
+                    cur.push_back(x); cur_m = std::move(m); continue;
+                }
+            }
+            close();
+            MultiDfa m;
+            std::vector<const Dfa *> one{&always_dfa[x]};
+            if (build_multi(one, (int)ALW_BUILD_STATES, m) &&
+                tab_bytes(m) <= ALW_GROUP_BYTES) { cur.push_back(x); cur_m = std::move(m); }
+            else always_single.push_back(always[x]);
+        }
+        close();
+        // slices: consecutive groups, <= ALW_SLICE_GROUPS of them within ALWAYS_LDS_BYTES
+        auto pad16 = [&]() { alw_pack.resize((alw_pack.size() + 15) & ~size_t(15), 0); };
+        for (size_t g0 = 0; g0 < gmem.size();) {
+            size_t g1 = g0, bytes = 1024;
+            while (g1 < gmem.size() && g1 - g0 < ALW_SLICE_GROUPS && bytes + tab_bytes(gdfa[g1]) + 16 <= ALWAYS_LDS_BYTES)
+                bytes += tab_bytes(gdfa[g1++]) + 16;
+            DAlwSlice sl{};
+            sl.off = (uint32_t)alw_pack.size();
+            sl.first_group = (uint32_t)alw.size();
+            sl.n_groups = (uint32_t)(g1 - g0);
+            std::vector<uint32_t> clsq(256, 0);
+            for (size_t j = g0; j < g1; j++)
+                for (int b = 0; b < 256; b++) clsq[b] |= (uint32_t)gdfa[j].cls[b] << (8 * (j - g0));
+            const uint8_t *cb = reinterpret_cast<const uint8_t *>(clsq.data());
+            alw_pack.insert(alw_pack.end(), cb, cb + 1024);
+            for (size_t j = g0; j < g1; j++) {
+                const MultiDfa &m = gdfa[j];
+                const size_t S = (size_t)m.n_states, Cn = (size_t)m.n_classes, Cp = Cn + (Cn & 1), R = Cp + 4;
+                DAlwGroup g{};
+                g.tr_off = (uint32_t)(alw_pack.size() - sl.off);
+                g.mask_off = (uint32_t)(2 * Cp);
+                g.start_row = (uint32_t)(2 * R);
+                std::vector<uint16_t> rows(S * R, 0);
+                for (size_t q = 1; q < S; q++) {
+                    for (size_t c = 0; c < Cn; c++) {
+                        const uint16_t e = m.trans[q * Cn + c];
+                        rows[q * R + c] = (uint16_t)(2 * R * (e & 0x3FFF) | ((e & MDFA_EMIT) ? ALW_EMIT : 0));
+                    }
+                    rows[q * R + Cp] = (uint16_t)m.emit[q]; rows[q * R + Cp + 1] = (uint16_t)(m.emit[q] >> 16);
+                    rows[q * R + Cp + 2] = (uint16_t)m.endm[q]; rows[q * R + Cp + 3] = (uint16_t)(m.endm[q] >> 16);
+                }
+                const uint8_t *rb = reinterpret_cast<const uint8_t *>(rows.data());
+                alw_pack.insert(alw_pack.end(), rb, rb + rows.size() * 2);
+                pad16();
+                g.n_classes = (uint32_t)Cn; g.n_states = (uint32_t)S;
+                g.first = (uint32_t)alw_rule.size();
+                for (size_t k = 0; k < gmem[j].size(); k++) {
+                    const DSigRegex &sr = sregex[always[gmem[j][k]]];
+                    alw_rule.push_back(sr.rule);
+                    always_grouped.push_back(always[gmem[j][k]]);
+                    for (uint32_t z = 0; z < 4; z++)
+                        if (sr.zones & (1u << z)) g.zone_mask[z] |= 1u << k;
+                    g.zones |= sr.zones;
+                }
+                sl.zones |= g.zones;
+                st.n_alw_states += (uint32_t)S;
+                alw.push_back(g);
+            }
+            sl.len = (uint32_t)(alw_pack.size() - sl.off);
+            alw_slices.push_back(sl);
+            g0 = g1;
+        }
     }
-    h.n_always_lds = (uint32_t)alw.size();
+    h.n_always_lds = (uint32_t)always_grouped.size();
+    h.n_alw_groups = (uint32_t)alw.size();
+    h.n_alw_slices = (uint32_t)alw_slices.size();
     h.alw_pack_len = (uint32_t)alw_pack.size();
+    st.n_alw_groups = h.n_alw_groups; st.n_alw_slices = h.n_alw_slices;
+    st.n_alw_single = (uint32_t)always_single.size();
+    always = always_grouped;
+    always.insert(always.end(), always_single.begin(), always_single.end());
     // the route's hot tables first, contiguous (k_route stages them into LDS when they fit)
     h.off_ports = I.put(ports);
     h.off_names = I.put(tab_exact); h.off_wild_head = I.put(tab_head); h.off_wild_tail = I.put(tab_tail);
@@ -1710,7 +1798,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_waf_a = I.put(waf_a); h.off_waf_b = I.put(waf_b);
     h.off_lit_buckets = I.put(ltab); h.off_lits = I.put(dlits); h.off_sig_regex = I.put(sregex);
     h.off_always = I.put(always);
-    h.off_alw = I.put(alw); h.off_alw_pack = I.put(alw_pack);
+    h.off_alw = I.put(alw); h.off_alw_slices = I.put(alw_slices); h.off_alw_pack = I.put(alw_pack);
+    h.off_alw_rule = I.put(alw_rule);
     h.n_rk_cap = rkcap; h.n_rk_ids = (uint32_t)rk_ids.size(); h.n_rk_ents_keys = (uint32_t)rk_lists.size();
     h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_rk_ents = I.put(rk_ents); h.off_rk_bloom = I.put(rk_bloom);
     h.n_ups = (uint32_t)dups.size(); h.n_peers = (uint32_t)peer_init.size();
@@ -1779,9 +1868,11 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.n_ups = h.n_ups; t.n_peers = h.n_peers;
     t.loc_uri = (const DLocUri *)(b + h.off_loc_uri);
     t.decoders = h.decoders;
-    t.alw = (const DAlw *)(b + h.off_alw);
+    t.alw = (const DAlwGroup *)(b + h.off_alw);
+    t.alw_slices = (const DAlwSlice *)(b + h.off_alw_slices);
     t.alw_pack = b + h.off_alw_pack;
-    t.n_always_lds = h.n_always_lds; t.alw_pack_len = h.alw_pack_len;
+    t.alw_rule = (const uint32_t *)(b + h.off_alw_rule);
+    t.n_always_lds = h.n_always_lds; t.n_alw_groups = h.n_alw_groups; t.n_alw_slices = h.n_alw_slices;
     t.n_ports = h.n_ports;
     t.names_mask = h.n_names_cap - 1; t.wild_head_mask = h.n_wild_head_cap - 1; t.wild_tail_mask = h.n_wild_tail_cap - 1;
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;

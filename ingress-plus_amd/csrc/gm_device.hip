@@ -1205,10 +1205,12 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SCAN_LDS_BYTES) != hipSuccess) {
                 t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
             }
-        if (hipFuncSetAttribute((const void *)k_waf_always_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)ALWAYS_LDS_BYTES) != hipSuccess) {
-            t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
-        }
+        const void *alws[] = {(const void *)k_waf_always_multi<1>, (const void *)k_waf_always_multi<2>,
+                              (const void *)k_waf_always_multi<3>, (const void *)k_waf_always_multi<4>};
+        for (const void *f : alws)
+            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ALWAYS_LDS_BYTES) != hipSuccess) {
+                t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
+            }
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, hip_device) == hipSuccess && cus > 0)
             c->cu_count = cus;
@@ -1285,6 +1287,32 @@ int gm_stats(gm_ctx *c, gm_stats_t *out) {
 
 // Enqueue one batch on stream s (device pointers).  No host synchronisation: every size a later
 // stage needs is a device status word or a host-known capacity.
+// the always-run regexes: the LDS-staged groups, then the groups read from the image, then the
+// regexes no group could take (lane per (request, regex))
+static int launch_always(gm_ctx *c, hipStream_t s, const Generation *g, const uint8_t *A, uint64_t alen,
+                         const gm_req *reqs, uint32_t n, Scratch *S, const Dedup &dd, bool skip_empty,
+                         const uint64_t *dlen) {
+    const GTab &t = g->tab;
+    const DAlwSlice *sls = reinterpret_cast<const DAlwSlice *>(g->host_image.data() + g->hdr.off_alw_slices);
+    for (uint32_t k = 0; k < t.n_alw_slices; k++) {
+        const DAlwSlice &sl = sls[k];
+        const dim3 grid((uint32_t)c->cu_count), blk(1024);
+        switch (sl.n_groups) {
+        case 1: k_waf_always_multi<1><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
+        case 2: k_waf_always_multi<2><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
+        case 3: k_waf_always_multi<3><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
+        default: k_waf_always_multi<4><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
+        }
+        HIPCHK(c, hipGetLastError());
+    }
+    if (t.n_always > t.n_always_lds) {
+        k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(A, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd,
+                                                               skip_empty, t.n_always_lds);
+        HIPCHK(c, hipGetLastError());
+    }
+    return GM_OK;
+}
+
 static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *reqs, const uint8_t *A, uint64_t alen,
                      uint32_t n, gm_verdict *out, uint32_t *hit_ids, size_t hit_cap, const uint64_t *dlen) {
     hipStream_t s = S->stream;
@@ -1424,16 +1452,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
                                                                (uint32_t)S->cap_pairs, dd);
         HIPCHK(c, hipGetLastError());
     }
-    if (t.n_always_lds) {
-        k_waf_always_lds<<<(uint32_t)c->cu_count, 1024, t.alw_pack_len, s>>>(A, alen, reqs, n, t, S->d_pairs,
-                                                                             (uint32_t)S->cap_pairs, dd, false, dlen);
-        HIPCHK(c, hipGetLastError());
-    }
-    if (t.n_always > t.n_always_lds) {
-        k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(A, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, false,
-                                                               t.n_always_lds);
-        HIPCHK(c, hipGetLastError());
-    }
+    if ((e = launch_always(c, s, g, A, alen, reqs, n, S, dd, false, dlen))) return e;
     if (t.decoders) {
         // ---- the request parsers' decoded views (gm_decode.inc): shadow records, same indices,
         // then the WAF stages once more over them; hits land in the same dedupe set and counts
@@ -1477,16 +1496,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
                                                                    (uint32_t)S->cap_pairs, dd2);
             HIPCHK(c, hipGetLastError());
         }
-        if (t.n_always_lds) {
-            k_waf_always_lds<<<(uint32_t)c->cu_count, 1024, t.alw_pack_len, s>>>(SA, scap, SR, n, t, S->d_pairs,
-                                                                                 (uint32_t)S->cap_pairs, dd2, true, slen);
-            HIPCHK(c, hipGetLastError());
-        }
-        if (t.n_always > t.n_always_lds) {
-            k_waf_always<<<(uint32_t)c->cu_count * 8, 256, 0, s>>>(SA, SR, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd2, true,
-                                                                   t.n_always_lds);
-            HIPCHK(c, hipGetLastError());
-        }
+        if ((e = launch_always(c, s, g, SA, scap, SR, n, S, dd2, true, slen))) return e;
     }
     // ---- hit emission: offsets by an exclusive scan of the per-request counts (request order)
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_temp, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));

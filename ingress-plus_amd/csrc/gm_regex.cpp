@@ -744,6 +744,147 @@ bool dfa_search(const Dfa &d, const uint8_t *s, size_t n) {
     return (d.acc[st] & 2) != 0;
 }
 
+// ---------------------------------------------------------------- union DFA (always-run groups)
+bool build_multi(const std::vector<const Dfa *> &comps, int max_states, MultiDfa &out) {
+    const size_t k = comps.size();
+    if (k == 0 || k > 32 || max_states > 0x3FFF) return false;
+    // joint byte classes: bytes with the same class in every component
+    int cls[256];
+    std::vector<int> rep;
+    {
+        std::map<std::vector<uint8_t>, int> sig;
+        for (int b = 0; b < 256; b++) {
+            std::vector<uint8_t> v(k);
+            for (size_t i = 0; i < k; i++) v[i] = comps[i]->cls[b];
+            auto it = sig.emplace(v, (int)sig.size()).first;
+            cls[b] = it->second;
+            if (it->second == (int)rep.size()) rep.push_back(b);
+        }
+    }
+    const int C = (int)rep.size();
+    // state key: component states (u16 each) + the emitted mask
+    std::unordered_map<std::string, int> ids;
+    std::vector<std::vector<uint16_t>> tup;
+    std::vector<uint32_t> emit;
+    auto key_of = [&](const std::vector<uint16_t> &t, uint32_t e) {
+        std::string s(reinterpret_cast<const char *>(t.data()), 2 * t.size());
+        s.append(reinterpret_cast<const char *>(&e), 4);
+        return s;
+    };
+    auto intern = [&](const std::vector<uint16_t> &t, uint32_t e) -> int {
+        const std::string key = key_of(t, e);
+        auto it = ids.find(key);
+        if (it != ids.end()) return it->second;
+        if ((int)tup.size() >= max_states) return -1;
+        ids.emplace(key, (int)tup.size());
+        tup.push_back(t);
+        emit.push_back(e);
+        return (int)tup.size() - 1;
+    };
+    intern(std::vector<uint16_t>(k, 0), 0);   // 0 = dead
+    {
+        std::vector<uint16_t> t(k, 1);
+        uint32_t e = 0;
+        for (size_t i = 0; i < k; i++)
+            if (comps[i]->acc[1] & 1) { e |= 1u << i; t[i] = 0; }
+        intern(t, e);
+    }
+    std::vector<uint16_t> trans;
+    for (size_t cur = 0; cur < tup.size(); cur++) {
+        trans.resize((cur + 1) * C, 0);
+        if (cur == 0) continue;
+        for (int c = 0; c < C; c++) {
+            const int b = rep[c];
+            std::vector<uint16_t> nt(k, 0);
+            uint32_t e = 0;
+            for (size_t i = 0; i < k; i++) {
+                const uint16_t s = tup[cur][i];
+                if (!s) continue;
+                const Dfa &d = *comps[i];
+                const uint16_t ns = d.trans[(size_t)s * d.n_classes + d.cls[b]];
+                if (d.acc[ns] & 1) e |= 1u << i; else nt[i] = ns;
+            }
+            const int id = intern(nt, e);
+            if (id < 0) return false;
+            trans[cur * C + c] = (uint16_t)(id | (e ? MDFA_EMIT : 0));
+        }
+    }
+    out.n_states = (int)tup.size();
+    out.n_classes = C;
+    out.trans = std::move(trans);
+    out.emit = emit;
+    out.endm.assign(tup.size(), 0);
+    for (size_t s = 0; s < tup.size(); s++)
+        for (size_t i = 0; i < k; i++)
+            if (tup[s][i] && (comps[i]->acc[tup[s][i]] & 2)) out.endm[s] |= 1u << i;
+    for (int b = 0; b < 256; b++) out.cls[b] = (uint8_t)cls[b];
+    minimize_multi(out);
+    return true;
+}
+
+// Moore partition refinement: states with the same emit / end masks whose transitions lead to
+// equivalent states on every class merge (the product carries many: retired components, the
+// same tuple reached with and without an emission).  Dead stays 0, start stays 1; the rest are
+// numbered breadth-first from the start.
+void minimize_multi(MultiDfa &m) {
+    const int S = m.n_states, C = m.n_classes;
+    if (S <= 2) return;
+    std::vector<int> part(S), np(S);
+    {
+        std::map<std::pair<uint32_t, uint32_t>, int> ids;
+        for (int s = 0; s < S; s++) part[s] = ids.emplace(std::make_pair(m.emit[s], m.endm[s]), (int)ids.size()).first->second;
+    }
+    int nparts = 0;
+    for (;;) {
+        std::unordered_map<std::string, int> ids;
+        std::vector<int> sig(C + 1);
+        for (int s = 0; s < S; s++) {
+            sig[0] = part[s];
+            for (int c = 0; c < C; c++) sig[c + 1] = part[m.trans[(size_t)s * C + c] & 0x3FFF];
+            std::string key(reinterpret_cast<const char *>(sig.data()), sig.size() * sizeof(int));
+            np[s] = ids.emplace(std::move(key), (int)ids.size()).first->second;
+        }
+        const int n = (int)ids.size();
+        part.swap(np);
+        if (n == nparts) break;
+        nparts = n;
+    }
+    if (part[0] == part[1]) return;   // nothing can ever match: keep the product as built
+    // renumber: dead 0, start 1, then BFS order
+    std::vector<int> id(nparts, -1), rep;
+    id[part[0]] = 0; rep.push_back(0);
+    id[part[1]] = 1; rep.push_back(1);
+    for (size_t q = 1; q < rep.size(); q++)
+        for (int c = 0; c < C; c++) {
+            const int t = m.trans[(size_t)rep[q] * C + c] & 0x3FFF;
+            if (id[part[t]] < 0) { id[part[t]] = (int)rep.size(); rep.push_back(t); }
+        }
+    const int S2 = (int)rep.size();
+    std::vector<uint16_t> tr((size_t)S2 * C, 0);
+    std::vector<uint32_t> em(S2), en(S2);
+    for (int q = 0; q < S2; q++) {
+        em[q] = m.emit[rep[q]]; en[q] = m.endm[rep[q]];
+        if (q == 0) continue;
+        for (int c = 0; c < C; c++) {
+            const uint16_t e = m.trans[(size_t)rep[q] * C + c];
+            tr[(size_t)q * C + c] = (uint16_t)(id[part[e & 0x3FFF]] | (e & MDFA_EMIT));
+        }
+    }
+    m.trans.swap(tr); m.emit.swap(em); m.endm.swap(en);
+    m.n_states = S2;
+}
+
+uint32_t multi_search(const MultiDfa &m, const uint8_t *s, size_t n) {
+    uint32_t st = 1, r = m.emit[1];
+    for (size_t i = 0; i < n; i++) {
+        if (i + 1 == n && s[i] == '\n') r |= m.endm[st];
+        st = m.trans[(size_t)st * m.n_classes + m.cls[s[i]]] & 0x3FFF;
+        r |= m.emit[st];
+        if (st == 0) return r;
+    }
+    return r | m.endm[st];
+}
+
 }  // namespace gm
 
 // ---------------------------------------------------------------- debug exports (gpumatch_debug.h)

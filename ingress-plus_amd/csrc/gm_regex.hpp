@@ -45,6 +45,26 @@ struct RegexInfo {
 
 RegexInfo compile_regex(const std::string &pattern, bool caseless, int max_states = 8192);
 
+// Union of search DFAs (compile_regex().dfa each): one pass over a subject answers "which of
+// them match".  A state is (every component's state, the components that matched on entering
+// it); a component that reaches an accepting state is retired (its state becomes 0) and the
+// target state emits its bit, so the union never carries a matched component further.
+// trans entries: target state | MDFA_EMIT when the target emits; endm[s]: components whose state
+// in s accepts at the end of the subject ($).  State 0 = dead, 1 = start.
+constexpr uint16_t MDFA_EMIT = 0x4000;
+struct MultiDfa {
+    std::vector<uint16_t> trans;   // [n_states * n_classes]
+    std::vector<uint32_t> emit, endm;
+    uint8_t cls[256];
+    int n_states = 0, n_classes = 0;
+};
+// false when the union needs more than max_states states (<= 0x3FFF) before minimisation, or
+// more than 32 components; the result is minimised (minimize_multi)
+bool build_multi(const std::vector<const Dfa *> &comps, int max_states, MultiDfa &out);
+void minimize_multi(MultiDfa &m);
+// Host evaluation: bit k set iff comps[k] matches s (dfa_search semantics per component)
+uint32_t multi_search(const MultiDfa &m, const uint8_t *s, size_t n);
+
 // Host evaluation with PCRE search semantics (used for compile-time map truth tables).
 bool dfa_search(const Dfa &d, const uint8_t *s, size_t n);
 

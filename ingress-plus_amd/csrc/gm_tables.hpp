@@ -251,16 +251,38 @@ __host__ __device__ inline uint32_t peer_draw(uint64_t lo, uint64_t hi, uint32_t
     return (uint32_t)(x >> 32);
 }
 
-// Always-run signature regexes (RXM_ALWAYS, no >= 4-byte factor) whose DFAs fit together in LDS:
-// k_waf_always_lds stages the pack once per workgroup and runs a wave per request with a lane per
-// regex -- the zone's bytes are read once per 64 regexes and every transition is an LDS read.
-// Pack: per regex its 256-byte class map, then its transitions (u16, as dfa_trans), 16-B aligned.
-constexpr uint32_t ALWAYS_LDS_BYTES = 96 * 1024;
-struct DAlw {
-    uint32_t cls_off, tr_off;   // byte offsets in the pack
-    uint16_t n_classes, acc1;   // acc1: the start state's accept flags
-    uint32_t rule;
-    uint32_t zones;
+// Always-run signature regexes (RXM_ALWAYS, no >= 4-byte factor): grouped into union DFAs
+// (gm_regex.hpp MultiDfa, <= ALW_GROUP_MAX regexes and ALW_GROUP_BYTES of rows a group), so one
+// pass over a zone answers a whole group.  Groups are packed into slices of <= ALW_SLICE_GROUPS
+// groups that fit ALWAYS_LDS_BYTES together; k_waf_always_multi stages one slice in LDS and runs a
+// transition chain per group of the slice.
+// Slice pack (16-B aligned): clsq u32[256] (byte b's class in group j of the slice = byte j of
+// clsq[b]) | per group, its rows.  A row (state) is Cp + 4 u16: the transitions of the C classes
+// (Cp = C rounded up to even), then the state's emit mask and end mask (u32 each).  A transition
+// is the target row's byte offset in the group | ALW_EMIT (bit 0) when the target emits: the step
+// needs no multiply, and row 0 (the dead state) is all zeros.
+constexpr uint32_t ALWAYS_LDS_BYTES = 128 * 1024;
+constexpr uint32_t ALW_GROUP_BYTES = 32 * 1024;   // row byte offsets fit a u16 with the flag bit
+constexpr uint32_t ALW_GROUP_MAX = 32;
+constexpr uint32_t ALW_SLICE_GROUPS = 4;
+constexpr uint32_t ALW_BUILD_STATES = 8192;   // product states before minimisation
+constexpr uint32_t ALW_EMIT = 1;
+constexpr uint32_t ALW_ROW_MASK = 0x7FFE;
+struct DAlwGroup {
+    uint32_t tr_off;         // byte offset of row 0 from the slice start
+    uint32_t mask_off;       // byte offset of the emit mask within a row (2 Cp); the end mask follows
+    uint32_t start_row;      // byte offset of the start state's row (row 1)
+    uint32_t n_classes, n_states;
+    uint32_t zone_mask[4];   // members (bit k) that scan zone z
+    uint32_t first;          // member k's rule id: alw_rule[first + k]
+    uint32_t zones;          // zones some member scans
+    uint32_t pad;
+};
+struct DAlwSlice {
+    uint32_t off, len;       // bytes of the pack
+    uint32_t first_group, n_groups;
+    uint32_t zones;          // zones some group scans
+    uint32_t pad[3];
 };
 
 struct TabHeader {
@@ -290,8 +312,9 @@ struct TabHeader {
     uint64_t off_ups, off_key_parts, off_points, off_peer_init;   // peer_init: u32 GM_PEER_DOWN per peer
     uint64_t off_loc_uri;          // DLocUri per location
     uint32_t decoders, pad_dec;    // the signature set's request parsers (DEC_*)
-    uint32_t n_always_lds, alw_pack_len;   // always[0, n_always_lds) are in the LDS pack
-    uint64_t off_alw, off_alw_pack;
+    uint32_t n_always_lds;         // always[0, n_always_lds) are in union-DFA groups
+    uint32_t n_alw_groups, n_alw_slices, alw_pack_len, pad_alw;
+    uint64_t off_alw, off_alw_slices, off_alw_pack, off_alw_rule;
 };
 // The route's hot tables -- ports, the three name tables, servers, server ifs, small-location
 // lists, locations and the name strings -- are laid out first and contiguously in the image;
@@ -316,7 +339,8 @@ struct GTab {                // device pointers, built on host from the image ba
     uint32_t n_ups, n_peers;
     const DLocUri *loc_uri;
     uint32_t decoders;
-    const DAlw *alw; const uint8_t *alw_pack; uint32_t n_always_lds, alw_pack_len;
+    const DAlwGroup *alw; const DAlwSlice *alw_slices; const uint8_t *alw_pack; const uint32_t *alw_rule;
+    uint32_t n_always_lds, n_alw_groups, n_alw_slices;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
     uint32_t gen;

@@ -83,6 +83,54 @@ def test_c4_stress_variant_parity(eng):
     assert st["n_sig_regex_always"] == 200 and st["last_candidates"] > 10 * len(reqs)
 
 
+def always_rules(n=150, seed=11):
+    """Factorless (always-run) regexes of mixed shapes: short literals, counted classes, anchors
+    (^, $ with nginx's "before a final newline"), alternations, an empty-matching pattern and
+    case-insensitive ones, over every zone set -- enough of them for several union-DFA groups and
+    LDS slices (gm_compile.cpp, k_waf_always_multi)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    L = "abcdefghij"
+    out = [sigs.Rule("re", False, "uahb", r"z*"), sigs.Rule("re", False, "b", r"^$"),
+           sigs.Rule("re", True, "ah", r"^q[0-9]"), sigs.Rule("re", False, "b", r"[a-c]{2}$")]
+    for i in range(n - len(out)):
+        t = int(rng.integers(0, 8))
+        a, b2 = (L[int(x)] for x in rng.integers(0, len(L), 2))
+        k = int(rng.integers(1, 5))
+        pat = [f"{a}{b2}[0-9]{{{k}}}", f"[0-9]{{{k},}}{a}x", f"({a}{b2}|{b2}{a})-{k}", f"{a}[^{b2}]{{{k}}}{a}",
+               f"^{a}{b2}", f"{a}{k}$", f"={a}\\s*{b2}", f"<{a}[a-z]{{0,{k}}}>"][t]
+        out.append(sigs.Rule("re", bool(rng.random() < 0.4), ["uahb", "ua", "b", "h", "u"][int(rng.integers(0, 5))], pat))
+    return out
+
+
+def always_items(n, seed=12):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    L = b"abcdefghij0123456789-=<> xzqABCJ\n"
+    items = []
+    for i in range(n):
+        def txt(lo, hi):
+            return bytes(L[int(x)] for x in rng.integers(0, len(L), int(rng.integers(lo, hi))))
+        body = txt(0, 300) if rng.random() < 0.8 else b""
+        if rng.random() < 0.2:
+            body += b"\n"
+        args = txt(0, 40).replace(b"\n", b"").decode() if rng.random() < 0.7 else ""
+        items.append({"host": "cafe.example.com", "uri": "/tea/" + txt(0, 20).replace(b"\n", b"").decode(),
+                      "args": args, "https": True, "body": body,
+                      "headers": [("X-T", txt(0, 30).replace(b"\n", b"").decode())]})
+    return items
+
+
+def test_always_union_groups(eng):
+    """Always-run regexes answered by union DFAs in LDS slices: every (request, rule) hit equal to
+    the oracle's PCRE answers (empty zones, a final newline, anchors, zone sets)."""
+    b = workloads.c4_blob(sigs.SigSet(always_rules()))
+    reqs, arena = records.from_dicts(always_items(20_000))
+    got, gh, exp, eh = run_both(eng, b, reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "always")
+    st = eng.stats()
+    assert st["n_alw_groups"] >= 4 and st["n_alw_slices"] >= 2 and st["n_alw_single"] == 0
+    assert len(eh) > 20_000   # dense hits: the empty-matching pattern alone hits every request
+
+
 def test_waf_edge_cases(eng):
     rules = [sigs.Rule("lit", True, "uahb", b"evil"), sigs.Rule("lit", False, "b", b"CaseSensitive"),
              sigs.Rule("lit", True, "u", b"/tea/x"), sigs.Rule("re", True, "ah", r"sel\s*ect\d+"),
