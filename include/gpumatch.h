@@ -186,6 +186,9 @@ typedef struct gm_stats_t {
     /* always-run regexes: union-DFA groups (one pass over a zone answers a group), their states,
      * the LDS slices they are run in, and regexes left to the per-regex kernel (too big alone) */
     uint32_t n_alw_groups, n_alw_states, n_alw_slices, n_alw_single;
+    /* regex locations of large servers (> RLOC_SEQ_MAX): union-DFA slices in LDS (0: the factor
+     * prefilter runs them) */
+    uint32_t n_rsl_slices;
 } gm_stats_t;
 
 /* Request parsers (Wallarm's) a signature set can declare ("@decoders" line of

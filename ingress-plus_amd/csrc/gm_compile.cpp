@@ -1672,54 +1672,49 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.n_dfas = (uint32_t)C.dfas.size();
     h.n_lit_buckets_cap = lcap; h.n_lits = (uint32_t)dlits.size(); h.n_sig_regex = (uint32_t)sregex.size();
     h.n_always = (uint32_t)always.size(); h.n_sigs = st.n_sigs;
-    // the always-run regexes in union-DFA groups.  Ordered by (zone set, pattern text) -- the
-    // same shapes side by side, whose unions stay small -- a regex joins the open group while the
-    // minimised union's tables stay within ALW_GROUP_BYTES (and ALW_GROUP_MAX members, one zone
-    // set); a regex whose DFA cannot form a group even alone stays with the per-regex kernel.
-    // Groups are then packed into LDS slices.  `always` is reordered: grouped regexes first (group
-    // order), then the rest.
+    // ---- union-DFA groups (gm_regex.hpp MultiDfa) packed into LDS slices (gm_tables.hpp
+    // DAlwSlice): the always-run signature regexes, then the regex locations of rk_on servers
     std::vector<DAlwGroup> alw;
     std::vector<DAlwSlice> alw_slices;
     std::vector<uint8_t> alw_pack;
     std::vector<uint32_t> alw_rule, always_grouped, always_single;
-    {
-        std::vector<uint32_t> ord(always.size());
-        for (uint32_t i = 0; i < ord.size(); i++) ord[i] = i;
-        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
-            const uint16_t zx = sregex[always[x]].zones, zy = sregex[always[y]].zones;
-            return zx != zy ? zx < zy : always_pat[x] < always_pat[y];
-        });
-        auto tab_bytes = [](const MultiDfa &m) {   // the group's rows (gm_tables.hpp DAlwGroup)
-            return (size_t)m.n_states * ((size_t)m.n_classes + (m.n_classes & 1) + 4) * 2;
-        };
-        std::vector<std::vector<uint32_t>> gmem;   // members (indices into always)
-        std::vector<MultiDfa> gdfa;
+    auto tab_bytes = [](const MultiDfa &m) {   // the group's rows (gm_tables.hpp DAlwGroup)
+        return (size_t)m.n_states * ((size_t)m.n_classes + (m.n_classes & 1) + 4) * 2;
+    };
+    // greedy: in `order`, a component joins the open group while joinable(first member, it), the
+    // group has < ALW_GROUP_MAX members and the minimised union's rows stay within
+    // ALW_GROUP_BYTES; a component that cannot form a group even alone goes to `single`
+    auto form_groups = [&](const std::vector<const Dfa *> &comps, const std::vector<uint32_t> &order, auto joinable,
+                           std::vector<std::vector<uint32_t>> &gmem, std::vector<MultiDfa> &gdfa,
+                           std::vector<uint32_t> &single) {
         std::vector<uint32_t> cur;
         MultiDfa cur_m;
         auto close = [&]() {
             if (!cur.empty()) { gmem.push_back(cur); gdfa.push_back(std::move(cur_m)); }
             cur.clear();
         };
-        for (uint32_t x : ord) {
-            const uint16_t zx = sregex[always[x]].zones;
-            if (!cur.empty() && sregex[always[cur[0]]].zones == zx && cur.size() < ALW_GROUP_MAX) {
-                std::vector<const Dfa *> comps;
-                for (uint32_t y : cur) comps.push_back(&always_dfa[y]);
-                comps.push_back(&always_dfa[x]);
+        for (uint32_t x : order) {
+            if (!cur.empty() && joinable(cur[0], x) && cur.size() < ALW_GROUP_MAX) {
+                std::vector<const Dfa *> cs;
+                for (uint32_t y : cur) cs.push_back(comps[y]);
+                cs.push_back(comps[x]);
                 MultiDfa m;
-                if (build_multi(comps, (int)ALW_BUILD_STATES, m) && tab_bytes(m) <= ALW_GROUP_BYTES) {
+                if (build_multi(cs, (int)ALW_BUILD_STATES, m) && tab_bytes(m) <= ALW_GROUP_BYTES) {
                     cur.push_back(x); cur_m = std::move(m); continue;
                 }
             }
             close();
             MultiDfa m;
-            std::vector<const Dfa *> one{&always_dfa[x]};
-            if (build_multi(one, (int)ALW_BUILD_STATES, m) &&
-                tab_bytes(m) <= ALW_GROUP_BYTES) { cur.push_back(x); cur_m = std::move(m); }
-            else always_single.push_back(always[x]);
+            if (build_multi({comps[x]}, (int)ALW_BUILD_STATES, m) && tab_bytes(m) <= ALW_GROUP_BYTES) {
+                cur.push_back(x); cur_m = std::move(m);
+            } else single.push_back(x);
         }
         close();
-        // slices: consecutive groups, <= ALW_SLICE_GROUPS of them within ALWAYS_LDS_BYTES
+    };
+    // slices: consecutive groups, <= ALW_SLICE_GROUPS of them within ALWAYS_LDS_BYTES; member k of
+    // group g stores val(g, k) in alw_rule and scans the zones zones(g, k)
+    auto pack_slices = [&](const std::vector<std::vector<uint32_t>> &gmem, const std::vector<MultiDfa> &gdfa,
+                           auto val, auto zones, uint32_t server) {
         auto pad16 = [&]() { alw_pack.resize((alw_pack.size() + 15) & ~size_t(15), 0); };
         for (size_t g0 = 0; g0 < gmem.size();) {
             size_t g1 = g0, bytes = 1024;
@@ -1729,6 +1724,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             sl.off = (uint32_t)alw_pack.size();
             sl.first_group = (uint32_t)alw.size();
             sl.n_groups = (uint32_t)(g1 - g0);
+            sl.server = server;
             std::vector<uint32_t> clsq(256, 0);
             for (size_t j = g0; j < g1; j++)
                 for (int b = 0; b < 256; b++) clsq[b] |= (uint32_t)gdfa[j].cls[b] << (8 * (j - g0));
@@ -1756,12 +1752,11 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 g.n_classes = (uint32_t)Cn; g.n_states = (uint32_t)S;
                 g.first = (uint32_t)alw_rule.size();
                 for (size_t k = 0; k < gmem[j].size(); k++) {
-                    const DSigRegex &sr = sregex[always[gmem[j][k]]];
-                    alw_rule.push_back(sr.rule);
-                    always_grouped.push_back(always[gmem[j][k]]);
+                    alw_rule.push_back(val(j, k));
+                    const uint32_t zk = zones(j, k);
                     for (uint32_t z = 0; z < 4; z++)
-                        if (sr.zones & (1u << z)) g.zone_mask[z] |= 1u << k;
-                    g.zones |= sr.zones;
+                        if (zk & (1u << z)) g.zone_mask[z] |= 1u << k;
+                    g.zones |= zk;
                 }
                 sl.zones |= g.zones;
                 st.n_alw_states += (uint32_t)S;
@@ -1771,10 +1766,76 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             alw_slices.push_back(sl);
             g0 = g1;
         }
+    };
+    // the always-run regexes, ordered by (zone set, pattern text) -- the same shapes side by side,
+    // whose unions stay small; a group holds one zone set.  `always` is reordered: the grouped
+    // regexes first (group order), then those left to the per-regex kernel.
+    {
+        std::vector<const Dfa *> comps;
+        for (const Dfa &d : always_dfa) comps.push_back(&d);
+        std::vector<uint32_t> ord(always.size());
+        for (uint32_t i = 0; i < ord.size(); i++) ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+            const uint16_t zx = sregex[always[x]].zones, zy = sregex[always[y]].zones;
+            return zx != zy ? zx < zy : always_pat[x] < always_pat[y];
+        });
+        std::vector<std::vector<uint32_t>> gmem;
+        std::vector<MultiDfa> gdfa;
+        std::vector<uint32_t> single;
+        form_groups(comps, ord, [&](uint32_t a, uint32_t b) { return sregex[always[a]].zones == sregex[always[b]].zones; },
+                    gmem, gdfa, single);
+        pack_slices(gmem, gdfa, [&](size_t j, size_t k) { return sregex[always[gmem[j][k]]].rule; },
+                    [&](size_t j, size_t k) { return (uint32_t)sregex[always[gmem[j][k]]].zones; }, GM_NONE);
+        for (auto &gm : gmem) for (uint32_t x : gm) always_grouped.push_back(always[x]);
+        for (uint32_t x : single) always_single.push_back(always[x]);
+    }
+    const uint32_t n_alw_slices = (uint32_t)alw_slices.size();
+    // the regex locations of every rk_on server, in config order (consecutive groups, so the
+    // first group with a match holds the first matching regex); a PCRE-only location carries its
+    // superset DFA, one without any DFA matches at once (a DFA whose start state accepts).  A
+    // server with a regex no group can hold keeps the factor prefilter.
+    {
+        Dfa match_all;
+        match_all.n_states = 2; match_all.n_classes = 1;
+        match_all.trans.assign(2, 0); match_all.trans[1] = 1;
+        match_all.acc = {0, 1};
+        memset(match_all.cls, 0, sizeof match_all.cls);
+        for (auto &Sv : M.servers) {
+            DServer &D = dservers[Sv.id];
+            if (!D.rk_on) continue;
+            std::vector<Dfa> own(D.n_rloc);
+            std::vector<const Dfa *> comps(D.n_rloc);
+            for (uint32_t k = 0; k < D.n_rloc; k++) {
+                const DRegexLoc &rl = rlocs[D.first_rloc + k];
+                if (rl.dfa == GM_NONE) { comps[k] = &match_all; continue; }
+                const DDfa &dd = C.dfas[rl.dfa];
+                Dfa &o = own[k];
+                o.n_states = dd.n_states; o.n_classes = dd.n_classes;
+                o.trans.resize((size_t)dd.n_states * dd.n_classes);
+                for (size_t i = 0; i < o.trans.size(); i++) o.trans[i] = C.dfa_trans[dd.trans_off + i] & DFA_TRANS_STATE_MASK;
+                o.acc.assign(C.dfa_acc.begin() + dd.acc_off, C.dfa_acc.begin() + dd.acc_off + dd.n_states);
+                for (int b2 = 0; b2 < 256; b2++) o.cls[b2] = C.dfa_cls[dd.cls_off + b2];
+                comps[k] = &o;
+            }
+            std::vector<uint32_t> ord(D.n_rloc);
+            for (uint32_t i = 0; i < ord.size(); i++) ord[i] = i;
+            std::vector<std::vector<uint32_t>> gmem;
+            std::vector<MultiDfa> gdfa;
+            std::vector<uint32_t> single;
+            form_groups(comps, ord, [](uint32_t, uint32_t) { return true; }, gmem, gdfa, single);
+            if (!single.empty()) { h.n_rk_prefilter++; continue; }
+            D.rsl_first = (uint32_t)alw_slices.size();
+            const uint32_t fr = D.first_rloc;
+            pack_slices(gmem, gdfa, [&](size_t j, size_t k) { return fr + gmem[j][k]; },
+                        [](size_t, size_t) { return 1u; }, (uint32_t)Sv.id);
+            D.rsl_n = (uint32_t)alw_slices.size() - D.rsl_first;
+            st.n_rsl_slices += D.rsl_n;
+        }
     }
     h.n_always_lds = (uint32_t)always_grouped.size();
     h.n_alw_groups = (uint32_t)alw.size();
-    h.n_alw_slices = (uint32_t)alw_slices.size();
+    h.n_alw_slices = n_alw_slices;
+    h.n_rsl = (uint32_t)alw_slices.size() - n_alw_slices;
     h.alw_pack_len = (uint32_t)alw_pack.size();
     st.n_alw_groups = h.n_alw_groups; st.n_alw_slices = h.n_alw_slices;
     st.n_alw_single = (uint32_t)always_single.size();
@@ -1873,6 +1934,7 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.alw_pack = b + h.off_alw_pack;
     t.alw_rule = (const uint32_t *)(b + h.off_alw_rule);
     t.n_always_lds = h.n_always_lds; t.n_alw_groups = h.n_alw_groups; t.n_alw_slices = h.n_alw_slices;
+    t.n_rsl = h.n_rsl; t.n_rk_prefilter = h.n_rk_prefilter;
     t.n_ports = h.n_ports;
     t.names_mask = h.n_names_cap - 1; t.wild_head_mask = h.n_wild_head_cap - 1; t.wild_tail_mask = h.n_wild_tail_cap - 1;
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;

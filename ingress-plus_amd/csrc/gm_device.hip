@@ -872,7 +872,8 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
         if (best >= 0 && t.locs[best].noregex) loc = best;
         else {
             if (S.rk_on && rk_in >= -1) loc = rk_in;
-            else if (S.rk_on && rk_in == RK_DEFER && r.uri_len <= RLOC_URI_CAP && S.n_rloc <= RLOC_BM_BITS) {
+            else if (S.rk_on && rk_in == RK_DEFER &&
+                     (S.rsl_n || (r.uri_len <= RLOC_URI_CAP && S.n_rloc <= RLOC_BM_BITS))) {
                 *pend = true;
                 return;
             } else loc = rloc_first_match(t, S, sid, u, r.uri_len, rkb);
@@ -1022,8 +1023,8 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
     }
 }
 
-#include "gm_rloc.inc"
 #include "gm_waf.inc"
+#include "gm_rloc.inc"
 #include "gm_decode.inc"
 
 }  // namespace
@@ -1206,7 +1207,9 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
                 t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
             }
         const void *alws[] = {(const void *)k_waf_always_multi<1>, (const void *)k_waf_always_multi<2>,
-                              (const void *)k_waf_always_multi<3>, (const void *)k_waf_always_multi<4>};
+                              (const void *)k_waf_always_multi<3>, (const void *)k_waf_always_multi<4>,
+                              (const void *)k_rloc_multi<1>, (const void *)k_rloc_multi<2>,
+                              (const void *)k_rloc_multi<3>, (const void *)k_rloc_multi<4>};
         for (const void *f : alws)
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ALWAYS_LDS_BYTES) != hipSuccess) {
                 t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
@@ -1334,23 +1337,41 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     // prefiltered regex locations: k_route defers their step to k_rloc (a tile of requests per
     // workgroup, gm_rloc.inc) and a second k_route pass over the deferred list finishes them
     RlocQ q{};
-    if (t.rk_keys) {
+    const bool rk = t.rk_keys || t.n_rsl;
+    if (rk) {
         int e2;
         if ((e2 = grow(c, s, S->d_rq, S->cap_rq, n)) || (e2 = grow(c, s, S->d_rql, S->cap_rql, n))) return e2;
         q = RlocQ{S->d_rq, S->d_status + RLOC_STATUS_WORD, S->d_rql};
     }
     auto launch_rloc = [&](hipStream_t rs, uint32_t tail_blocks) -> int {
-        k_rloc<<<(uint32_t)c->cu_count * 4, RLOC_BLOCK, 0, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen);
+        // union-DFA slices of the servers that have them (config order: a request answered by one
+        // slice skips the later ones), then the factor prefilter for the others
+        if (t.n_rsl) {
+            HIPCHK(c, hipMemsetAsync(q.loc, 0xFF, (size_t)n * 4, rs));
+            const DAlwSlice *sls = reinterpret_cast<const DAlwSlice *>(g->host_image.data() + g->hdr.off_alw_slices);
+            for (uint32_t k = t.n_alw_slices; k < t.n_alw_slices + t.n_rsl; k++) {
+                const dim3 grid((uint32_t)c->cu_count), blk(1024);
+                switch (sls[k].n_groups) {
+                case 1: k_rloc_multi<1><<<grid, blk, sls[k].len, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen, k); break;
+                case 2: k_rloc_multi<2><<<grid, blk, sls[k].len, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen, k); break;
+                case 3: k_rloc_multi<3><<<grid, blk, sls[k].len, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen, k); break;
+                default: k_rloc_multi<4><<<grid, blk, sls[k].len, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen, k); break;
+                }
+                HIPCHK(c, hipGetLastError());
+            }
+        }
+        if (t.n_rk_prefilter)
+            k_rloc<<<(uint32_t)c->cu_count * 4, RLOC_BLOCK, 0, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen);
         k_route<3, true, true><<<tail_blocks, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk,
                                                                     nullptr, 0, dlen, q);
         HIPCHK(c, hipGetLastError());
         return GM_OK;
     };
     if (!waf) {
-        if (t.rk_keys) k_route<3, true><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, q);
+        if (rk) k_route<3, true><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, q);
         else k_route<3><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen);
         HIPCHK(c, hipGetLastError());
-        if (t.rk_keys) {
+        if (rk) {
             const int e4 = launch_rloc(s, route_blocks);
             if (e4) return e4;
         }
@@ -1412,13 +1433,13 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         if (prof) HIPCHK(c, hipEventRecord(S->ev_route[0], rs));
         // raised issue priority beside the scan: the route's short latency-bound waves finish
         // early instead of stretching past the scan
-        if (t.rk_keys)
+        if (rk)
             k_route<5, true><<<nb, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1, dlen, q);
         else
             k_route<5><<<nb, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1, dlen);
         HIPCHK(c, hipGetLastError());
         int e3;
-        if (t.rk_keys && (e3 = launch_rloc(rs, nb))) return e3;
+        if (rk && (e3 = launch_rloc(rs, nb))) return e3;
         if (prof) HIPCHK(c, hipEventRecord(S->ev_route[1], rs));
         if (!serial) HIPCHK(c, hipEventRecord(S->ev_join, rs));
         S->route_side = true;

@@ -49,6 +49,8 @@ struct DServer {
     uint32_t first_ralw, n_ralw;  // rk_ids slice: regex locations evaluated for every URI (no
                                   // >= 4-byte factor, or PCRE-only), ascending
     uint32_t sl_first, sl_n;      // small-server location list (DSmallLoc), sl_n = 0: trie walk
+    uint32_t rsl_first, rsl_n;    // rk_on servers: union-DFA slices of the regex locations
+                                  // (DAlwSlice, config order; rsl_n = 0: the factor prefilter)
 };
 // A server whose location names all fit 16 bytes and whose trie has at most SMALL_LOCS_MAX
 // nodes carrying a location gets those nodes as a flat list: the route compares the URI's
@@ -282,7 +284,8 @@ struct DAlwSlice {
     uint32_t off, len;       // bytes of the pack
     uint32_t first_group, n_groups;
     uint32_t zones;          // zones some group scans
-    uint32_t pad[3];
+    uint32_t server;         // regex-location slices: the server (GM_NONE: always-run regexes)
+    uint32_t pad[2];
 };
 
 struct TabHeader {
@@ -313,7 +316,9 @@ struct TabHeader {
     uint64_t off_loc_uri;          // DLocUri per location
     uint32_t decoders, pad_dec;    // the signature set's request parsers (DEC_*)
     uint32_t n_always_lds;         // always[0, n_always_lds) are in union-DFA groups
-    uint32_t n_alw_groups, n_alw_slices, alw_pack_len, pad_alw;
+    uint32_t n_alw_groups, n_alw_slices, alw_pack_len, n_rsl;   // n_rsl: regex-location slices
+                                                                 // after the n_alw_slices
+    uint32_t n_rk_prefilter, pad_rkp;   // rk_on servers left to the factor prefilter (rsl_n 0)
     uint64_t off_alw, off_alw_slices, off_alw_pack, off_alw_rule;
 };
 // The route's hot tables -- ports, the three name tables, servers, server ifs, small-location
@@ -340,7 +345,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const DLocUri *loc_uri;
     uint32_t decoders;
     const DAlwGroup *alw; const DAlwSlice *alw_slices; const uint8_t *alw_pack; const uint32_t *alw_rule;
-    uint32_t n_always_lds, n_alw_groups, n_alw_slices;
+    uint32_t n_always_lds, n_alw_groups, n_alw_slices, n_rsl, n_rk_prefilter;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
     uint32_t gen;
