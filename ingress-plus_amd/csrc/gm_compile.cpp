@@ -1799,6 +1799,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         match_all.n_states = 2; match_all.n_classes = 1;
         match_all.trans.assign(2, 0); match_all.trans[1] = 1;
         match_all.acc = {0, 1};
+        match_all.anchored_start = true;
         memset(match_all.cls, 0, sizeof match_all.cls);
         for (auto &Sv : M.servers) {
             DServer &D = dservers[Sv.id];
@@ -1811,24 +1812,38 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 const DDfa &dd = C.dfas[rl.dfa];
                 Dfa &o = own[k];
                 o.n_states = dd.n_states; o.n_classes = dd.n_classes;
+                o.anchored_start = (dd.flags & DFA_ANCHOR_START) != 0;
                 o.trans.resize((size_t)dd.n_states * dd.n_classes);
                 for (size_t i = 0; i < o.trans.size(); i++) o.trans[i] = C.dfa_trans[dd.trans_off + i] & DFA_TRANS_STATE_MASK;
                 o.acc.assign(C.dfa_acc.begin() + dd.acc_off, C.dfa_acc.begin() + dd.acc_off + dd.n_states);
                 for (int b2 = 0; b2 < 256; b2++) o.cls[b2] = C.dfa_cls[dd.cls_off + b2];
                 comps[k] = &o;
             }
-            std::vector<uint32_t> ord(D.n_rloc);
-            for (uint32_t i = 0; i < ord.size(); i++) ord[i] = i;
+            // anchored (^) and unanchored regexes in separate groups, each in config order: a
+            // union of anchored regexes dies within a few bytes of most URIs; the groups are then
+            // ordered by their first (lowest) member
+            std::vector<uint32_t> ord_a, ord_u;
+            for (uint32_t k = 0; k < D.n_rloc; k++) (comps[k]->anchored_start ? ord_a : ord_u).push_back(k);
+            std::vector<std::vector<uint32_t>> gm_a, gm_u;
+            std::vector<MultiDfa> gd_a, gd_u;
+            std::vector<uint32_t> single;
+            form_groups(comps, ord_a, [](uint32_t, uint32_t) { return true; }, gm_a, gd_a, single);
+            form_groups(comps, ord_u, [](uint32_t, uint32_t) { return true; }, gm_u, gd_u, single);
+            if (!single.empty()) { h.n_rk_prefilter++; continue; }
             std::vector<std::vector<uint32_t>> gmem;
             std::vector<MultiDfa> gdfa;
-            std::vector<uint32_t> single;
-            form_groups(comps, ord, [](uint32_t, uint32_t) { return true; }, gmem, gdfa, single);
-            if (!single.empty()) { h.n_rk_prefilter++; continue; }
+            for (size_t ia = 0, iu = 0; ia < gm_a.size() || iu < gm_u.size();) {
+                const bool take_a = iu == gm_u.size() || (ia < gm_a.size() && gm_a[ia][0] < gm_u[iu][0]);
+                if (take_a) { gmem.push_back(gm_a[ia]); gdfa.push_back(std::move(gd_a[ia])); ia++; }
+                else { gmem.push_back(gm_u[iu]); gdfa.push_back(std::move(gd_u[iu])); iu++; }
+            }
             D.rsl_first = (uint32_t)alw_slices.size();
             const uint32_t fr = D.first_rloc;
             pack_slices(gmem, gdfa, [&](size_t j, size_t k) { return fr + gmem[j][k]; },
                         [](size_t, size_t) { return 1u; }, (uint32_t)Sv.id);
             D.rsl_n = (uint32_t)alw_slices.size() - D.rsl_first;
+            for (uint32_t k = D.rsl_first; k < D.rsl_first + D.rsl_n; k++)
+                alw_slices[k].min_member = alw_rule[alw[alw_slices[k].first_group].first];
             st.n_rsl_slices += D.rsl_n;
         }
     }

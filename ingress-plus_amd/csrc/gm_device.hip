@@ -1359,6 +1359,8 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
                 }
                 HIPCHK(c, hipGetLastError());
             }
+            k_rloc_fin<<<(uint32_t)c->cu_count * 4, 256, 0, rs>>>(t, q.list, q.count, q.loc);
+            HIPCHK(c, hipGetLastError());
         }
         if (t.n_rk_prefilter)
             k_rloc<<<(uint32_t)c->cu_count * 4, RLOC_BLOCK, 0, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen);

@@ -285,7 +285,8 @@ struct DAlwSlice {
     uint32_t first_group, n_groups;
     uint32_t zones;          // zones some group scans
     uint32_t server;         // regex-location slices: the server (GM_NONE: always-run regexes)
-    uint32_t pad[2];
+    uint32_t min_member;     // regex-location slices: the lowest regex-location index it holds
+    uint32_t pad;
 };
 
 struct TabHeader {
