@@ -1423,7 +1423,15 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     // GM_CREATE_SERIAL (measurement): the route alone first, on the caller's stream.
     const bool serial = c->flags & GM_CREATE_SERIAL;
     hipStream_t rs = serial ? s : S->side;
-    if (!serial) {
+    // GM_EXP_ROUTE_AFTER (measurement build): the route after the scan, beside the context
+    // filter -- the scan alone runs 3.4-3.8 ms instead of 4.8, but the step is longer (6.46 vs
+    // 5.89 ms per 10M C4 requests): the route beside the scan is the shipped schedule
+#ifdef GM_EXP_ROUTE_AFTER
+    constexpr bool route_after = true;
+#else
+    constexpr bool route_after = false;
+#endif
+    if (!serial && !route_after) {
         HIPCHK(c, hipEventRecord(S->ev_fork, s));
         HIPCHK(c, hipStreamWaitEvent(S->side, S->ev_fork, 0));
     }
@@ -1431,7 +1439,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         // beside the scan, 2 route blocks per CU: 1 leaves the route the tail of the step, 3+
         // steal issue slots from the scan (measured on C4: 6.75 / 5.88 / 5.99 ms per step)
         const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
-                                                                     (uint32_t)c->cu_count * (serial ? 8 : 2)));
+                                                                     (uint32_t)c->cu_count * (serial || route_after ? 8 : 2)));
         if (prof) HIPCHK(c, hipEventRecord(S->ev_route[0], rs));
         // raised issue priority beside the scan: the route's short latency-bound waves finish
         // early instead of stretching past the scan
@@ -1456,6 +1464,10 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
     else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
     HIPCHK(c, hipGetLastError());
+    if (!serial && route_after) {   // the route beside the context filter, after the scan
+        HIPCHK(c, hipEventRecord(S->ev_fork, s));
+        HIPCHK(c, hipStreamWaitEvent(S->side, S->ev_fork, 0));
+    }
     if (!serial && (e = launch_route())) return e;
     if (mark(2)) return GM_E_HIP;
     const uint32_t bcap = (uint32_t)std::min<size_t>(S->cap_surv / scan_blocks, 0xFFFFFFFFu);
