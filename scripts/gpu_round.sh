@@ -19,7 +19,7 @@ if [ -z "$NO_BENCH" ]; then
 fi
 if [ -n "$PROF" ]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 1 --no-cpu > "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}.log" 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 1 --no-cpu --stress-requests 0 > "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}.log" 2>&1
   rc=$?
   tail -2 "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}.log"
   [ $rc -eq 0 ] || exit $rc
