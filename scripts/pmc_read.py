@@ -4,7 +4,7 @@ import csv
 import glob
 import sys
 
-for p in ("sq", "lds"):
+for p in ("sq", "lds", "fetch"):
     fs = glob.glob(f"{sys.argv[1]}_{p}/**/*counter_collection.csv", recursive=True)
     if not fs:
         continue
