@@ -105,3 +105,35 @@ def test_oracle_under_sanitizers(harnesses, tmp_path):
     err = r.stderr.decode(errors="replace")
     assert r.returncode == 0 and "runtime error" not in err and "AddressSanitizer" not in err, err[-4000:]
     assert r.stdout.decode().count("requests ok") == len(traffic)
+
+
+def test_union_dfa_under_sanitizers(harnesses, tmp_path):
+    """The union DFAs (gm_regex.cpp build_multi + minimize_multi) under ASan/UBSan, and their
+    answers: for groups of 1..32 regexes -- the always-run shapes of the WAF stress set and of the
+    parity test, and C3's regex locations -- every member's bit equals its own search DFA's answer
+    on random subjects (empty ones, a final newline, anchors)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_gpu_parity import always_rules
+    pats = [(r.nocase, r.pattern) for r in always_rules()]
+    pats += [(r.nocase, r.pattern) for r in sigs.gen_waf_sigset_stress(200, 300).rules if r.kind == "re"][:120]
+    pats += [(ci, pat) for (pat, ci, *_r) in workloads.c3_regexes(300)]
+    (tmp_path / "re.txt").write_text("".join(f"{int(ci)} {p}\n" for ci, p in pats))
+    rng = np.random.Generator(np.random.PCG64(5))
+    alpha = "abcdefghij0123456789-=<>/. xzqAB'\\"
+    subj = []
+    for _ in range(400):
+        s = "".join(alpha[int(i)] for i in rng.integers(0, len(alpha), int(rng.integers(0, 60))))
+        if rng.random() < 0.3:
+            s = "/" + s
+        if rng.random() < 0.2:
+            s += "\\n"
+        subj.append(s)
+    (tmp_path / "subj.txt").write_text("\n".join(subj) + "\n")
+    exe = os.path.join(SAN, "union_harness")
+    r = subprocess.run([exe, str(tmp_path / "re.txt"), str(tmp_path / "subj.txt")], capture_output=True,
+                       timeout=1200, env=ENV)
+    err = r.stderr.decode(errors="replace")
+    assert r.returncode == 0 and "runtime error" not in err and "AddressSanitizer" not in err, err[-4000:]
+    out = r.stdout.decode()
+    assert "mismatches 0" in out and int(out.split("groups ")[1].split()[0]) >= 10, out
