@@ -168,6 +168,23 @@ def main():
                      "algorithmic_bytes_per_launch": zone_bytes},
     }
     result["roofline"].update(pmc_traffic())
+    if world == 1 and not args.serial:
+        # the scan kernel alone (GM_CREATE_SERIAL: the route first, then the scan on its own), on
+        # the same resident batch: its own roofline fraction beside the in-pipeline one above,
+        # where the route shares the CUs
+        eng_s = engine.Engine(local, profile=True, serial=True)
+        eng_s.load(gblob, 1)
+        alone = []
+        for k in range(1 + 3):
+            eng_s.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), arena_len, n, d_out.data_ptr(), d_hits.data_ptr(),
+                            hit_cap, stream.cuda_stream)
+            eng_s.sync(stream.cuda_stream)
+            if k:
+                alone.append(eng_s.stats()["last_ms_scan"])
+        eng_s.close()
+        a_ms = float(np.mean(alone))
+        result["roofline"]["scan_alone_ms"] = a_ms
+        result["roofline"]["frac_alone"] = zone_bytes / (a_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
     if world == 1 and args.stress_requests > 0:
         del d_arena, d_reqs, d_out, d_hits
         torch.cuda.empty_cache()

@@ -580,8 +580,15 @@ __device__ __forceinline__ uint32_t flags_nibble(uint32_t f) { return ((f >> 7) 
 // position masks; ngx_http_validate_host's rules then follow from the masks (".." = adjacent
 // dots; the first ':' ends the host; the last '.' is stripped when it ends the host).  A host
 // starting with '[' (IPv6 literal) takes the byte loop.
-__device__ __forceinline__ int host_fast(const uint32_t (&hw)[8], uint32_t n, const GTab &t, uint32_t pi,
-                                         uint32_t &server) {
+// The route's hot tables (gm_tables.hpp ROUTE_STAGE_BYTES): the block's LDS copy when they fit,
+// else the image.  Kept apart from GTab and passed by value: a modified local copy of the whole
+// GTab (~600 B) lived in scratch, and every table pointer the route read was a scratch load.
+struct HotTabs {
+    const DPort *ports; const DName *names; const DServer *servers; const DServerIf *server_ifs;
+    const DSmallLoc *small; const DLoc *locs; const uint8_t *name_bytes;
+};
+__device__ __forceinline__ int host_fast(const uint32_t (&hw)[8], uint32_t n, const GTab &t, const HotTabs &h,
+                                         uint32_t pi, uint32_t &server) {
     server = GM_NONE;
     int host_len;
     if ((hw[0] & 0xFF) == '[') {
@@ -624,11 +631,11 @@ __device__ __forceinline__ int host_fast(const uint32_t (&hw)[8], uint32_t n, co
     }
     hs = name_hash_fin(hs, pi);
     for (uint32_t i = hs & t.names_mask;; i = (i + 1) & t.names_mask) {
-        const DName e = t.names[i];
+        const DName e = h.names[i];
         if (e.hash == 0) break;
         if (e.hash == hs && e.port_idx == pi && e.name_len == (uint32_t)host_len) {
             uint32_t tw[8];
-            load_span32(t.name_bytes, e.name_off, ~0ull, tw);   // the name strings end with 64 B of slack
+            load_span32(h.name_bytes, e.name_off, ~0ull, tw);   // the name strings end with 64 B of slack
             uint32_t diff = 0;
 #pragma unroll
             for (int k = 0; k < 8; k++) {
@@ -756,16 +763,16 @@ constexpr uint32_t RLOC_STATUS_WORD = 16;   // batch status word: requests defer
 // (the location index, -1 none).  *sid_out: the server chosen (valid whenever *pend is set).
 constexpr int32_t RK_INLINE = -3, RK_DEFER = -2;
 __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const RoutePre &pre,
-                          const GTab &t, RouteOut &o, const uint32_t *rkb, int32_t rk_in = RK_INLINE,
+                          const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb, int32_t rk_in = RK_INLINE,
                           bool *pend = nullptr) {
     o.server = GM_NONE; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0;
     o.action = GM_ACT_NO_LISTENER; o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF;
     const uint64_t f_uri = r.base, f_host = r.base + r.uri_len + r.args_len + r.hdr_len + r.body_len;
     // ---- listen port
     uint32_t pi = GM_NONE;
-    for (uint32_t i = 0; i < t.n_ports; i++) if (t.ports[i].port == r.port) { pi = i; break; }
+    for (uint32_t i = 0; i < t.n_ports; i++) if (h.ports[i].port == r.port) { pi = i; break; }
     if (pi == GM_NONE) return;
-    const DPort P = t.ports[pi];
+    const DPort P = h.ports[pi];
     const bool https = r.flags & GM_REQ_HTTPS;
     if (https && !P.ssl) return;
     uint32_t sid = P.default_server;
@@ -779,28 +786,28 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
         uint32_t s = GM_NONE;
         int hl;
         if (r.host_len <= 32) {
-            hl = host_fast(pre.hw, r.host_len, t, pi, s);
+            hl = host_fast(pre.hw, r.host_len, t, h, pi, s);
         } else {
             hl = validate_host(A + f_host, r.host_len);
-            if (hl >= 0) s = name_probe(t.names, t.names_mask, t.name_bytes, A + f_host, 0, (uint32_t)hl, pi);
+            if (hl >= 0) s = name_probe(h.names, t.names_mask, h.name_bytes, A + f_host, 0, (uint32_t)hl, pi);
         }
         if (hl < 0) bad = true;
         else {
-            if (s == GM_NONE) s = host_wildcards(A + f_host, hl, t, pi);
+            if (s == GM_NONE) s = host_wildcards(A + f_host, hl, *t.self, pi);
             if (s != GM_NONE) sid = s;
         }
     }
     o.server = sid;
     if (bad || (P.ssl && !https)) { o.action = GM_ACT_BAD_REQUEST; o.status = 400; return; }
-    const DServer S = t.servers[sid];
+    const DServer S = h.servers[sid];
     // ---- server rewrite phase
     for (uint32_t i = 0; i < S.n_if; i++) {
-        const DServerIf f = t.server_ifs[S.first_if + i];
+        const DServerIf f = h.server_ifs[S.first_if + i];
         bool hit;
         if (f.op == SIF_RETURN) hit = true;
         else if (f.op == SIF_FLAGS) hit = (f.tt >> (r.flags & 3)) & 1u;
         else if (f.op == 0xFF) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; return; }
-        else hit = server_if_generic(A, rp, t, S.first_if + i) != 0;
+        else hit = server_if_generic(A, rp, *t.self, S.first_if + i) != 0;
         if (hit) { o.action = is_redirect(f.code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = f.code; return; }
     }
     // ---- location: trie walk (exact, longest prefix, auto_redirect), then regex locations.
@@ -815,7 +822,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
         // small server: compare the URI's first 16 bytes with every location-carrying node
         uint32_t bestlen = 0;
         for (uint32_t j = 0; j < S.sl_n; j++) {
-            const DSmallLoc E = t.small[S.sl_first + j];
+            const DSmallLoc E = h.small[S.sl_first + j];
             if (E.len > r.uri_len) continue;
             uint32_t diff = 0;
 #pragma unroll
@@ -869,29 +876,29 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
         else if (far >= 0) { o.loc = (uint32_t)far; o.action = GM_ACT_AUTO_301; o.status = 301; return; }
     }
     if (loc < 0) {
-        if (best >= 0 && t.locs[best].noregex) loc = best;
+        if (best >= 0 && h.locs[best].noregex) loc = best;
         else {
             if (S.rk_on && rk_in >= -1) loc = rk_in;
             else if (S.rk_on && rk_in == RK_DEFER &&
                      (S.rsl_n || (r.uri_len <= RLOC_URI_CAP && S.n_rloc <= RLOC_BM_BITS))) {
                 *pend = true;
                 return;
-            } else loc = rloc_first_match(t, S, sid, u, r.uri_len, rkb);
+            } else loc = rloc_first_match(*t.self, S, sid, u, r.uri_len, rkb);
             if (loc < 0) loc = best;
         }
     }
     if (loc < 0) { o.action = GM_ACT_NOT_FOUND; o.status = 404; return; }
     o.loc = (uint32_t)loc;
-    DLoc L = t.locs[loc];
+    DLoc L = h.locs[loc];
     uint32_t fin = (uint32_t)loc;
     if (L.kind == LK_IRL_RULES) {
         const DRules R = t.rules[L.route];
-        const uint8_t idx = rules_generic(A, rp, t, L.route);
+        const uint8_t idx = rules_generic(A, rp, *t.self, L.route);
         o.kind = GM_ROUTE_RULES; o.match = idx;
         fin = idx == 0xFF ? R.default_target : t.rtargets[R.first_target + idx];
     } else if (L.kind == LK_IRL_SPLIT) {
         o.kind = GM_ROUTE_SPLIT;
-        const uint32_t k = split_generic(A, rp, t, L.route);
+        const uint32_t k = split_generic(A, rp, *t.self, L.route);
         if (k == 0xFFFFFFFFu) { o.action = GM_ACT_UNSUPPORTED; return; }
         fin = GM_NONE;
         if (k != 0xFFu) { o.bucket = (uint8_t)k; fin = t.parts[t.splits[L.route].first_part + k].target; }
@@ -900,7 +907,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
     }
     if (L.kind == LK_IRL_RULES || L.kind == LK_IRL_SPLIT) {
         if (fin == GM_NONE) { o.action = GM_ACT_ERRPAGE; o.status = 302; return; }
-        L = t.locs[fin];
+        L = h.locs[fin];
         if (L.kind != LK_PROXY && L.kind != LK_RETURN && L.kind != LK_NONE) { o.action = GM_ACT_UNSUPPORTED; return; }
     }
     if (L.kind == LK_RETURN) { o.action = is_redirect(L.ret_code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = L.ret_code; return; }
@@ -938,21 +945,20 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
     // the generation's hot tables in LDS (gm_tables.hpp ROUTE_STAGE_BYTES): every pointer into
     // the hot prefix is rebased onto the block's copy; generic (flat) loads then hit LDS
     __shared__ uint4 hot[ROUTE_STAGE_BYTES / 16];
-    GTab t = tg;
+    const GTab &t = tg;
+    HotTabs h{tg.ports, tg.names, tg.servers, tg.server_ifs, tg.small, tg.locs, tg.name_bytes};
     if (tg.hot_len) {
         const uint4 *src = reinterpret_cast<const uint4 *>(tg.hot_base);
         for (uint32_t k = threadIdx.x; k < tg.hot_len / 16; k += blockDim.x) hot[k] = src[k];
         const uint8_t *lb = reinterpret_cast<const uint8_t *>(hot);
         auto rb = [&](const void *p) { return lb + (reinterpret_cast<const uint8_t *>(p) - tg.hot_base); };
-        t.ports = (const DPort *)rb(tg.ports);
-        t.names = (const DName *)rb(tg.names);
-        t.wild_head = (const DName *)rb(tg.wild_head);
-        t.wild_tail = (const DName *)rb(tg.wild_tail);
-        t.servers = (const DServer *)rb(tg.servers);
-        t.server_ifs = (const DServerIf *)rb(tg.server_ifs);
-        t.small = (const DSmallLoc *)rb(tg.small);
-        t.locs = (const DLoc *)rb(tg.locs);
-        t.name_bytes = rb(tg.name_bytes);
+        h.ports = (const DPort *)rb(tg.ports);
+        h.names = (const DName *)rb(tg.names);
+        h.servers = (const DServer *)rb(tg.servers);
+        h.server_ifs = (const DServerIf *)rb(tg.server_ifs);
+        h.small = (const DSmallLoc *)rb(tg.small);
+        h.locs = (const DLoc *)rb(tg.locs);
+        h.name_bytes = rb(tg.name_bytes);
     }
     const bool use_hist = t.n_locs <= LDS_HIST_MAX;
     if (use_hist) for (uint32_t k = threadIdx.x; k < t.n_locs; k += blockDim.x) hist[k] = 0;
@@ -968,7 +974,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
         route_prefetch(A, arena_len, r, pre);
         RouteOut o;
         bool pend = false;
-        route_one(A, arena_len, reqs + i, r, pre, t, o, RK ? rkb : nullptr,
+        route_one(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
                   TAIL ? q.loc[x] : (RK && q.list ? RK_DEFER : RK_INLINE), &pend);
         if (RK && !TAIL) {   // deferred to k_rloc: appended, one atomic per wave
             const unsigned long long pm = __ballot(pend);
@@ -1037,6 +1043,7 @@ struct Generation {
     uint8_t *d_image = nullptr;
     unsigned long long *d_counters = nullptr;       // this device's cumulative counters
     unsigned long long *d_counters_sum = nullptr;   // gm_counters_allreduce's out-of-place result
+    GTab *d_gtab = nullptr;                         // tab in device memory (GTab::self)
     size_t n_counters = 0;
     TabHeader hdr{};
     GTab tab{};
@@ -1045,7 +1052,7 @@ struct Generation {
     std::vector<std::string> peer_addrs;   // gm_peer_address
     std::vector<uint32_t> peer_ups;
     ~Generation() {
-        for (void *p : {(void *)d_image, (void *)d_counters, (void *)d_counters_sum})
+        for (void *p : {(void *)d_image, (void *)d_counters, (void *)d_counters_sum, (void *)d_gtab})
             if (p) (void)hipFree(p);
     }
 };
@@ -1252,6 +1259,9 @@ int gm_load_generation(gm_ctx *c, const void *blob, size_t len, uint32_t gen) {
         HIPCHK(c, hipMalloc((void **)&g->d_image, R.image.size()));
         HIPCHK(c, hipMemcpy(g->d_image, R.image.data(), R.image.size(), hipMemcpyHostToDevice));
         g->tab = make_gtab(g->hdr, g->d_image, gen);
+        HIPCHK(c, hipMalloc((void **)&g->d_gtab, sizeof(GTab)));
+        g->tab.self = g->d_gtab;
+        HIPCHK(c, hipMemcpy(g->d_gtab, &g->tab, sizeof(GTab), hipMemcpyHostToDevice));
         g->n_counters = g->stats.n_counters;
         const size_t cb = std::max<size_t>(g->n_counters, 1) * 8;
         HIPCHK(c, hipMalloc((void **)&g->d_counters, cb));

@@ -350,6 +350,9 @@ struct GTab {                // device pointers, built on host from the image ba
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
     uint32_t gen;
+    // this struct's copy in device memory: a kernel hands *self (not its kernel argument) to
+    // out-of-line device functions, so the ~600-byte argument is not copied to scratch
+    const GTab *self;
 };
 
 // hashing shared by compiler and kernels
