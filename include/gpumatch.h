@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 3u
+#define GM_ABI_VERSION 4u   /* 4: gm_stats_t grew the union-DFA fields */
 
 /* ---------------------------------------------------------------- status codes */
 #define GM_OK            0

@@ -1433,6 +1433,12 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     // GM_CREATE_SERIAL (measurement): the route alone first, on the caller's stream.
     const bool serial = c->flags & GM_CREATE_SERIAL;
     hipStream_t rs = serial ? s : S->side;
+#ifndef GM_ROUTE_BPC
+#define GM_ROUTE_BPC 2   // route blocks per CU beside the scan (1: 5.86, 2: 5.41, 3: 5.60 ms per C4 step)
+#endif
+#ifndef GM_ROUTE_PRIO
+#define GM_ROUTE_PRIO 0  // 1: the route at raised issue priority beside the scan (5.32 vs 5.06 ms per C4 step)
+#endif
     // GM_EXP_ROUTE_AFTER (measurement build): the route after the scan, beside the context
     // filter -- the scan alone runs 3.4-3.8 ms instead of 4.8, but the step is longer (6.46 vs
     // 5.89 ms per 10M C4 requests): the route beside the scan is the shipped schedule
@@ -1449,14 +1455,14 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         // beside the scan, 2 route blocks per CU: 1 leaves the route the tail of the step, 3+
         // steal issue slots from the scan (measured on C4: 6.75 / 5.88 / 5.99 ms per step)
         const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
-                                                                     (uint32_t)c->cu_count * (serial || route_after ? 8 : 2)));
+                                                                     (uint32_t)c->cu_count * (serial || route_after ? 8 : GM_ROUTE_BPC)));
         if (prof) HIPCHK(c, hipEventRecord(S->ev_route[0], rs));
         // raised issue priority beside the scan: the route's short latency-bound waves finish
         // early instead of stretching past the scan
         if (rk)
-            k_route<5, true><<<nb, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1, dlen, q);
+            k_route<5, true><<<nb, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, q);
         else
-            k_route<5><<<nb, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, 1, dlen);
+            k_route<5><<<nb, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen);
         HIPCHK(c, hipGetLastError());
         int e3;
         if (rk && (e3 = launch_rloc(rs, nb))) return e3;

@@ -18,6 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GM_LIB") or os.path.join(os.path.dirname(HERE), "libgpumatch.so")
 
 GM_OK = 0
+GM_ABI_VERSION = 4   # include/gpumatch.h
 GM_E_OVERFLOW = -4
 GM_CREATE_COMPILE_ONLY = 0x1
 GM_BATCH_HOST = 0x1
@@ -74,6 +75,8 @@ def lib():
         L.gm_create.argtypes = [ctypes.c_int, ctypes.c_uint32]
         L.gm_destroy.argtypes = [ctypes.c_void_p]
         L.gm_abi_version.restype = ctypes.c_uint32
+        if L.gm_abi_version() != GM_ABI_VERSION:   # the structs below mirror this ABI exactly
+            raise ImportError(f"{LIB_PATH}: ABI {L.gm_abi_version()}, this binding expects {GM_ABI_VERSION}")
         L.gm_load_generation.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32]
         L.gm_match_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(GmBatch), ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_size_t, ctypes.c_void_p]

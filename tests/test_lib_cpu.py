@@ -25,7 +25,7 @@ def test_exports_every_declared_symbol():
     assert set(engine.EXPORTS) <= syms
     for s in sorted(syms):
         assert hasattr(L, s), s
-    assert L.gm_abi_version() == 3
+    assert L.gm_abi_version() == engine.GM_ABI_VERSION
 
 
 @pytest.fixture(scope="module")
