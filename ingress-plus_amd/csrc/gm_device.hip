@@ -94,42 +94,41 @@ __device__ void ctx_init(Ctx &c, const uint8_t *A, const Rec &r) {
     c.ruri = o; o += r.ruri_len; c.raddr = o;
 }
 
-// first position of byte `ch` in A[p, e), or e: aligned 16-byte loads, SWAR zero-byte test per
-// word (the lowest flagged byte of (x - 0x01..) & ~x & 0x80.. is always a true match); only
-// words wholly inside [p, e) are read
-__device__ uint64_t find_byte(const uint8_t *A, uint64_t p, uint64_t e, uint32_t ch) {
-    const uint32_t pat = ch * 0x01010101u;
-    while (p < e && (p & 15)) { if (A[p] == ch) return p; p++; }
-    for (; p + 16 <= e; p += 16) {
-        const uint4 q = *reinterpret_cast<const uint4 *>(A + p);
-        const uint32_t w[4] = {q.x ^ pat, q.y ^ pat, q.z ^ pat, q.w ^ pat};
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t z = (w[k] - 0x01010101u) & ~w[k] & 0x80808080u;
-            if (z) return p + 4 * k + (__builtin_ctz(z) >> 3);
-        }
-    }
-    for (; p < e; p++) if (A[p] == ch) return p;
-    return e;
+// exact per-byte flags (bit 7 of each byte) of the zero bytes of x
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
 }
-
-// first position of either byte in A[p, e), or e (find_byte with two patterns: the lowest flag
-// of each SWAR mask is a true match, so the lowest flag of their union is the first match)
-__device__ uint64_t find_byte2(const uint8_t *A, uint64_t p, uint64_t e, uint32_t c1, uint32_t c2) {
-    const uint32_t p1 = c1 * 0x01010101u, p2 = c2 * 0x01010101u;
-    while (p < e && (p & 15)) { if (A[p] == c1 || A[p] == c2) return p; p++; }
-    for (; p + 16 <= e; p += 16) {
-        const uint4 q = *reinterpret_cast<const uint4 *>(A + p);
+// the first position of a byte flagged by `hit` (per-word flags) in A[p, e), or e: whole aligned
+// 16-byte blocks (the first and the last masked to [p, e): an aligned block never leaves the
+// allocation), exact SWAR flags per word
+template <class F>
+__device__ __forceinline__ uint64_t find_flagged(const uint8_t *A, uint64_t p, uint64_t e, F hit) {
+    if (p >= e) return e;
+    for (uint64_t b = p & ~15ull; b < e; b += 16) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(A + b);
         const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const uint32_t a = w[k] ^ p1, b = w[k] ^ p2;
-            const uint32_t z = ((a - 0x01010101u) & ~a & 0x80808080u) | ((b - 0x01010101u) & ~b & 0x80808080u);
-            if (z) return p + 4 * k + (__builtin_ctz(z) >> 3);
+            uint32_t z = hit(w[k]);
+            const uint64_t wb = b + 4 * k;   // bytes [wb, wb + 4)
+            if (p > wb) z = p - wb >= 4 ? 0u : z & (~0u << (8 * (uint32_t)(p - wb)));
+            if (wb + 4 > e) z = e <= wb ? 0u : z & ((1u << (8 * (uint32_t)(e - wb))) - 1u);
+            if (z) return wb + (__builtin_ctz(z) >> 3);
         }
     }
-    for (; p < e; p++) if (A[p] == c1 || A[p] == c2) return p;
     return e;
+}
+
+// first position of byte `ch` in A[p, e), or e
+__device__ uint64_t find_byte(const uint8_t *A, uint64_t p, uint64_t e, uint32_t ch) {
+    const uint32_t pat = ch * 0x01010101u;
+    return find_flagged(A, p, e, [pat](uint32_t w) { return zero_bytes(w ^ pat); });
+}
+
+// first position of either byte in A[p, e), or e
+__device__ uint64_t find_byte2(const uint8_t *A, uint64_t p, uint64_t e, uint32_t c1, uint32_t c2) {
+    const uint32_t p1 = c1 * 0x01010101u, p2 = c2 * 0x01010101u;
+    return find_flagged(A, p, e, [p1, p2](uint32_t w) { return zero_bytes(w ^ p1) | zero_bytes(w ^ p2); });
 }
 
 // iterate "Name: value\r\n" lines (ngx_http_parse_header_line); returns false at end
