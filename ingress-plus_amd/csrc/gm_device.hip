@@ -523,6 +523,21 @@ struct RouteOut {
 
 // 32 arena bytes starting at `off` (any alignment) as 8 little-endian dwords, from three aligned
 // 16-B loads; blocks starting at or beyond `lim` are not read (zero).  Callers mask by length.
+// w = the 32 bytes from byte r (0..15) of the 48 in d: the dword offset r >> 2 picked with bit
+// selects (v_bfi: a per-lane select of registers, where `qd == 0 ? d[k] : ...` compiled to
+// branches and scratch), then a byte funnel shift
+__device__ __forceinline__ void funnel32(const uint32_t (&d)[12], uint32_t r, uint32_t (&w)[8]) {
+    const uint32_t m1 = 0u - ((r >> 2) & 1u), m2 = 0u - ((r >> 3) & 1u);
+    uint32_t sdw[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        const uint32_t a = (d[k + 1] & m1) | (d[k] & ~m1);
+        const uint32_t b = (d[k + 3] & m1) | (d[k + 2] & ~m1);
+        sdw[k] = (b & m2) | (a & ~m2);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = __builtin_amdgcn_alignbyte(sdw[k + 1], sdw[k], r & 3);
+}
 __device__ __forceinline__ void load_span32(const uint8_t *A, uint64_t off, uint64_t lim, uint32_t (&w)[8]) {
     const uint64_t a = off & ~15ull;
     uint32_t d[12];
@@ -532,13 +547,7 @@ __device__ __forceinline__ void load_span32(const uint8_t *A, uint64_t off, uint
         if (a + 16 * b < lim) q = *reinterpret_cast<const uint4 *>(A + a + 16 * b);
         d[4 * b] = q.x; d[4 * b + 1] = q.y; d[4 * b + 2] = q.z; d[4 * b + 3] = q.w;
     }
-    const uint32_t r = (uint32_t)(off & 15), qd = r >> 2, sh = r & 3;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const uint32_t lo = qd == 0 ? d[k] : qd == 1 ? d[k + 1] : qd == 2 ? d[k + 2] : d[k + 3];
-        const uint32_t hi = qd == 0 ? d[k + 1] : qd == 1 ? d[k + 2] : qd == 2 ? d[k + 3] : d[k + 4];
-        w[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
-    }
+    funnel32(d, (uint32_t)(off & 15), w);
 }
 
 // load_span32 restricted to the aligned 16-byte blocks that hold [off, off + nbytes) (nbytes <=
@@ -554,13 +563,7 @@ __device__ __forceinline__ void load_span_n(const uint8_t *A, uint64_t off, uint
         if ((uint32_t)b < nb && a + 16 * b < lim) q = *reinterpret_cast<const uint4 *>(A + a + 16 * b);
         d[4 * b] = q.x; d[4 * b + 1] = q.y; d[4 * b + 2] = q.z; d[4 * b + 3] = q.w;
     }
-    const uint32_t qd = r >> 2, sh = r & 3;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const uint32_t lo = qd == 0 ? d[k] : qd == 1 ? d[k + 1] : qd == 2 ? d[k + 2] : d[k + 3];
-        const uint32_t hi = qd == 0 ? d[k + 1] : qd == 1 ? d[k + 2] : qd == 2 ? d[k + 3] : d[k + 4];
-        w[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
-    }
+    funnel32(d, r, w);
 }
 
 __device__ __forceinline__ uint32_t byte_of(const uint32_t (&w)[8], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xFF; }
