@@ -125,6 +125,13 @@ _EDGE = [
     b"GET / HTTP/1.1\r\nHost: a\r\nX-Long: " + b"v" * 9000 + b"\r\n\r\n",   # header line > 8 KiB: 400
     b"GET / HTTP/1.1\r\nHost: a\r\n" + b"X-H: 1\r\n" * 300 + b"\r\n",       # > 254 header lines: 400
     b"GET / HTTP/1.1\r\nHost: a\r\n" + b"X-H: 1\r\n" * 200 + b"\r\n",       # 201 lines: ok
+    b"GET /a/. HTTP/1.1\r\nHost: a\r\n\r\n",                                # trailing "/."
+    b"GET /a/.b#f HTTP/1.1\r\nHost: a\r\n\r\n",                             # "/." not a segment
+    b"GET /a\0b HTTP/1.1\r\nHost: a\r\n\r\n",                               # NUL in the target: 400
+    b"GET /a\0b?q HTTP/1.1\r\nHost: a\r\n\r\n",
+    b"GET /" + b"s" * 1500 + b"?" + b"q" * 900 + b" HTTP/1.1\r\nHost: a\r\n\r\n",      # long, simple
+    b"GET /" + b"s" * 1500 + b"//x%41 HTTP/1.1\r\nHost: a\r\n\r\n",         # long, complex late
+    b"GET http://h:8/x/../y HTTP/1.1\r\nHost: a\r\n\r\n",                    # absolute, dot segment
 ]
 
 
