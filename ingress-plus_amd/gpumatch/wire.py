@@ -132,6 +132,9 @@ _EDGE = [
     b"GET /" + b"s" * 1500 + b"?" + b"q" * 900 + b" HTTP/1.1\r\nHost: a\r\n\r\n",      # long, simple
     b"GET /" + b"s" * 1500 + b"//x%41 HTTP/1.1\r\nHost: a\r\n\r\n",         # long, complex late
     b"GET http://h:8/x/../y HTTP/1.1\r\nHost: a\r\n\r\n",                    # absolute, dot segment
+    b"GET / HTTP/1.1\r\nHost: a\r\nX: v \nY: w\r\n\r\n",                    # trailing SP, bare LF
+    b"GET / HTTP/1.1\r\nHost: a\r\nX: v\r\r\nY: \r\nZ:\r\n\r\n",             # CR in a value, empties
+    b"GET / HTTP/1.1\r\nHost: a\r\nX:  v\r\nY:v\r\n\r\n",                    # two spaces, none
 ]
 
 
