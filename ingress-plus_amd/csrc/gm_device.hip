@@ -1087,6 +1087,7 @@ struct Scratch {
     uint64_t *d_wsize = nullptr, *d_wbase = nullptr; size_t cap_wsize = 0, cap_wbase = 0;   // wire parser
     uint8_t *d_wtemp = nullptr; size_t cap_wtemp = 0;
     uint8_t *d_wscr = nullptr; size_t cap_wscr = 0;   // the wire parser's per-wave $uri scratch
+    uint8_t *d_wsum = nullptr; size_t cap_wsum = 0;   // and its pass-1 summaries (WireSum, 80 B each)
     uint32_t *d_pk = nullptr; size_t cap_pk = 0;     // peer selection: keys, values (x2: sorted),
     uint32_t *d_pseg = nullptr; size_t cap_pseg = 0; // per-upstream ranges, periodic programs
     uint4 *d_pprog = nullptr; size_t cap_pprog = 0;
@@ -1104,7 +1105,7 @@ struct Scratch {
     ~Scratch() {
         for (void *p : {(void *)d_status, (void *)d_blk2rec, (void *)d_cand, (void *)d_surv, (void *)d_pairs,
                         (void *)d_jobs, (void *)d_set, (void *)d_cnt, (void *)d_start, (void *)d_ccnt,
-                        (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp, (void *)d_wscr,
+                        (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp, (void *)d_wscr, (void *)d_wsum,
                         (void *)d_pk, (void *)d_pseg, (void *)d_pprog, (void *)d_ppat, (void *)d_ptemp,
                         (void *)d_usize, (void *)d_utemp, (void *)d_sreqs, (void *)d_sarena, (void *)d_sblk,
                         (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql})
@@ -1963,11 +1964,14 @@ extern "C" int gm_parse_requests(gm_ctx *c, const uint8_t *wire, const gm_wire_m
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + WIRE_WAVES - 1) / WIRE_WAVES,
                                                                      (uint32_t)c->cu_count * 16));
     if ((e = grow(c, s, S->d_wscr, S->cap_wscr, (size_t)blocks * WIRE_WAVES * WIRE_SCR))) return e;
-    k_wire_size<<<blocks, 64 * WIRE_WAVES, 0, s>>>(wire, msgs, n, S->d_wsize, S->d_wscr);
+    if ((e = grow(c, s, S->d_wsum, S->cap_wsum, (size_t)n * sizeof(WireSum)))) return e;
+    WireSum *wsum = reinterpret_cast<WireSum *>(S->d_wsum);
+    k_wire_size<<<blocks, 64 * WIRE_WAVES, 0, s>>>(wire, msgs, n, S->d_wsize, S->d_wscr, wsum);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_wtemp, tmp, S->d_wsize, S->d_wbase, (int)n + 1, s));
     k_wire_emit<<<blocks, 64 * WIRE_WAVES, 0, s>>>(wire, msgs, n, S->d_wsize, S->d_wbase, reqs, arena, arena_cap,
-                                                   arena_len_dev, S->d_status + PARSE_STATUS_WORD, S->d_wscr);
+                                                   arena_len_dev, S->d_status + PARSE_STATUS_WORD, S->d_wscr,
+                                                   wsum);
     HIPCHK(c, hipGetLastError());
     return GM_OK;
 }

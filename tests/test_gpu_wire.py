@@ -22,9 +22,9 @@ def env():
     return torch, torch.device("cuda", 0), engine.Engine(0)
 
 
-def _gpu_parse(torch, dev, e, W, M, stream=0):
+def _gpu_parse(torch, dev, e, W, M, stream=0, cap=None):
     n = len(M)
-    cap = wire.arena_bound(M)
+    cap = wire.arena_bound(M) if cap is None else cap
     d_w = torch.from_numpy(W).to(dev)
     d_m = torch.from_numpy(M.view(np.uint8).reshape(-1).copy()).to(dev)
     d_r = torch.zeros(n * 64 + 16, dtype=torch.uint8, device=dev)
@@ -32,6 +32,25 @@ def _gpu_parse(torch, dev, e, W, M, stream=0):
     d_len = torch.zeros(1, dtype=torch.int64, device=dev)
     e.parse_ptr(d_w.data_ptr(), d_m.data_ptr(), n, d_r.data_ptr(), d_a.data_ptr(), cap, d_len.data_ptr(), stream)
     return d_w, d_m, d_r, d_a, d_len, cap
+
+
+def test_gpu_parse_arena_overflow(env):
+    """An arena smaller than the records need: gm_sync reports GM_E_OVERFLOW, nothing is written
+    past the capacity, and every record stays inside it (the void batch's layout is legal)."""
+    torch, dev, e = env
+    msgs, conn = wire.synthetic(3_000, seed=7)
+    W, M = wire.build(msgs, conn)
+    full = wire.arena_bound(M)
+    cap = (full // 3) & ~15
+    d_w, d_m, d_r, d_a, d_len, cap = _gpu_parse(torch, dev, e, W, M, cap=cap)
+    with pytest.raises(engine.GmError) as ei:
+        e.sync(0)
+    assert ei.value.code == engine.GM_E_OVERFLOW
+    a = d_a.cpu().numpy()
+    assert (a[cap:] == 0xAB).all()
+    got = d_r[:len(M) * 64].cpu().numpy().view(records.REQ_DTYPE)
+    assert int(d_len.item()) <= cap
+    assert (got["base"].astype(np.int64) <= cap).all()
 
 
 def _fields(reqs, arena):
