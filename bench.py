@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--stress-requests", type=int, default=2_000_000,
                     help="the C4 stress variant's batch (0: skip); reported under the line's 'stress' key")
+    ap.add_argument("--no-alone", action="store_true",
+                    help="skip the scan-alone measurement (profiling runs: kernel stats of the pipeline only)")
     ap.add_argument("--serial", action="store_true",
                     help="measurement: the route stage alone before the scan (GM_CREATE_SERIAL)")
     args = ap.parse_args()
@@ -167,8 +169,8 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
                      "algorithmic_bytes_per_launch": zone_bytes},
     }
-    result["roofline"].update(pmc_traffic())
-    if world == 1 and not args.serial:
+    result["roofline"].update(profiled(zone_bytes))
+    if world == 1 and not args.serial and not args.no_alone:
         # the scan kernel alone (GM_CREATE_SERIAL: the route first, then the scan on its own), on
         # the same resident batch: its own roofline fraction beside the in-pipeline one above,
         # where the route shares the CUs
@@ -256,36 +258,46 @@ def stress_leg(torch, engine, records, workloads, args, local):
             "stage_ms": {k: float(np.mean(v)) for k, v in ms.items()}}
 
 
-# The PMC summary of this bench's C4 scan (scripts/pmc.sh on the same tree; bumped with each
-# re-profile).  Selected by name -- never "the newest *pmc_summary.json", which may belong to
-# another kernel's profile.
-PMC_SUMMARY = "profiles/r2_pmc_summary.json"
+# The committed profile of this bench's C4 scan (scripts/scan_profile.py over a rocprofv3
+# --kernel-trace --stats run and the PMC passes of scripts/pmc.sh on the same tree), stamped with
+# the hash of the kernel sources.  Selected by name, and used only when that hash matches the tree
+# being benched: a new kernel never pairs with an old profile (VERDICT r2 "Next round" 1).
+SCAN_PROFILE = "profiles/r3_scan_profile.json"
 
 
-def pmc_traffic():
-    """HBM read bytes per k_waf_scan launch from the committed PMC pass of this workload
-    (scripts/pmc.sh: a separate `rocprofv3 --pmc FETCH_SIZE` run of this bench, FETCH_SIZE x 2 x
-    1024 per the gfx950 correction in MI355X_MICROARCH.md).  Counters cannot be read from inside
-    the timed run, so the value is the profiled one, named with its source file."""
-    path = os.path.join(ROOT, PMC_SUMMARY)
+def profiled(zone_bytes: int) -> dict:
+    """roofline fields from the committed same-tree profile: `traffic` (HBM read bytes per
+    k_waf_scan launch, 2 x FETCH_SIZE x 1024 per the gfx950 correction in MI355X_MICROARCH.md),
+    the LDS bank-conflict rate of the Bloom probes (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE), and
+    `frac_profiled` = zone bytes / the rocprofv3 average k_waf_scan duration / HBM peak.  Counters
+    cannot be read inside the timed run, so these come from the profile, named with its source."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from scan_profile import csrc_hash
+    here = csrc_hash(ROOT)
+    path = os.path.join(ROOT, SCAN_PROFILE)
+    out = {"traffic": None, "frac_profiled": None, "csrc_hash": here}
     if not os.path.exists(path):
-        # fall back to the newest round's summary that carries the scan's bytes
-        import glob
-        cands = [p for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
-                 if "k_waf_scan_hbm_read_bytes_per_launch" in json.load(open(p))]
-        if not cands:
-            return {}
-        path = cands[-1]
+        out["profile_status"] = f"no profile ({SCAN_PROFILE} missing)"
+        return out
     s = json.load(open(path))
-    b = s.get("k_waf_scan_hbm_read_bytes_per_launch")
-    if b is None:
-        return {}
-    out = {"traffic": b, "traffic_unit": "bytes/launch",
-           "traffic_source": os.path.relpath(path, ROOT) + " (rocprofv3 --pmc FETCH_SIZE)"}
-    # north_star: the LDS bank-conflict rate of the scan's Bloom probes, from the same passes
-    # (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE: conflict cycles per LDS-active cycle)
-    if s.get("k_waf_scan_lds_bank_conflict_rate") is not None:
-        out["lds_bank_conflict_rate"] = s["k_waf_scan_lds_bank_conflict_rate"]
+    out["profile_source"] = SCAN_PROFILE
+    if s.get("csrc_hash") != here:
+        out["profile_status"] = (f"stale: profiled sources {s.get('csrc_hash')} != benched sources {here}; "
+                                 "traffic and frac_profiled withheld")
+        return out
+    out["profile_status"] = "same tree"
+    avg = s.get("k_waf_scan_avg_ns")
+    if avg:
+        out["scan_ms_profiled"] = avg / 1e6
+        out["frac_profiled"] = zone_bytes / (avg * 1e-9) / 1e9 / HBM_PEAK_GBPS
+    if s.get("pmc_csrc_hash") == here and s.get("k_waf_scan_hbm_read_bytes_per_launch") is not None:
+        out["traffic"] = s["k_waf_scan_hbm_read_bytes_per_launch"]
+        out["traffic_unit"] = "bytes/launch"
+        out["traffic_source"] = f"{s.get('pmc_summary')} (rocprofv3 --pmc FETCH_SIZE, x2 gfx950)"
+        if s.get("k_waf_scan_lds_bank_conflict_rate") is not None:
+            out["lds_bank_conflict_rate"] = s["k_waf_scan_lds_bank_conflict_rate"]
+    elif s.get("pmc_csrc_hash") != here:
+        out["traffic_status"] = "PMC passes from other sources; traffic withheld"
     return out
 
 
@@ -331,8 +343,14 @@ def cpu_baseline(ss, gblob, preqs, parena, seconds):
         return m / dt, m, dt
     v, m, dt = rate(cores, seconds)
     v1, m1, dt1 = rate(1, seconds / 3)
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     return {"value": v, "unit": "requests/s", "cores": cores, "kind": "port",
             "value_1core": v1, "cores_1": 1, "cpu_model": _cpu_model(),
+            # the box is one GPU's share of a larger host: os.cpu_count() is the whole machine,
+            # OMP_NUM_THREADS the share this job may use; the line says which it ran on
+            "host_cpus": os.cpu_count(), "affinity_cpus": aff,
+            "cpu_share": os.environ.get("OMP_NUM_THREADS") or "unset",
+            "per_core_value_x_host_cpus": v1 * (os.cpu_count() or 1),
             "engine": "oracle/gm_oracle.c: Aho-Corasick literals + PCRE 8.39 regexes behind a required-factor prefilter",
             "sample": f"first {m} requests of the C4 pool ({dt:.1f}s wall, {cores} threads); "
                       f"1-thread: first {m1} ({dt1:.1f}s)"}

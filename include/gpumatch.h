@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 4u   /* 4: gm_stats_t grew the union-DFA fields */
+#define GM_ABI_VERSION 5u   /* 5: gm_update_upstream / gm_peers_migrate; 4: union-DFA stats */
 
 /* ---------------------------------------------------------------- status codes */
 #define GM_OK            0
@@ -340,6 +340,25 @@ int         gm_select_peers(gm_ctx *ctx, const gm_batch *in, const gm_verdict *v
 /* conns -= 1 for each peer id in peer_ids[0 .. n) (GM_NONE / GM_PEER_DEFER skipped).  Async. */
 int         gm_release_peers(gm_ctx *ctx, const uint32_t *peer_ids, uint32_t n, gm_peer_state *state,
                              uint32_t n_peers, void *stream);
+/* NGINX Plus runtime server update of one upstream, with no reload (SURVEY.md §8 f3 + A11):
+ * Configurator.UpdateEndpoints / UpdateEndpointsMergeableIngress / UpdateEndpointsForVirtualServers
+ * push each upstream's endpoints through Manager.UpdateServersInPlus(upstream, servers, cfg)
+ * (configurator.go:442,467,489; interface manager.go:47; LocalManager manager.go:257-284, the Plus
+ * API's UpdateHTTPServers).  Publishes the live tables with upstream `upstream`'s `server` list
+ * replaced by servers[0..n) ("10.0.0.7:8080"; none `down` -- the ServerConfig's max_fails /
+ * fail_timeout / slow_start do not change a pick), RCU-style: calls already enqueued keep the
+ * tables they started with.  configVersion does not change, so neither does `gen`: verdicts of
+ * either table stay valid for gm_select_peers (same upstream ids).  Counters carry over.  The
+ * peer table is renumbered (gm_stats_t.n_peers, gm_peer_address): carry every balancer state
+ * array over with gm_peers_migrate before its next gm_select_peers.  GM_E_INVAL: no upstream of
+ * that name (the previous tables stay live). */
+int         gm_update_upstream(gm_ctx *ctx, const char *upstream, const char *const *servers, uint32_t n);
+/* new_state[j] = old_state[i] where peer j of the live table is the server of the same upstream
+ * and address as peer i of the table before the last gm_update_upstream (NGINX Plus keeps a kept
+ * server's conns / weights / flags), else the initial state.  old_n / new_n: that table's and
+ * the live gm_stats_t.n_peers.  Device pointers (distinct arrays), asynchronous on `stream`. */
+int         gm_peers_migrate(gm_ctx *ctx, const gm_peer_state *old_state, uint32_t old_n,
+                             gm_peer_state *new_state, uint32_t new_n, void *stream);
 /* Host: the `server` address of a peer id ("10.0.0.1:8080") and its upstream id. */
 int         gm_peer_address(gm_ctx *ctx, uint32_t peer, char *buf, size_t cap, uint32_t *upstream_id);
 

@@ -1064,6 +1064,49 @@ BloomChoice choose_bloom_mul(const std::vector<uint32_t> &keys, uint32_t pk, con
 
 }  // namespace
 
+// ngx_http_upstream_update_chash: per server, 160 * weight points; the base CRC over host, one NUL
+// byte and port (split at the last ':' followed by digits only; "unix:" paths have no port), each
+// point = final(base + the previous point's 4 LE bytes).  Sorted by hash; equal hashes keep one
+// point (nginx keeps the first after an unstable sort -- here the lowest peer index).  Appends
+// the ring to `points` (peer = index within the upstream).
+void chash_ring(const std::vector<std::string> &addrs, std::vector<DPoint> &points) {
+    static constexpr Crc32Table T = make_crc32_table();
+    auto upd = [&](uint32_t c, const uint8_t *p, size_t n) {
+        for (size_t q = 0; q < n; q++) c = T.t[(c ^ p[q]) & 0xFF] ^ (c >> 8);
+        return c;
+    };
+    std::vector<DPoint> ring;
+    for (uint32_t j = 0; j < addrs.size(); j++) {
+        const std::string &sv = addrs[j];
+        std::string host = sv, port;
+        if (sv.size() >= 5 && lower(sv.substr(0, 5)) == "unix:") host = sv.substr(5);
+        else {
+            for (size_t q = 0; q < sv.size(); q++) {
+                const char c = sv[sv.size() - q - 1];
+                if (c == ':') { host = sv.substr(0, sv.size() - q - 1); port = sv.substr(sv.size() - q); break; }
+                if (c < '0' || c > '9') break;
+            }
+        }
+        uint32_t base = 0xFFFFFFFFu;
+        base = upd(base, (const uint8_t *)host.data(), host.size());
+        const uint8_t nul = 0;
+        base = upd(base, &nul, 1);
+        base = upd(base, (const uint8_t *)port.data(), port.size());
+        uint32_t prev = 0;
+        for (int q = 0; q < 160; q++) {
+            const uint8_t pb[4] = {(uint8_t)prev, (uint8_t)(prev >> 8), (uint8_t)(prev >> 16), (uint8_t)(prev >> 24)};
+            const uint32_t h = upd(base, pb, 4) ^ 0xFFFFFFFFu;
+            ring.push_back(DPoint{h, j});
+            prev = h;
+        }
+    }
+    std::sort(ring.begin(), ring.end(), [](const DPoint &a, const DPoint &b) {
+        return a.hash != b.hash ? a.hash < b.hash : a.peer < b.peer;
+    });
+    for (size_t q = 0; q < ring.size(); q++)
+        if (q == 0 || ring[q].hash != ring[q - 1].hash) points.push_back(ring[q]);
+}
+
 // ============================================================================ entry
 CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) {
     CompileResult R;
@@ -1131,6 +1174,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     std::vector<DPoint> points;
     std::vector<uint32_t> peer_init;
     R.peer_addrs.clear(); R.peer_ups.clear();
+    R.ups_meta.assign(ups.size(), UpstreamMeta{});
+    for (size_t u = 0; u < ups.size(); u++) R.ups_meta[u].name = ups[u];
     {
         std::map<std::string, const UpstreamIR *> defs;
         for (const UpstreamIR &U : M.upstream_defs) defs.emplace(U.name, &U);
@@ -1148,6 +1193,9 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 R.peer_ups.push_back((uint32_t)u);
             }
             bool defer = U->defer;
+            UpstreamMeta &um = R.ups_meta[u];
+            um.has_block = true;
+            um.method = U->method;
             if ((D.method == UM_RR || D.method == UM_LEAST_CONN) && D.n_peers > SEQ_PEERS_MAX) defer = true;
             if (D.method == UM_HASH || D.method == UM_CHASH) {
                 // key = literal text and $variables; the engine's variables except $host (nginx's
@@ -1182,51 +1230,17 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 D.n_parts = (uint32_t)key_parts.size() - D.first_part;
                 // chash: two server lines with one address would share ring points (nginx then
                 // round-robins between them): not modelled
+                um.defer_fixed = U->defer || defer;   // the key's shape, not the servers
                 std::set<std::string> seen;
                 for (const auto &p : U->peers) if (!seen.insert(p.addr).second && D.method == UM_CHASH) defer = true;
+            } else {
+                um.defer_fixed = U->defer;
             }
             if (D.method == UM_CHASH && !defer) {
-                // ngx_http_upstream_update_chash: per server, 160 * weight points; the base CRC over
-                // host, one NUL byte and port (split at the last ':' followed by digits only; "unix:"
-                // paths have no port), each point = final(base + the previous point's 4 LE bytes)
-                static constexpr Crc32Table T = make_crc32_table();
-                auto upd = [&](uint32_t c, const uint8_t *p, size_t n) {
-                    for (size_t q = 0; q < n; q++) c = T.t[(c ^ p[q]) & 0xFF] ^ (c >> 8);
-                    return c;
-                };
-                std::vector<DPoint> ring;
-                for (uint32_t j = 0; j < D.n_peers; j++) {
-                    const std::string &sv = U->peers[j].addr;
-                    std::string host = sv, port;
-                    if (sv.size() >= 5 && lower(sv.substr(0, 5)) == "unix:") host = sv.substr(5);
-                    else {
-                        for (size_t q = 0; q < sv.size(); q++) {
-                            const char c = sv[sv.size() - q - 1];
-                            if (c == ':') { host = sv.substr(0, sv.size() - q - 1); port = sv.substr(sv.size() - q); break; }
-                            if (c < '0' || c > '9') break;
-                        }
-                    }
-                    uint32_t base = 0xFFFFFFFFu;
-                    base = upd(base, (const uint8_t *)host.data(), host.size());
-                    const uint8_t nul = 0;
-                    base = upd(base, &nul, 1);
-                    base = upd(base, (const uint8_t *)port.data(), port.size());
-                    uint32_t prev = 0;
-                    for (int q = 0; q < 160; q++) {
-                        const uint8_t pb[4] = {(uint8_t)prev, (uint8_t)(prev >> 8), (uint8_t)(prev >> 16), (uint8_t)(prev >> 24)};
-                        const uint32_t h = upd(base, pb, 4) ^ 0xFFFFFFFFu;
-                        ring.push_back(DPoint{h, j});
-                        prev = h;
-                    }
-                }
-                // sorted by hash; equal hashes keep one point (nginx keeps the first after an
-                // unstable sort -- here the lowest peer index)
-                std::sort(ring.begin(), ring.end(), [](const DPoint &a, const DPoint &b) {
-                    return a.hash != b.hash ? a.hash < b.hash : a.peer < b.peer;
-                });
+                std::vector<std::string> addrs;
+                for (const auto &p : U->peers) addrs.push_back(p.addr);
                 D.first_point = (uint32_t)points.size();
-                for (size_t q = 0; q < ring.size(); q++)
-                    if (q == 0 || ring[q].hash != ring[q - 1].hash) points.push_back(ring[q]);
+                chash_ring(addrs, points);
                 D.n_points = (uint32_t)points.size() - D.first_point;
             }
             if (defer) { D.method = UM_DEFER; st.n_upstreams_deferred++; }
@@ -1891,6 +1905,93 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.bloom_log2 = BLOOM_LOG2; h.bloom_mul = bloom_mul; h.bloom_pk = bloom_pk; h.ctx_mul = CTX_MUL_DEFAULT;
     memcpy(I.buf.data(), &h, sizeof h);
     st.table_bytes = h.total;
+    R.image = std::move(I.buf);
+    R.ok = true;
+    return R;
+}
+
+CompileResult update_upstream(const CompileResult &live, const std::string &name, const std::vector<std::string> &addrs) {
+    CompileResult R;
+    const TabHeader &h0 = live.hdr;
+    const uint8_t *b = live.image.data();
+    const uint32_t nu = h0.n_ups;
+    uint32_t uu = GM_NONE;
+    for (uint32_t u = 0; u < nu && u < live.ups_meta.size(); u++)
+        if (live.ups_meta[u].name == name) { uu = u; break; }
+    if (uu == GM_NONE) { R.code = GM_E_INVAL; R.err = "no upstream named '" + name + "'"; return R; }
+    const DUpstream *ou = (const DUpstream *)(b + h0.off_ups);
+    const DPoint *opt = (const DPoint *)(b + h0.off_points);
+    const uint32_t *oinit = (const uint32_t *)(b + h0.off_peer_init);
+    std::vector<DUpstream> dups(ou, ou + nu);
+    std::vector<DPoint> points;
+    std::vector<uint32_t> peer_init;
+    R.stats = live.stats;
+    R.stats.n_upstreams_deferred = 0;
+    R.ups_meta = live.ups_meta;
+    for (uint32_t u = 0; u < nu; u++) {
+        DUpstream &D = dups[u];
+        const DUpstream &O = ou[u];
+        D.first_peer = (uint32_t)peer_init.size();
+        if (u != uu) {
+            for (uint32_t j = 0; j < O.n_peers; j++) {
+                peer_init.push_back(oinit[O.first_peer + j]);
+                R.peer_addrs.push_back(live.peer_addrs[O.first_peer + j]);
+                R.peer_ups.push_back(u);
+                R.peer_map.push_back(O.first_peer + j);
+            }
+            D.first_point = (uint32_t)points.size();
+            points.insert(points.end(), opt + O.first_point, opt + O.first_point + O.n_points);
+            if (D.method == UM_DEFER) R.stats.n_upstreams_deferred++;
+            continue;
+        }
+        // the updated upstream: its servers in the given order, a kept address keeps its state
+        const UpstreamMeta &M = live.ups_meta[u];
+        std::vector<bool> used(O.n_peers, false);
+        for (const std::string &a : addrs) {
+            uint32_t from = GM_NONE;
+            for (uint32_t j = 0; j < O.n_peers; j++)
+                if (!used[j] && live.peer_addrs[O.first_peer + j] == a) { used[j] = true; from = O.first_peer + j; break; }
+            peer_init.push_back(0u);   // Plus API servers: none `down`
+            R.peer_addrs.push_back(a);
+            R.peer_ups.push_back(u);
+            R.peer_map.push_back(from);
+        }
+        D.n_peers = (uint32_t)addrs.size();
+        D.method = M.has_block ? M.method : UM_DEFER;
+        bool defer = !M.has_block || M.defer_fixed;
+        if ((D.method == UM_RR || D.method == UM_LEAST_CONN) && D.n_peers > SEQ_PEERS_MAX) defer = true;
+        D.first_point = (uint32_t)points.size();
+        D.n_points = 0;
+        if (D.method == UM_CHASH && !defer) {
+            std::set<std::string> seen;
+            for (const std::string &a : addrs) if (!seen.insert(a).second) defer = true;
+            if (!defer) chash_ring(addrs, points);
+            D.n_points = (uint32_t)points.size() - D.first_point;
+        }
+        if (defer) { D.method = UM_DEFER; R.stats.n_upstreams_deferred++; }
+    }
+    R.stats.n_peers = (uint32_t)peer_init.size();
+    // the image: everything before the upstream section as it is, then the rebuilt section, then
+    // the sections after it (DLocUri, the byte pool) moved along -- their contents are offsets into
+    // the byte pool, relative to its own base, so they move unchanged
+    Image I;
+    I.buf.assign(b, b + h0.off_ups);
+    TabHeader h = h0;
+    h.n_peers = R.stats.n_peers;
+    h.n_points = (uint32_t)points.size();
+    std::vector<DKeyPart> key_parts((const DKeyPart *)(b + h0.off_key_parts),
+                                    (const DKeyPart *)(b + h0.off_key_parts) + h0.n_key_parts);
+    std::vector<DLocUri> dluri((const DLocUri *)(b + h0.off_loc_uri), (const DLocUri *)(b + h0.off_loc_uri) + h0.n_locs);
+    std::vector<uint8_t> bytes(b + h0.off_bytes, b + h0.total);
+    h.off_ups = I.put(dups); h.off_key_parts = I.put(key_parts); h.off_points = I.put(points);
+    h.off_peer_init = I.put(peer_init);
+    h.off_loc_uri = I.put(dluri);
+    h.off_bytes = I.put(bytes);
+    I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
+    h.total = I.buf.size();
+    memcpy(I.buf.data(), &h, sizeof h);
+    R.stats.table_bytes = h.total;
+    R.hdr = h;
     R.image = std::move(I.buf);
     R.ok = true;
     return R;

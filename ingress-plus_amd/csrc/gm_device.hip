@@ -1053,8 +1053,13 @@ struct Generation {
     std::vector<uint8_t> host_image;   // kept for host-side introspection (gpumatch_debug.h)
     std::vector<std::string> peer_addrs;   // gm_peer_address
     std::vector<uint32_t> peer_ups;
+    std::vector<UpstreamMeta> ups_meta;     // gm_update_upstream
+    // gm_update_upstream -> gm_peers_migrate: new peer id -> the previous table's peer id (GM_NONE:
+    // a new server), and the previous table's peer count
+    uint32_t *d_peer_map = nullptr;
+    uint32_t peer_map_old_n = GM_NONE;
     ~Generation() {
-        for (void *p : {(void *)d_image, (void *)d_counters, (void *)d_counters_sum, (void *)d_gtab})
+        for (void *p : {(void *)d_image, (void *)d_counters, (void *)d_counters_sum, (void *)d_gtab, (void *)d_peer_map})
             if (p) (void)hipFree(p);
     }
 };
@@ -1065,6 +1070,10 @@ struct Scratch {
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;               // k_route beside the WAF scan
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // recorded on `stream` after every call that enqueues work reading a generation or its
+    // counters: a generation swap or a counter read waits for these events (not for the device)
+    hipEvent_t ev_done = nullptr;
+    bool done_rec = false;
     hipEvent_t ev[5] = {}, ev_route[2] = {};  // GM_CREATE_PROFILE stage events
     bool ev_pending = false, route_side = false;
     int ev_used = 0;
@@ -1115,6 +1124,7 @@ struct Scratch {
         for (auto &e : ev_route) if (e) (void)hipEventDestroy(e);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
         if (ev_join) (void)hipEventDestroy(ev_join);
+        if (ev_done) (void)hipEventDestroy(ev_done);
         if (side) (void)hipStreamDestroy(side);
     }
 };
@@ -1178,7 +1188,8 @@ static Scratch *scratch_for(gm_ctx *c, hipStream_t stream) {
         hipMemset(s->d_status, 0, STATUS_WORDS * 4) != hipSuccess ||
         hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming) != hipSuccess) {
         t_err = "scratch allocation failed";
         return nullptr;
     }
@@ -1190,6 +1201,27 @@ static Scratch *scratch_for(gm_ctx *c, hipStream_t stream) {
     Scratch *p = s.get();
     c->scratch.emplace(stream, std::move(s));
     return p;
+}
+
+// the call just enqueued on S's stream is the stream's last use of the live generation so far
+static int mark_done(gm_ctx *c, Scratch *S) {
+    HIPCHK(c, hipEventRecord(S->ev_done, S->stream));
+    S->done_rec = true;
+    return GM_OK;
+}
+
+// Wait until every call enqueued so far through this ctx has completed: the completion event of
+// each stream's last call (RCU retirement of a swapped-out generation, counter reads).  Only this
+// ctx's streams are waited for -- not the device (other work on it, other contexts).  Events are
+// owned by the scratch, so a stream the caller has destroyed since is no hazard.
+static int wait_done(gm_ctx *c) {
+    std::vector<hipEvent_t> evs;
+    {
+        std::lock_guard<std::mutex> lk(c->scr_mu);
+        for (auto &kv : c->scratch) if (kv.second->done_rec) evs.push_back(kv.second->ev_done);
+    }
+    for (hipEvent_t e : evs) HIPCHK(c, hipEventSynchronize(e));
+    return GM_OK;
 }
 
 #ifdef GM_EXP_COUNT
@@ -1246,18 +1278,23 @@ void gm_destroy(gm_ctx *c) {
 
 const char *gm_last_error(gm_ctx *) { return t_err.c_str(); }
 
-int gm_load_generation(gm_ctx *c, const void *blob, size_t len, uint32_t gen) {
-    if (!c || !blob) return fail(c, GM_E_INVAL, "null argument");
-    CompileResult R = compile_generation((const uint8_t *)blob, len, gen);
-    if (!R.ok) return fail(c, R.code, R.err);   // previous generation stays live
+// Publish compiled tables as the live generation: device copy-in beside the live one, swap under
+// the exclusive lock, then RCU retirement -- every call that read the old generation finished
+// enqueueing before the lock was granted, and its completion event is waited for before the old
+// memory is freed.  `same_counters`: the new tables keep the live generation's counter space
+// (gm_update_upstream: same locations and signatures), the counters move over unreset.
+static int publish(gm_ctx *c, CompileResult &R, uint32_t gen, bool same_counters) {
     if (R.stats.n_sigs >= (1u << 21) || R.stats.n_sig_regex >= (1u << 21))
         return fail(c, GM_E_INVAL, "more than 2^21 signatures");
     std::unique_ptr<Generation> g(new Generation());
     g->hdr = R.hdr;
     g->host_image = R.image;
     g->stats = R.stats;
+    g->stats.gen = gen;
     g->peer_addrs = std::move(R.peer_addrs);
     g->peer_ups = std::move(R.peer_ups);
+    g->ups_meta = std::move(R.ups_meta);
+    g->n_counters = g->stats.n_counters;
     if (!(c->flags & GM_CREATE_COMPILE_ONLY)) {
         HIPCHK(c, hipSetDevice(c->dev));
         HIPCHK(c, hipMalloc((void **)&g->d_image, R.image.size()));
@@ -1266,24 +1303,67 @@ int gm_load_generation(gm_ctx *c, const void *blob, size_t len, uint32_t gen) {
         HIPCHK(c, hipMalloc((void **)&g->d_gtab, sizeof(GTab)));
         g->tab.self = g->d_gtab;
         HIPCHK(c, hipMemcpy(g->d_gtab, &g->tab, sizeof(GTab), hipMemcpyHostToDevice));
-        g->n_counters = g->stats.n_counters;
-        const size_t cb = std::max<size_t>(g->n_counters, 1) * 8;
-        HIPCHK(c, hipMalloc((void **)&g->d_counters, cb));
-        HIPCHK(c, hipMalloc((void **)&g->d_counters_sum, cb));
-        HIPCHK(c, hipMemset(g->d_counters, 0, cb));
-        HIPCHK(c, hipMemset(g->d_counters_sum, 0, cb));
+        if (!R.peer_map.empty()) {
+            HIPCHK(c, hipMalloc((void **)&g->d_peer_map, R.peer_map.size() * 4));
+            HIPCHK(c, hipMemcpy(g->d_peer_map, R.peer_map.data(), R.peer_map.size() * 4, hipMemcpyHostToDevice));
+        }
+        if (!same_counters) {
+            const size_t cb = std::max<size_t>(g->n_counters, 1) * 8;
+            HIPCHK(c, hipMalloc((void **)&g->d_counters, cb));
+            HIPCHK(c, hipMalloc((void **)&g->d_counters_sum, cb));
+            HIPCHK(c, hipMemset(g->d_counters, 0, cb));
+            HIPCHK(c, hipMemset(g->d_counters_sum, 0, cb));
+        }
     }
     Generation *old;
     {
         std::unique_lock<std::shared_mutex> lk(c->gen_mu);
         old = c->gen;
+        if (same_counters && old) {
+            if (old->n_counters != g->n_counters) return fail(c, GM_E_INVAL, "counter space changed");
+            g->d_counters = old->d_counters; g->d_counters_sum = old->d_counters_sum;
+            old->d_counters = old->d_counters_sum = nullptr;
+            g->peer_map_old_n = old->stats.n_peers;
+        }
         c->gen = g.release();
     }
-    // RCU-style retirement: every batch that read the old generation finished enqueueing before
-    // the exclusive lock was granted; the device drains them before its memory is freed
-    if (old && !(c->flags & GM_CREATE_COMPILE_ONLY)) (void)hipDeviceSynchronize();
+    if (old && !(c->flags & GM_CREATE_COMPILE_ONLY)) {
+        const int e = wait_done(c);
+        if (e) { delete old; return e; }
+    }
     delete old;
     return GM_OK;
+}
+
+int gm_load_generation(gm_ctx *c, const void *blob, size_t len, uint32_t gen) {
+    if (!c || !blob) return fail(c, GM_E_INVAL, "null argument");
+    CompileResult R = compile_generation((const uint8_t *)blob, len, gen);
+    if (!R.ok) return fail(c, R.code, R.err);   // previous generation stays live
+    return publish(c, R, gen, false);
+}
+
+int gm_update_upstream(gm_ctx *c, const char *upstream, const char *const *servers, uint32_t n) {
+    if (!c || !upstream || (n && !servers)) return fail(c, GM_E_INVAL, "null argument");
+    std::vector<std::string> addrs;
+    for (uint32_t i = 0; i < n; i++) {
+        if (!servers[i] || !servers[i][0]) return fail(c, GM_E_INVAL, "empty server address");
+        addrs.emplace_back(servers[i]);
+    }
+    CompileResult live;
+    uint32_t gen;
+    {
+        std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+        const Generation *g = c->gen;
+        if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
+        live.image = g->host_image; live.hdr = g->hdr; live.stats = g->stats;
+        live.peer_addrs = g->peer_addrs; live.peer_ups = g->peer_ups; live.ups_meta = g->ups_meta;
+        gen = g->stats.gen;
+    }
+    CompileResult R = update_upstream(live, upstream, addrs);
+    if (!R.ok) return fail(c, R.code, R.err);
+    // (two concurrent updates: the second publishes over the first's tables -- the Manager calls
+    // UpdateServersInPlus one upstream at a time, configurator.go:442,467,489)
+    return publish(c, R, gen, true);
 }
 
 int gm_stats(gm_ctx *c, gm_stats_t *out) {
@@ -1579,9 +1659,11 @@ int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit
     if (((uintptr_t)in->arena & 15) || ((uintptr_t)in->reqs & 15) || ((uintptr_t)out & 15))
         return fail(c, GM_E_INVAL, "reqs / arena / out must be 16-byte aligned");
     if (hit_cap > 0xFFFFFFFFull) hit_cap = 0xFFFFFFFFull;   // hit offsets are u32
-    if (!(in->flags & GM_BATCH_HOST))
-        return run_batch(c, S, g, in->reqs, in->arena, in->arena_len, in->n, out, hit_ids, hit_ids ? hit_cap : 0,
-                         in->arena_len_dev);
+    if (!(in->flags & GM_BATCH_HOST)) {
+        const int e = run_batch(c, S, g, in->reqs, in->arena, in->arena_len, in->n, out, hit_ids, hit_ids ? hit_cap : 0,
+                                in->arena_len_dev);
+        return e ? e : mark_done(c, S);
+    }
     // host buffers: stage reqs + arena + verdicts + hits through HBM (PCIe both ways)
     size_t rq = (size_t)in->n * sizeof(gm_req), ar = (in->arena_len + 255) & ~255ull;
     size_t vo = (size_t)in->n * sizeof(gm_verdict), ho = hit_cap * 4;
@@ -1600,7 +1682,7 @@ int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit
     if (e) return e;
     HIPCHK(c, hipMemcpyAsync(out, dv, vo, hipMemcpyDeviceToHost, s));
     if (hit_ids && hit_cap) HIPCHK(c, hipMemcpyAsync(hit_ids, dh, ho, hipMemcpyDeviceToHost, s));
-    return GM_OK;
+    return mark_done(c, S);
 }
 
 int gm_sync(gm_ctx *c, void *stream) {
@@ -1649,7 +1731,7 @@ int gm_counters(gm_ctx *c, uint64_t *out, size_t n) {
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
     HIPCHK(c, hipSetDevice(c->dev));
-    HIPCHK(c, hipDeviceSynchronize());
+    if (int e = wait_done(c)) return e;
     HIPCHK(c, hipMemcpy(out, c->gen->d_counters, std::min(n, c->gen->n_counters) * 8, hipMemcpyDeviceToHost));
     return GM_OK;
 }
@@ -1660,7 +1742,7 @@ int gm_counters_global(gm_ctx *c, uint64_t *out, size_t n) {
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
     HIPCHK(c, hipSetDevice(c->dev));
-    HIPCHK(c, hipDeviceSynchronize());
+    if (int e = wait_done(c)) return e;
     HIPCHK(c, hipMemcpy(out, c->gen->d_counters_sum, std::min(n, c->gen->n_counters) * 8, hipMemcpyDeviceToHost));
     return GM_OK;
 }
@@ -1671,7 +1753,7 @@ int gm_counters_reset(gm_ctx *c) {
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     if (!c->gen) return GM_OK;
     HIPCHK(c, hipSetDevice(c->dev));
-    HIPCHK(c, hipDeviceSynchronize());
+    if (int e = wait_done(c)) return e;
     const size_t cb = std::max<size_t>(c->gen->n_counters, 1) * 8;
     HIPCHK(c, hipMemset(c->gen->d_counters, 0, cb));
     HIPCHK(c, hipMemset(c->gen->d_counters_sum, 0, cb));
@@ -1703,10 +1785,12 @@ int gm_counters_allreduce(gm_ctx *c, void *stream) {
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     if (!c->gen || !c->gen->d_counters) return fail(c, GM_E_NOGEN, "no counters");
     HIPCHK(c, hipSetDevice(c->dev));
+    Scratch *S = scratch_for(c, (hipStream_t)stream);
+    if (!S) return fail(c, GM_E_NOMEM, t_err);
     ncclResult_t r = ncclAllReduce(c->gen->d_counters, c->gen->d_counters_sum, std::max<size_t>(c->gen->n_counters, 1),
                                    ncclUint64, ncclSum, c->comm, (hipStream_t)stream);
     if (r != ncclSuccess) return fail(c, GM_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-    return GM_OK;
+    return mark_done(c, S);
 }
 
 }  // extern "C"
@@ -1997,9 +2081,45 @@ extern "C" int gm_peers_init(gm_ctx *c, gm_peer_state *state, uint32_t n_peers, 
     if (n_peers != g->tab.n_peers) return fail(c, GM_E_INVAL, "n_peers differs from the generation's peer count");
     if (n_peers == 0) return GM_OK;
     if (!state) return fail(c, GM_E_INVAL, "null state");
+    Scratch *S = scratch_for(c, (hipStream_t)stream);
+    if (!S) return fail(c, GM_E_NOMEM, t_err);
     k_peers_init<<<std::min<uint32_t>((n_peers + 255) / 256, 1024), 256, 0, (hipStream_t)stream>>>(g->tab, state);
     HIPCHK(c, hipGetLastError());
-    return GM_OK;
+    return mark_done(c, S);
+}
+
+// NGINX Plus keeps a kept server's runtime state across an API update: new_state[j] = the state
+// of the previous table's peer it came from (gm_update_upstream's map), else the initial state.
+__global__ void k_peers_migrate(const gm_peer_state *__restrict__ old_st, const uint32_t *__restrict__ map,
+                                const uint32_t *__restrict__ init, uint32_t n, gm_peer_state *__restrict__ new_st) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const uint32_t from = map[j];
+        gm_peer_state v{0u, 0, init[j], 0u};
+        if (from != GM_NONE) v = old_st[from];
+        new_st[j] = v;
+    }
+}
+
+extern "C" int gm_peers_migrate(gm_ctx *c, const gm_peer_state *old_state, uint32_t old_n, gm_peer_state *new_state,
+                                uint32_t new_n, void *stream) {
+    if (!c) return fail(c, GM_E_INVAL, "null ctx");
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return fail(c, GM_E_NODEVICE, "compile-only context");
+    HIPCHK(c, hipSetDevice(c->dev));
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    const Generation *g = c->gen;
+    if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
+    if (!g->d_peer_map && g->tab.n_peers) return fail(c, GM_E_INVAL, "the live tables did not come from gm_update_upstream");
+    if (old_n != g->peer_map_old_n) return fail(c, GM_E_INVAL, "old_n differs from the previous table's peer count");
+    if (new_n != g->tab.n_peers) return fail(c, GM_E_INVAL, "new_n differs from the generation's peer count");
+    if (new_n == 0) return GM_OK;
+    if (!new_state || (old_n && !old_state)) return fail(c, GM_E_INVAL, "null state");
+    if ((const void *)old_state == (const void *)new_state) return fail(c, GM_E_INVAL, "migrate in place");
+    Scratch *S = scratch_for(c, (hipStream_t)stream);
+    if (!S) return fail(c, GM_E_NOMEM, t_err);
+    k_peers_migrate<<<std::min<uint32_t>((new_n + 255) / 256, 1024), 256, 0, (hipStream_t)stream>>>(
+        old_state, g->d_peer_map, g->tab.peer_init, new_n, new_state);
+    HIPCHK(c, hipGetLastError());
+    return mark_done(c, S);
 }
 
 extern "C" int gm_select_peers(gm_ctx *c, const gm_batch *in, const gm_verdict *verdicts, gm_peer_state *state,
@@ -2053,7 +2173,7 @@ extern "C" int gm_select_peers(gm_ctx *c, const gm_batch *in, const gm_verdict *
             peer_out, n, state, t.n_peers, 1);
         HIPCHK(c, hipGetLastError());
     }
-    return GM_OK;
+    return mark_done(c, S);
 }
 
 extern "C" int gm_release_peers(gm_ctx *c, const uint32_t *peer_ids, uint32_t n, gm_peer_state *state,
@@ -2067,10 +2187,12 @@ extern "C" int gm_release_peers(gm_ctx *c, const uint32_t *peer_ids, uint32_t n,
     if (n_peers != g->tab.n_peers) return fail(c, GM_E_INVAL, "n_peers differs from the generation's peer count");
     if (n == 0 || n_peers == 0) return GM_OK;
     if (!peer_ids || !state) return fail(c, GM_E_INVAL, "null argument");
+    Scratch *S = scratch_for(c, (hipStream_t)stream);
+    if (!S) return fail(c, GM_E_NOMEM, t_err);
     k_peer_count<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 4095) / 4096, (uint32_t)c->cu_count * 2)), 256, 0,
                    (hipStream_t)stream>>>(peer_ids, n, state, n_peers, -1);
     HIPCHK(c, hipGetLastError());
-    return GM_OK;
+    return mark_done(c, S);
 }
 
 extern "C" int gm_peer_address(gm_ctx *c, uint32_t peer, char *buf, size_t cap, uint32_t *upstream_id) {
@@ -2120,5 +2242,5 @@ extern "C" int gm_upstream_uris(gm_ctx *c, const gm_batch *in, const gm_verdict 
     k_upuri_emit<<<blocks, 256, 0, s>>>(in->reqs, in->arena, verdicts, n, g->tab, out_off, out, out_cap, out_len,
                                         S->d_status + UPURI_STATUS_WORD);
     HIPCHK(c, hipGetLastError());
-    return GM_OK;
+    return mark_done(c, S);
 }

@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GM_LIB") or os.path.join(os.path.dirname(HERE), "libgpumatch.so")
 
 GM_OK = 0
-GM_ABI_VERSION = 4   # include/gpumatch.h
+GM_ABI_VERSION = 5   # include/gpumatch.h
 GM_E_OVERFLOW = -4
 GM_CREATE_COMPILE_ONLY = 0x1
 GM_BATCH_HOST = 0x1
@@ -54,7 +54,8 @@ class GmBatch(ctypes.Structure):
 EXPORTS = ["gm_create", "gm_destroy", "gm_abi_version", "gm_load_generation", "gm_match_batch", "gm_sync",
            "gm_counters", "gm_counters_reset", "gm_comm_unique_id", "gm_comm_init", "gm_counters_allreduce",
            "gm_stats", "gm_last_error", "gm_normalize_uris", "gm_counters_global", "gm_parse_requests",
-           "gm_peers_init", "gm_select_peers", "gm_release_peers", "gm_peer_address", "gm_upstream_uris"]
+           "gm_peers_init", "gm_select_peers", "gm_release_peers", "gm_peer_address", "gm_upstream_uris",
+           "gm_update_upstream", "gm_peers_migrate"]
 
 # gm_peer_state (include/gpumatch.h)
 PEER_STATE_DTYPE = np.dtype([("conns", "<u4"), ("current_weight", "<i4"), ("flags", "<u4"), ("reserved", "<u4")])
@@ -94,6 +95,10 @@ def lib():
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                         ctypes.c_void_p]
         L.gm_peers_init.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+        L.gm_update_upstream.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p),
+                                         ctypes.c_uint32]
+        L.gm_peers_migrate.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                       ctypes.c_uint32, ctypes.c_void_p]
         L.gm_select_peers.argtypes = [ctypes.c_void_p, ctypes.POINTER(GmBatch), ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
         L.gm_release_peers.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
@@ -182,6 +187,15 @@ class Engine:
     def peers_init_ptr(self, state_ptr, n_peers, stream=0):
         """gm_peers_init: the generation's initial balancer state into a device gm_peer_state array."""
         self._chk(lib().gm_peers_init(self.h, state_ptr, n_peers, stream))
+
+    def update_upstream(self, name: str, servers):
+        """gm_update_upstream: NGINX Plus UpdateServersInPlus(name, servers) without a reload."""
+        arr = (ctypes.c_char_p * max(len(servers), 1))(*[x.encode() for x in servers])
+        self._chk(lib().gm_update_upstream(self.h, name.encode(), arr, len(servers)))
+
+    def peers_migrate_ptr(self, old_ptr, old_n, new_ptr, new_n, stream=0):
+        """gm_peers_migrate: a balancer state array across the last update_upstream."""
+        self._chk(lib().gm_peers_migrate(self.h, old_ptr, old_n, new_ptr, new_n, stream))
 
     def select_peers_ptr(self, reqs_ptr, arena_ptr, arena_len, n, verdicts_ptr, state_ptr, n_peers, out_ptr,
                          stream=0):

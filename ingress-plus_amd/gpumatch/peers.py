@@ -37,23 +37,42 @@ def _addr(u, j):
     return f"10.{u}.{j // 250}.{j % 250 + 1}:{8080 + (j % 3)}"
 
 
-def conf_text(method: str | None = None) -> str:
-    """``method``: one LBMethod for every upstream (e.g. the default "random two least_conn")."""
+def upstream_name(u: int) -> str:
+    return f"default-peers-u{u:02d}-svc-80"
+
+
+def server_addrs(u: int) -> list:
+    """The `server` addresses upstream u is rendered with (config order)."""
+    return [_addr(u, j) for j in range(UPSTREAMS[u][1])]
+
+
+def conf_text(method: str | None = None, servers: dict | None = None, upstreams=None) -> str:
+    """``method``: one LBMethod for every upstream (e.g. the default "random two least_conn").
+    ``servers``: {upstream index: [address, ...]} -- the server list an NGINX Plus API update
+    left (Manager.UpdateServersInPlus), rendered as a reload with those lines would be (no
+    ``down``).  ``upstreams``: another (method, n) list in place of UPSTREAMS."""
     L = []
     names = []
-    for u, (m, k) in enumerate(UPSTREAMS):
+    ups = UPSTREAMS if upstreams is None else upstreams
+    for u, (m, k) in enumerate(ups):
         m = m if method is None else method
-        name = f"default-peers-u{u:02d}-svc-80"
+        name = upstream_name(u)
         names.append(name)
         L.append(f"upstream {name} {{")
         if m:
             L.append(f"\t{m};")
+        if servers is not None and u in servers:
+            for a in servers[u]:
+                L.append(f"\tserver {a} max_fails=1 fail_timeout=10s;")
+            L.append("\tkeepalive 32;")
+            L.append("}")
+            continue
         for j in range(k):
             down = " down" if (u, j) in DOWN else ""
             L.append(f"\tserver {_addr(u, j)} max_fails=1 fail_timeout=10s{down};")
         L.append("\tkeepalive 32;")
         L.append("}")
-    name = f"default-peers-u{DEFER_WEIGHT:02d}-svc-80"
+    name = upstream_name(len(ups))
     names.append(name)
     L.append(f"upstream {name} {{\n\tserver 10.99.0.1:80 weight=2;\n\tserver 10.99.0.2:80;\n}}")
     for u, name in enumerate(names):
@@ -63,10 +82,10 @@ def conf_text(method: str | None = None) -> str:
     return "\n".join(L) + "\n"
 
 
-def peers_blob(method: str | None = None) -> bytes:
+def peers_blob(method: str | None = None, servers: dict | None = None, upstreams=None) -> bytes:
     main = ("http {\n\tserver {\n\t\tlisten 80 default_server;\n\t\tserver_name _;\n"
             "\t\tlocation / {\n\t\t\treturn 404;\n\t\t}\n\t}\n\tinclude /etc/nginx/conf.d/*.conf;\n}\n")
-    return blob.make_blob(main, {"default-peers": conf_text(method)})
+    return blob.make_blob(main, {"default-peers": conf_text(method, servers, upstreams)})
 
 
 def _raddrs(rng, m):
@@ -88,11 +107,11 @@ def _raddrs(rng, m):
     return out
 
 
-def gen_requests(n: int, seed: int = records.SEED_BASE + 40, hot: tuple = ()):
+def gen_requests(n: int, seed: int = records.SEED_BASE + 40, hot: tuple = (), upstreams=None):
     """n requests over the peers config.  ``hot``: upstream indices that get most of the traffic
-    (long sequential runs for round robin / least_conn)."""
+    (long sequential runs for round robin / least_conn).  ``upstreams``: as for conf_text."""
     rng = np.random.default_rng(seed)
-    nu = len(UPSTREAMS) + 1
+    nu = len(UPSTREAMS if upstreams is None else upstreams) + 1
     w = np.ones(nu)
     for h in hot:
         w[h] = 40.0 * nu

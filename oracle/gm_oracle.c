@@ -816,7 +816,8 @@ int orc_factor(const char *pat, char *out) {
  * engine does not model defers (GM_PEER_DEFER): server parameters beyond max_fails /
  * fail_timeout / slow_start / down, Plus-only methods, hash keys with $host or variables outside
  * the engine's set, a consistent-hash upstream naming one address twice, more than 1024 peers
- * under round robin / least_conn. */
+ * under round robin / least_conn, and a request of another method whose pick falls back to round
+ * robin (empty hash key, > 20 tries on down peers) in an upstream of more than 1024 peers. */
 static int is_var_ch(char ch);
 static uint32_t crc32_bytes(uint32_t c, const void *p, size_t n) {   /* bitwise CRC-32/IEEE, running */
     const uint8_t *b = p;
@@ -2212,6 +2213,8 @@ int orc_select_peers(orc_ctx *c, const gm_req *reqs, const uint8_t *arena, const
         } else {
             p = U->method == OM_RR ? -1 : orc_stateless(c, U, &reqs[i], arena, st, snap, &sc);
             if (p == -2) { out[i] = GM_PEER_DEFER; continue; }
+            /* the engine's round-robin fallback holds at most 1024 peers (SEQ_PEERS_MAX) */
+            if (p == -1 && U->npeers > 1024) { out[i] = GM_PEER_DEFER; continue; }
             if (p == -1) p = orc_rr(U, st);
             if (p >= 0) picks[U->first_peer + p]++;
         }

@@ -19,13 +19,18 @@ if [ -z "$NO_BENCH" ]; then
 fi
 if [ -n "$PROF" ]; then
   cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 1 --no-cpu --stress-requests 0 > "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}.log" 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 1 --no-cpu --no-alone --stress-requests 0 > "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}.log" 2>&1
   rc=$?
   tail -2 "$GRAFT_REPO_ROOT/gpurun_out/prof_${TAG}.log"
   [ $rc -eq 0 ] || exit $rc
   cd "$GRAFT_REPO_ROOT"
+  f=$(find gpurun_out/prof_${TAG} -name "*kernel_stats.csv" | head -1)
+  [ -n "$f" ] && cp "$f" gpurun_out/${TAG}_kernel_stats.csv && python3 scripts/kstats.py "$f" | head -8
 fi
 if [ -n "$PMC" ]; then
   TAG=$TAG bash scripts/pmc.sh || exit $?
+fi
+if [ -f gpurun_out/${TAG}_kernel_stats.csv ]; then
+  python3 scripts/scan_profile.py $TAG gpurun_out/${TAG}_kernel_stats.csv gpurun_out/pmc_${TAG}_summary.json > gpurun_out/${TAG}_scan_profile.json
 fi
 exit 0

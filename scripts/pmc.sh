@@ -7,7 +7,7 @@
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 TAG=${TAG:-r1}
-ARGS="--steps 2 --warmup 1 --no-cpu --stress-requests 0 ${BENCH_ARGS}"
+ARGS="--steps 2 --warmup 1 --no-cpu --no-alone --stress-requests 0 ${BENCH_ARGS}"
 cd /tmp && export TMPDIR=/tmp
 run() {
   local name=$1; shift

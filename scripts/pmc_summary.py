@@ -21,7 +21,9 @@ for p in ("fetch", "write", "sq", "lds"):
         for c, v in d.items():
             res[k][c] = sum(v) / len(v)
             res[k]["dispatches"] = len(v)
-summary = {"tag": tag, "kernels": res}
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from scan_profile import csrc_hash  # noqa: E402
+summary = {"tag": tag, "csrc_hash": csrc_hash(), "kernels": res}
 scan = res.get("k_waf_scan", {})
 if "FETCH_SIZE" in scan:
     summary["k_waf_scan_hbm_read_bytes_per_launch"] = 2.0 * scan["FETCH_SIZE"] * 1024

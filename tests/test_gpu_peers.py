@@ -119,3 +119,85 @@ def test_peer_selection_long_sequential_runs(torch_dev):
         v, got = g.match_select(reqs, arena)
         exp = bal.select(reqs, arena, v)
         _check(f"1M batch {k}", got, exp, g.state_np(), bal.state)
+
+
+def _expected_migration(e_old_addrs, old_state, e_new_addrs):
+    """new peer j keeps the state of the first unused old peer of the same (address, upstream)."""
+    used = set()
+    out = np.zeros(len(e_new_addrs), dtype=engine.PEER_STATE_DTYPE)
+    for j, key in enumerate(e_new_addrs):
+        for i, k2 in enumerate(e_old_addrs):
+            if k2 == key and i not in used:
+                used.add(i)
+                out[j] = old_state[i]
+                break
+    return out
+
+
+def test_plus_endpoint_update_and_migration(torch_dev):
+    """NGINX Plus endpoint updates (UpdateServersInPlus, configurator.go:442,467,489, no Reload):
+    gm_update_upstream swaps one upstream's servers, gm_peers_migrate carries the balancer state
+    (kept servers keep conns / current_weight / flags), and gm_select_peers then matches the
+    oracle on the config a reload with the new server lines would have rendered, state included."""
+    torch, dev = torch_dev
+    b = peers.peers_blob()
+    g = Gpu(torch, dev, b)
+    o = Oracle(b, 1)
+    bal = Balancer(o)
+    reqs, arena = peers.gen_requests(40_000, seed=records.SEED_BASE + 70, hot=(1, 4, 9))
+    v, got = g.match_select(reqs, arena)
+    exp = bal.select(reqs, arena, v)
+    _check("before the update", got, exp, g.state_np(), bal.state)
+    servers = {}
+    updates = [(1, [peers._addr(1, j) for j in range(5, 55)] + [f"10.77.0.{j}:9000" for j in range(1, 21)]),
+               (9, [peers._addr(9, j) for j in (6, 0, 2)] + ["10.9.9.9:80"]),
+               (4, [peers._addr(4, j) for j in range(0, 67, 2)] + ["10.4.9.1:8080"])]
+    for k, (u, sv) in enumerate(updates):
+        old_addrs = [g.e.peer_address(p) for p in range(g.n_peers)]
+        old_state = g.state_np()
+        old_n = g.n_peers
+        g.e.update_upstream(peers.upstream_name(u), sv)
+        servers[u] = sv
+        st = g.e.stats()
+        assert st["gen"] == 1   # configVersion unchanged by a Plus API update
+        new_n = st["n_peers"]
+        new_addrs = [g.e.peer_address(p) for p in range(new_n)]
+        new_state = torch.zeros(max(new_n, 1) * 16, dtype=torch.uint8, device=dev)
+        g.e.peers_migrate_ptr(g.state.data_ptr(), old_n, new_state.data_ptr(), new_n, g.s)
+        g.state, g.n_peers = new_state, new_n
+        exp_state = _expected_migration(old_addrs, old_state, new_addrs)
+        _check(f"migration {k}", np.zeros(0), np.zeros(0), g.state_np(), exp_state)
+        # the oracle on the re-rendered config, from the migrated state
+        o2 = Oracle(peers.peers_blob(servers=servers), 1)
+        bal2 = Balancer(o2)
+        assert bal2.n_peers == new_n
+        bal2.state[:] = exp_state
+        reqs, arena = peers.gen_requests(40_000, seed=records.SEED_BASE + 71 + k, hot=(1, 4, 9))
+        v, got = g.match_select(reqs, arena)
+        exp = bal2.select(reqs, arena, v)
+        _check(f"after update {k}", got, exp, g.state_np(), bal2.state)
+
+
+BIG = [("hash $arg_user", 1500), ("hash $arg_user consistent", 1200), ("ip_hash", 1100), ("random", 1300),
+       ("least_conn", 1500), ("", 3)]
+
+
+def test_large_upstreams_round_robin_fallback(torch_dev):
+    """a stateless method's round-robin fallback (empty hash key, > 20 down tries) in an
+    upstream past k_peer_seq's LDS capacity (SEQ_PEERS_MAX = 1024 peers) defers to nginx instead
+    of indexing past the LDS arrays; every other pick still matches the oracle."""
+    torch, dev = torch_dev
+    b = peers.peers_blob(upstreams=BIG)
+    g = Gpu(torch, dev, b)
+    o = Oracle(b, 1)
+    bal = Balancer(o)
+    reqs, arena = peers.gen_requests(60_000, seed=records.SEED_BASE + 80, upstreams=BIG)
+    v, got = g.match_select(reqs, arena)
+    exp = bal.select(reqs, arena, v)
+    _check("big upstreams", got, exp, g.state_np(), bal.state)
+    # the empty-key requests of the 1500-peer hash upstream deferred, the keyed ones picked
+    up = v["upstream_id"]
+    names = sorted(peers.upstream_name(u) for u in range(len(BIG) + 1))
+    hid = names.index(peers.upstream_name(0))
+    sel = (up == hid) & (v["action"] == 0)
+    assert (got[sel] == engine.GM_PEER_DEFER).any() and (got[sel] < g.n_peers).any()

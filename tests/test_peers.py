@@ -307,3 +307,41 @@ def test_oracle_state_accounting(pblob):
     assert int(bal.state["conns"].sum()) == len(real) - 1000
     down = bal.state["flags"] & engine.GM_PEER_DOWN
     assert not np.any(np.isin(real, np.nonzero(down)[0]))
+
+
+# ---------------------------------------------------------------- NGINX Plus endpoint updates
+# Configurator.UpdateEndpoints* push servers through Manager.UpdateServersInPlus with no reload
+# (configurator.go:442,467,489; manager.go:257-284): gm_update_upstream patches the live tables'
+# upstream section.  Its peer tables must equal a fresh compile of the config a reload with the
+# new server lines would have rendered.
+def _addresses(e):
+    st = e.stats()
+    return [e.peer_address(p) for p in range(st["n_peers"])]
+
+
+@pytest.mark.parametrize("u,servers", [
+    (1, [peers._addr(1, j) for j in range(5, 55)] + [f"10.77.0.{j}:9000" for j in range(1, 21)]),   # RR 70 -> 70
+    (9, [peers._addr(9, j) for j in (6, 0, 2)] + ["10.9.9.9:80"]),                                 # chash 7 -> 4
+    (9, ["10.9.9.9:80", "10.9.9.9:80"]),                       # chash naming one address twice: deferred
+    (4, [f"10.4.1.{j}:8080" for j in range(1, 1100)]),          # least_conn past SEQ_PEERS_MAX: deferred
+    (2, []),                                                     # every server removed
+])
+def test_update_upstream_equals_fresh_compile(pblob, u, servers):
+    e = engine.Engine(compile_only=True)
+    e.load(pblob, 4)
+    e.update_upstream(peers.upstream_name(u), servers)
+    f = engine.Engine(compile_only=True)
+    f.load(peers.peers_blob(servers={u: servers}), 4)
+    se, sf = e.stats(), f.stats()
+    for k in ("gen", "n_peers", "n_upstreams", "n_upstreams_deferred", "n_counters", "n_locations"):
+        assert se[k] == sf[k], k
+    assert _addresses(e) == _addresses(f)
+
+
+def test_update_upstream_unknown_name(pblob):
+    e = engine.Engine(compile_only=True)
+    e.load(pblob, 4)
+    n0 = e.stats()["n_peers"]
+    with pytest.raises(engine.GmError):
+        e.update_upstream("no-such-upstream", ["10.0.0.1:80"])
+    assert e.stats()["n_peers"] == n0   # the live tables stay
