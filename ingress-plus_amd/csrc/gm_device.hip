@@ -1133,6 +1133,7 @@ struct gm_ctx {
     int dev = 0;
     uint32_t flags = 0;
     int cu_count = 256;
+    double cap_scale = 1.0;                   // GM_SCRATCH_SCALE (test hook): internal WAF capacities
     std::shared_mutex gen_mu;                 // shared: enqueueing batches; exclusive: the swap
     Generation *gen = nullptr;
     std::mutex scr_mu;                        // the stream -> scratch map only
@@ -1240,11 +1241,17 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
     gm_ctx *c = new gm_ctx();
     c->dev = hip_device;
     c->flags = flags;
+    if (const char *sc = getenv("GM_SCRATCH_SCALE")) {
+        const double v = atof(sc);
+        if (v > 0 && v <= 1) c->cap_scale = v;
+    }
     if (!(flags & GM_CREATE_COMPILE_ONLY)) {
         if (hipSetDevice(hip_device) != hipSuccess) { t_err = "hipSetDevice failed"; delete c; return nullptr; }
         // the WAF scan's Bloom filter is dynamic LDS beyond the 64 KiB default
         const void *scans[] = {(const void *)k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH>, (const void *)k_waf_scan<1, SCAN_DEPTH>,
-                               (const void *)k_waf_scan<2, SCAN_DEPTH>, (const void *)k_waf_scan<3, SCAN_DEPTH>};
+                               (const void *)k_waf_scan<2, SCAN_DEPTH>, (const void *)k_waf_scan<3, SCAN_DEPTH>,
+                               (const void *)k_waf_direct<BLOOM_PK_PERM>, (const void *)k_waf_direct<1>,
+                               (const void *)k_waf_direct<2>, (const void *)k_waf_direct<3>};
         for (const void *f : scans)
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SCAN_LDS_BYTES) != hipSuccess) {
                 t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
@@ -1480,16 +1487,23 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     // truncated silently
     const uint32_t scan_blocks = (uint32_t)c->cu_count;
     const uint32_t W = scan_blocks * SCAN_WAVES;
-    const size_t ccap = 4 * (alen / 64 + 16384) * S->cand_mult;
-    const size_t pcap = ((size_t)n * 2 + 65536) * S->list_mult, jcap = ((size_t)n + 65536) * S->list_mult;
+    // (GM_SCRATCH_SCALE, a test hook: scales these defaults, so the overflow continuations run on
+    // batches small enough for the oracle)
+    const double sc = c->cap_scale;
+    auto scaled = [sc](size_t x, size_t lo) { return std::max<size_t>(lo, (size_t)((double)x * sc)); };
+    const size_t ccap = scaled(4 * (alen / 64 + 16384) * S->cand_mult, 4 * W);
+    const size_t pcap = scaled(((size_t)n * 2 + 65536) * S->list_mult, 64);
+    const size_t jcap = scaled(((size_t)n + 65536) * S->list_mult, 64);
     size_t set_need = 1;
     while (set_need < 2 * (pcap + jcap)) set_need <<= 1;
     size_t scan_tmp = 0;
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
     if ((e = grow(c, s, S->d_blk2rec, S->cap_blk, nblk))) return e;
-    if ((e = grow(c, s, S->d_cand, S->cap_cand, std::max<size_t>(ccap, (size_t)W * 4096)))) return e;
-    if ((e = grow(c, s, S->d_ccnt, S->cap_ccnt, W + scan_blocks))) return e;   // scan-wave + ctx-block counts
-    if ((e = grow(c, s, S->d_surv, S->cap_surv, std::min<size_t>((alen / 256 + 65536) * S->surv_mult, 0xFFFFFFFFu)))) return e;
+    if ((e = grow(c, s, S->d_cand, S->cap_cand, std::max<size_t>(ccap, scaled((size_t)W * 4096, 4 * W))))) return e;
+    // scan-wave counts, ctx-block counts, scan-wave resume chunks, ctx-region resume records
+    if ((e = grow(c, s, S->d_ccnt, S->cap_ccnt, 3 * (size_t)W + scan_blocks))) return e;
+    if ((e = grow(c, s, S->d_surv, S->cap_surv, std::min<size_t>(scaled((alen / 256 + 65536) * S->surv_mult, scan_blocks),
+                                                                 0xFFFFFFFFu)))) return e;
     if ((e = grow(c, s, S->d_pairs, S->cap_pairs, pcap))) return e;
     if ((e = grow(c, s, S->d_jobs, S->cap_jobs, jcap))) return e;
     if ((e = grow(c, s, S->d_cnt, S->cap_cnt, (size_t)n + 1))) return e;
@@ -1559,10 +1573,10 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     if (mark(1)) return GM_E_HIP;
     // persistent scan grid: one 1024-thread workgroup per CU (128 KiB LDS prefilter); every wave
     // owns a contiguous arena range and a private candidate region of wcap records
-    if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
-    else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
-    else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
-    else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen);
+    if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
+    else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
+    else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
+    else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
     HIPCHK(c, hipGetLastError());
     if (!serial && route_after) {   // the route beside the context filter, after the scan
         HIPCHK(c, hipEventRecord(S->ev_fork, s));
@@ -1571,8 +1585,22 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     if (!serial && (e = launch_route())) return e;
     if (mark(2)) return GM_E_HIP;
     const uint32_t bcap = (uint32_t)std::min<size_t>(S->cap_surv / scan_blocks, 0xFFFFFFFFu);
+    // the continuation of overflowed candidate / survivor regions (a no-op launch otherwise)
+    auto launch_direct = [&](const uint8_t *DA, uint64_t dl, const gm_req *DR, const uint32_t *b2r, const Dedup &d,
+                             const uint64_t *dlp) -> int {
+        uint32_t *res = S->d_ccnt + W + scan_blocks, *cres = S->d_ccnt + 2 * W + scan_blocks;
+#define GM_DIRECT(PKV) k_waf_direct<PKV><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(DA, dl, DR, n, b2r, t, cand, wcap, \
+            S->d_ccnt, res, cres, S->d_pairs, (uint32_t)S->cap_pairs, S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, d, dlp)
+        if (t.bloom_pk == BLOOM_PK_PERM) GM_DIRECT(BLOOM_PK_PERM);
+        else if (t.bloom_pk == 1) GM_DIRECT(1);
+        else if (t.bloom_pk == 2) GM_DIRECT(2);
+        else GM_DIRECT(3);
+#undef GM_DIRECT
+        HIPCHK(c, hipGetLastError());
+        return GM_OK;
+    };
     k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, S->d_ccnt, W, t, S->d_surv, bcap, S->d_ccnt + W,
-                                                S->d_status);
+                                                S->d_status, S->d_ccnt + 2 * W + scan_blocks);
     HIPCHK(c, hipGetLastError());
     // join: blk2rec, the verdicts and the zeroed counts are complete before the exact check
     if (!serial) HIPCHK(c, hipStreamWaitEvent(s, S->ev_join, 0));
@@ -1581,6 +1609,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
                                                          S->d_ccnt + W, EXACT_SUB, S->d_pairs, (uint32_t)S->cap_pairs,
                                                          S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, dd, dlen);
     HIPCHK(c, hipGetLastError());
+    if ((e = launch_direct(A, alen, reqs, S->d_blk2rec, dd, dlen))) return e;
     if (mark(3)) return GM_E_HIP;
     if (t.n_sig_regex) {
         k_waf_regex<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(A, reqs, t, S->d_jobs, (uint32_t)S->cap_jobs, S->d_pairs,
@@ -1614,18 +1643,19 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         dd2.jepoch = S->epoch + 1;
         const uint8_t *SA = S->d_sarena;
         const gm_req *SR = S->d_sreqs;
-        if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen);
-        else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen);
-        else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen);
-        else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen);
+        if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
+        else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
+        else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
+        else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
         HIPCHK(c, hipGetLastError());
         k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, S->d_ccnt, W, t, S->d_surv, bcap, S->d_ccnt + W,
-                                                    S->d_status);
+                                                    S->d_status, S->d_ccnt + 2 * W + scan_blocks);
         HIPCHK(c, hipGetLastError());
         k_waf_exact<<<scan_blocks * EXACT_SUB, 256, 0, s>>>(SA, scap, SR, n, S->d_sblk, t, S->d_surv, bcap,
                                                              S->d_ccnt + W, EXACT_SUB, S->d_pairs, (uint32_t)S->cap_pairs,
                                                              S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, dd2, slen);
         HIPCHK(c, hipGetLastError());
+        if ((e = launch_direct(SA, scap, SR, S->d_sblk, dd2, slen))) return e;
         if (t.n_sig_regex) {
             k_waf_regex<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(SA, SR, t, S->d_jobs, (uint32_t)S->cap_jobs, S->d_pairs,
                                                                    (uint32_t)S->cap_pairs, dd2);
@@ -1636,7 +1666,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     // ---- hit emission: offsets by an exclusive scan of the per-request counts (request order)
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_temp, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
     k_hits_scatter<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(S->d_pairs, (uint32_t)S->cap_pairs, S->d_cnt, S->d_start,
-                                                              hit_ids, hit_cap, ctr, t.n_locs, S->d_status);
+                                                              hit_ids, hit_cap, ctr, t.n_locs, S->d_status, dd);
     HIPCHK(c, hipGetLastError());
     k_hits_finalize<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8)), 256, 0, s>>>(
         S->d_start, n, out, hit_ids, hit_cap, S->d_status);
@@ -1714,14 +1744,17 @@ int gm_sync(gm_ctx *c, void *stream) {
     }
     const uint32_t ov = S->h_status[3];
     // the next batch on this stream gets twice the buffer that overflowed (bounded)
-    if ((ov & 4u) && S->cand_mult < 64) S->cand_mult *= 2;
-    if ((ov & 8u) && S->surv_mult < 64) S->surv_mult *= 2;
-    if ((ov & 17u) && S->list_mult < 64) S->list_mult *= 2;
+    if ((ov & OV_CAND) && S->cand_mult < 64) S->cand_mult *= 2;
+    if ((ov & OV_SURV) && S->surv_mult < 64) S->surv_mult *= 2;
+    if ((ov & (OV_PAIRS | OV_JOBS | OV_SET)) && S->list_mult < 64) S->list_mult *= 2;
     if (S->h_status[PARSE_STATUS_WORD + 3]) return fail(c, GM_E_OVERFLOW, "gm_parse_requests: arena capacity exceeded");
     if (S->h_status[UPURI_STATUS_WORD]) return fail(c, GM_E_OVERFLOW, "gm_upstream_uris: output capacity exceeded");
-    if (ov & 2u) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded");
-    if (ov) return fail(c, GM_E_OVERFLOW, "WAF candidate / survivor / pair / job capacity exceeded "
-                                          "(the stream's buffers are doubled for the next batch: retry it)");
+    if (ov & OV_HITS) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded");
+    // candidate / survivor / pair / job overflows were completed on the device (k_waf_direct, the
+    // set-based scatter and regex runs): the batch is whole, the buffers grow for speed
+    if (ov & OV_SET) return fail(c, GM_E_OVERFLOW, "WAF dedupe set full (> 6 unique hits + regex jobs per request); "
+                                                   "it is doubled for the stream's next batch: retry it");
+    if (ov & 64u) return fail(c, GM_E_OVERFLOW, "decoded-view arena capacity exceeded");
     return GM_OK;
 }
 

@@ -130,9 +130,29 @@ def _regex_rule(rng, nocase):
     return pat, ex.encode()
 
 
-def gen_waf_sigset(n_lit: int = 8000, n_re: int = 2000, seed: int = 0xC0FFEE + 3) -> SigSet:
+def _job_regex_rule(rng, nocase):
+    """A regex whose required >= 4-byte factor is NOT a prefix (a class or alternation comes
+    first): the prefilter's factor hits become (request, zone, regex) jobs for k_waf_regex."""
+    t = int(rng.integers(0, 4))
+    w1 = _rand_word(rng, 4, 8)
+    w2 = _rand_word(rng, 4, 8)
+    if t == 0:
+        pat, ex = f"\\d+{w1}\\s+{w2}", f"42{w1}  {w2}"
+    elif t == 1:
+        pat, ex = f"[a-z]+_{w1}\\s", f"abc_{w1} "
+    elif t == 2:
+        pat, ex = f"(?:%27|'){w1}[=(]", f"'{w1}("
+    else:
+        pat, ex = f"[0-9a-f]{{2,}}{w1}.{{0,6}}{w2}", f"0a{w1}..{w2}"
+    if nocase:
+        ex = ex.upper()
+    return pat, ex.encode()
+
+
+def gen_waf_sigset(n_lit: int = 8000, n_re: int = 2000, seed: int = 0xC0FFEE + 3, job_frac: float = 0.0) -> SigSet:
     """C4: literals 4-32 B (SQLi/XSS/traversal-style tokens + random tails so that benign
-    text does not contain them) and RE2-subset regexes."""
+    text does not contain them) and RE2-subset regexes.  ``job_frac``: the share of regexes whose
+    factor is not a prefix (k_waf_regex jobs; 0 keeps the headline set's random stream)."""
     rng = np.random.Generator(np.random.PCG64(seed ^ 0x5157))
     rules = []
     seen = set()
@@ -155,7 +175,10 @@ def gen_waf_sigset(n_lit: int = 8000, n_re: int = 2000, seed: int = 0xC0FFEE + 3
         rules.append(Rule("lit", nocase, _zones(rng), b, ex))
     for _ in range(n_re):
         nocase = rng.random() < 0.5
-        pat, ex = _regex_rule(rng, nocase)
+        if job_frac > 0 and rng.random() < job_frac:
+            pat, ex = _job_regex_rule(rng, nocase)
+        else:
+            pat, ex = _regex_rule(rng, nocase)
         rules.append(Rule("re", nocase, _zones(rng), pat, ex))
     order = rng.permutation(len(rules))
     return SigSet([rules[i] for i in order])
@@ -166,7 +189,8 @@ def gen_waf_sigset(n_lit: int = 8000, n_re: int = 2000, seed: int = 0xC0FFEE + 3
 # required word in every regex).  The stress variant drops both: literals are plain SQL / HTML /
 # shell vocabulary (two or three words) that benign text (records.gen_c4(stress=True)) also
 # speaks, and 10% of the regexes have no >= 4-byte factor, so every (request, zone) runs them
-# (k_waf_always); the other regexes keep the headline's shapes.  The prefilter passes far more
+# (k_waf_always); another 10% have a factor that is not a prefix (k_waf_regex jobs); the other
+# regexes keep the headline's shapes.  The prefilter passes far more
 # windows, the exact stage verifies real matches, and the always-run DFAs carry the load.
 VOCAB = ("select", "from", "where", "union", "insert", "into", "update", "delete", "drop", "table", "order",
          "group", "by", "having", "limit", "offset", "join", "inner", "outer", "left", "values", "set",
@@ -199,6 +223,7 @@ def gen_waf_sigset_stress(n_lit: int = 8000, n_re: int = 2000, seed: int = 0xC0F
         b = s.encode()
         rules.append(Rule("lit", nocase, _zones(rng), b, b.upper() if nocase and rng.random() < 0.5 else b))
     n_always = n_re // 10
+    n_jobs = n_re // 10
     for i in range(n_re):
         nocase = rng.random() < 0.5
         if i < n_always:   # no >= 4-byte factor: every (request, zone) runs it (k_waf_always)
@@ -217,6 +242,9 @@ def gen_waf_sigset_stress(n_lit: int = 8000, n_re: int = 2000, seed: int = 0xC0F
             if nocase:
                 ex = ex.upper()
             rules.append(Rule("re", nocase, _zones(rng), pat, ex.encode()))
+        elif i < n_always + n_jobs:   # the factor is not a prefix: k_waf_regex jobs
+            pat, ex = _job_regex_rule(rng, nocase)
+            rules.append(Rule("re", nocase, _zones(rng), pat, ex))
         else:
             pat, ex = _regex_rule(rng, nocase)
             rules.append(Rule("re", nocase, _zones(rng), pat, ex))

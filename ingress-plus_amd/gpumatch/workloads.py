@@ -155,6 +155,12 @@ def c4_sigset(n_lit=8000, n_re=2000) -> sigs.SigSet:
     return sigs.gen_waf_sigset(n_lit, n_re)
 
 
+def c4_job_sigset(n_lit=200, n_re=300) -> sigs.SigSet:
+    """A small C4-shaped set whose regexes are mostly factor-but-not-prefix shapes: the regex-job
+    path (k_waf_regex) carries load (it had none in any benchmarked workload)."""
+    return sigs.gen_waf_sigset(n_lit, n_re, seed=0xC0FFEE + 21, job_frac=0.8)
+
+
 def c4_bench_generation():
     """The benchmarked C4 generation (bench.py): the 10k-rule set on the cafe Ingress in
     wallarm_mode block, with a benign traffic sample (disjoint seed) steering the prefilter's

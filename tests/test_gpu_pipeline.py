@@ -188,3 +188,88 @@ def test_normalize_after_overflow_syncs_clean(torch_dev):
     out = d_a.cpu().numpy().tobytes()
     ol = d_ol.cpu().numpy()
     assert [out[16 * i:16 * i + int(ol[i])] for i in range(len(paths))] == [b"/a/c", b"/x/y", b"/A/"]
+
+
+# ---------------------------------------------------------------- internal overflow completes
+# a batch that overflows an internal WAF buffer must complete on the device.  The
+# scan's candidate regions and the context filter's survivor regions are finished by
+# k_waf_direct; an overflowing pair or job list is replaced by the dedupe set (k_hits_scatter /
+# k_waf_regex read it).  GM_SCRATCH_SCALE (read at gm_create) shrinks the default capacities so
+# that every continuation runs on a batch the oracle checks in seconds.
+OV_PAIRS, OV_CAND, OV_SURV, OV_JOBS = 1, 4, 8, 128
+
+
+def _engine_scaled(scale):
+    import os
+    old = os.environ.get("GM_SCRATCH_SCALE")
+    os.environ["GM_SCRATCH_SCALE"] = str(scale)
+    try:
+        return engine.Engine(0)
+    finally:
+        if old is None:
+            del os.environ["GM_SCRATCH_SCALE"]
+        else:
+            os.environ["GM_SCRATCH_SCALE"] = old
+
+
+@pytest.mark.parametrize("scale,want", [(0.002, OV_CAND | OV_SURV), (0.0002, OV_CAND | OV_SURV | OV_PAIRS)])
+def test_internal_overflow_completes_on_device(torch_dev, scale, want):
+    """The stress variant (many candidates, real matches) on a fresh stream with shrunken internal
+    buffers: the first call returns GM_OK, the overflow bits show which continuations ran, and
+    verdicts and hit ids equal the oracle's."""
+    ss, b = workloads.c4_stress_generation()
+    reqs, arena = records.gen_c4(6_000, ss, seed=workloads.C4_STRESS_POOL_SEED + 7, plant_rate=0.3, stress=True)
+    e = _engine_scaled(scale)
+    e.load(b, 5)
+    got, gh = e.match_host(reqs, arena)          # no GmError: the batch completed
+    ov = int(e.debug_status()[3])
+    assert ov & want == want, f"overflow bits {ov:#x}, expected {want:#x} (continuations not exercised)"
+    exp, eh = Oracle(b, 5).match(reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, f"overflow continuation (scale {scale})")
+
+
+def test_job_list_overflow_runs_jobs_from_set(torch_dev):
+    """Factor regexes that are not prefix-mode (k_waf_regex jobs) with a shrunken job list: the
+    jobs run from the dedupe set and every hit equals the oracle's."""
+    ss = workloads.c4_job_sigset()
+    reqs, arena = records.gen_c4(8_000, ss, seed=records.SEED_BASE + 91, plant_rate=0.5, pool_mb=4)
+    b = workloads.c4_blob(ss)
+    e = _engine_scaled(0.0002)
+    e.load(b, 6)
+    got, gh = e.match_host(reqs, arena)
+    st = e.stats()
+    ov = int(e.debug_status()[3])
+    assert st["last_jobs"] > 0 and ov & OV_JOBS, f"jobs {st['last_jobs']}, overflow bits {ov:#x}"
+    exp, eh = Oracle(b, 6).match(reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "job list overflow")
+
+
+def test_stress_first_batch_default_sizing(torch_dev):
+    """bench.py's stress leg at default sizing on a fresh stream: its first batch (which used to
+    be void) returns GM_OK and equals the same batch run again once the stream's buffers grew."""
+    torch, dev = torch_dev
+    ss, b = workloads.c4_stress_generation()
+    preqs, parena = records.gen_c4(200_000, ss, seed=workloads.C4_STRESS_POOL_SEED, stress=True, pool_mb=8)
+    n = 2_000_000
+    reqs, plen, reps, alen = workloads.replicate_pool(preqs, len(parena), n)
+    d_pool = torch.from_numpy(np.ascontiguousarray(parena)).to(dev)
+    d_arena = torch.zeros(reps * plen + 1024, dtype=torch.uint8, device=dev)
+    for k in range(reps):
+        d_arena[k * plen:k * plen + len(parena)].copy_(d_pool)
+    d_reqs = torch.from_numpy(reqs.view(np.uint8).reshape(-1)).to(dev)
+    cap = 4 * n + (1 << 20)
+    outs = []
+    e = engine.Engine(0)
+    e.load(b, 2)
+    s = torch.cuda.current_stream().cuda_stream
+    ovs = []
+    for _ in range(2):
+        d_out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+        d_hits = torch.zeros(cap, dtype=torch.int32, device=dev)
+        e.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), alen, n, d_out.data_ptr(), d_hits.data_ptr(), cap, s)
+        e.sync(s)                                # GM_OK on the first call
+        ovs.append(int(e.debug_status()[3]))
+        tot = e.stats()["last_hits"]
+        outs.append((d_out.cpu().numpy(), d_hits[:tot].cpu().numpy()))
+    assert ovs[0] & (OV_CAND | OV_SURV), f"first batch did not overflow ({ovs[0]:#x}): the test lost its point"
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
