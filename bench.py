@@ -44,7 +44,14 @@ def main():
                     help="skip the scan-alone measurement (profiling runs: kernel stats of the pipeline only)")
     ap.add_argument("--serial", action="store_true",
                     help="measurement: the route stage alone before the scan (GM_CREATE_SERIAL)")
+    ap.add_argument("--config", default="c4", choices=("c4", "c5"),
+                    help="c4: the headline (default); c5: BASELINE configs[4], a request stream sharded "
+                         "over the ranks with the hit counters all-reduced (--stream, --batch)")
+    ap.add_argument("--stream", type=int, default=100_000_000, help="c5: requests in the whole stream")
+    ap.add_argument("--batch", type=int, default=10_000_000, help="c5: requests per gm_match_batch")
     args = ap.parse_args()
+    if args.config == "c5":
+        return c5_main(args)
 
     import torch
     from gpumatch import engine, records, workloads
@@ -196,6 +203,100 @@ def main():
     if dist:
         dist.destroy_process_group()
     print(json.dumps(result), flush=True)
+
+
+def c5_main(args):
+    """BASELINE.json configs[4]: mergeable Ingresses (1k hosts, wildcard TLS), a --stream request
+    stream sharded contiguously over WORLD_SIZE ranks (gpumatch.shard: the same slice / batch /
+    reduce code tests/test_multi_cpu.py drives with gloo), each rank's slice resident in HBM and
+    classified in --batch requests per gm_match_batch; after every step the per-location hit
+    counters are all-reduced out of place with RCCL (gm_counters_allreduce).  Weak scaling is not
+    this config's shape: the stream's size is fixed, so "scaling" is "strong"."""
+    import torch
+    from gpumatch import engine, shard, workloads
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    t0 = time.time()
+    blob = workloads.c5_blob()
+    eng = engine.Engine(local, profile=True)
+    eng.load(blob, 1)
+    preqs, parena = workloads.gen_c5(min(args.pool, 200_000))
+    lo, hi = shard.shard_bounds(args.stream, world, rank)
+    reqs, plen, first, ncopies, alen = shard.stream_records(preqs, len(parena), lo, hi)
+    n = hi - lo
+    dev = torch.device("cuda", local)
+    d_pool = torch.from_numpy(np.ascontiguousarray(parena)).to(dev)
+    d_arena = torch.zeros(ncopies * plen + 1024, dtype=torch.uint8, device=dev)
+    for k in range(ncopies):
+        d_arena[k * plen:k * plen + len(parena)].copy_(d_pool)
+    del d_pool
+    d_reqs = torch.from_numpy(reqs.view(np.uint8).reshape(-1)).to(dev)
+    d_out = torch.empty(max(n, 1) * 32, dtype=torch.uint8, device=dev)
+    d_hits = torch.empty(1 << 16, dtype=torch.int32, device=dev)
+    alg = workloads.algorithmic_bytes(reqs, "c5")
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] C5: stream [{lo}, {hi}) of {args.stream}, {ncopies} pool copies ({alen / 1e9:.2f} GB) "
+        f"resident; setup {time.time() - t0:.1f}s")
+    obj = [engine.Engine.comm_unique_id() if rank == 0 else None]
+    if dist:
+        dist.broadcast_object_list(obj, src=0)
+    eng.comm_init(obj[0], world, rank)
+    stream = torch.cuda.current_stream().cuda_stream
+    route_ms = []
+
+    def classify(b0, b1):   # positions relative to this rank's slice
+        eng.match_ptr(d_reqs.data_ptr() + 64 * b0, d_arena.data_ptr(), alen, b1 - b0, d_out.data_ptr() + 32 * b0,
+                      d_hits.data_ptr(), 1 << 16, stream)
+
+    def after_step(_step):
+        eng.counters_allreduce(stream)   # job-wide totals, out of place
+        eng.sync(stream)
+        route_ms.append(eng.stats()["last_ms_route"])
+
+    shard.run_stream(classify, 0, n, args.batch, after_step, steps=max(1, args.warmup))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    route_ms.clear()
+    t_start = time.perf_counter()
+    shard.run_stream(classify, 0, n, args.batch, after_step, steps=args.steps)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # the reduced totals: every rank's locations, steps + warmup times the stream
+    tot = eng.counters_global()
+    st = eng.stats()
+    routed = int(tot[:st["n_locations"]].sum())
+    log(f"[rank {rank}] {args.steps} steps in {elapsed:.3f}s; job-wide location hits {routed}")
+    if rank == 0:
+        print(json.dumps({
+            "metric": "requests/sec (C5: mergeable Ingresses, 1k hosts incl. wildcard TLS, request stream sharded "
+                      "over the GPUs, hit-counter all-reduce)",
+            "value": args.stream * args.steps / elapsed, "unit": "requests/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (workloads.gen_c5 pool, Zipf(1.1) hosts, replicated into the stream)",
+            "config": {"workload": "C5: mergeable Ingresses, 1000 hosts x 1-8 minions, wildcard TLS",
+                       "stream_requests": args.stream, "batch": args.batch,
+                       "parallelism": f"dp{world} (contiguous stream shards, RCCL counter all-reduce)"},
+            "route_ms_per_batch_last": float(np.mean(route_ms)) if route_ms else None,
+            "algorithmic_GBps": alg * world * args.steps / elapsed / 1e9,
+            "job_location_hits": routed}), flush=True)
+    if dist:
+        dist.destroy_process_group()
 
 
 def stress_leg(torch, engine, records, workloads, args, local):

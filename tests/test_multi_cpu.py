@@ -89,3 +89,91 @@ def test_two_rank_gloo_shards_match_single_batch(tmp_path):
     for step in range(1, STEPS + 1):
         assert np.array_equal(np.load(tmp_path / f"counters_{step}.npy"), step * _counters(v, h, 8, n_rules))
     assert len(h) > 0
+
+
+# ---------------------------------------------------------------- C5: a sharded request stream
+# BASELINE.json configs[4] through the same gpumatch.shard code bench.py --config c5 runs with
+# libgpumatch and RCCL: stream_records (a rank's contiguous slice of a stream that repeats a
+# pool), run_stream (the slice in batches, a counter reduction after every step) and
+# StreamCounters (cumulative local counters, out-of-place totals).  The oracle classifies and
+# gloo reduces here.
+C5_STREAM, C5_POOL, C5_BATCH = 5000, 1700, 700
+
+
+def _c5_pool():
+    return workloads.c5_blob(n_hosts=60), workloads.gen_c5(C5_POOL, n_hosts=60)
+
+
+def _c5_arena(parena, plen, ncopies):
+    a = np.zeros(ncopies * plen, dtype=np.uint8)
+    for k in range(ncopies):
+        a[k * plen:k * plen + len(parena)] = parena
+    return a
+
+
+def _c5_rank(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    blob, (preqs, parena) = _c5_pool()
+    o = Oracle(blob, 1)
+    n_locs = 4096   # >= the generation's locations (60 hosts x <= 8 minions x <= 2 paths)
+    lo, hi = shard.shard_bounds(C5_STREAM, world, rank)
+    reqs, plen, first, ncopies, alen = shard.stream_records(preqs, len(parena), lo, hi)
+    arena = _c5_arena(parena, plen, ncopies)
+
+    def reduce(x):
+        t = torch.from_numpy(x)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t.numpy()
+    ctr = shard.StreamCounters(n_locs, reduce)
+    verdicts = {}
+
+    def classify(b0, b1):
+        v, _ = o.match(reqs[b0:b1], arena, nthreads=1)
+        loc = v["location_id"][v["location_id"] != 0xFFFFFFFF].astype(np.int64)
+        ctr.add(np.bincount(loc, minlength=n_locs))
+        verdicts[b0] = v
+        return v
+
+    def after_step(step):
+        tot = ctr.reduce()
+        if rank == 0:
+            np.save(os.path.join(out_dir, f"c5_counters_{step}.npy"), tot)
+    shard.run_stream(classify, 0, hi - lo, C5_BATCH, after_step, steps=2)
+    mine = np.concatenate([verdicts[k] for k in sorted(verdicts)])
+    gathered = [None] * world
+    dist.all_gather_object(gathered, mine.tobytes())
+    if rank == 0:
+        np.save(os.path.join(out_dir, "c5_verdicts.npy"),
+                np.concatenate([np.frombuffer(b, dtype=records.VERDICT_DTYPE) for b in gathered]))
+    dist.destroy_process_group()
+
+
+def test_stream_records_slices_the_repeated_pool():
+    """Stream positions map to (copy, pool record): a slice's records are the pool's, rebased onto
+    the copies the slice spans."""
+    _, (preqs, parena) = _c5_pool()
+    full, plen, f0, n0, alen0 = shard.stream_records(preqs, len(parena), 0, C5_STREAM)
+    assert f0 == 0 and n0 == (C5_STREAM + C5_POOL - 1) // C5_POOL
+    for lo, hi in [(0, 10), (1690, 1720), (3400, 5000), (777, 777)]:
+        part, _, first, ncopies, alen = shard.stream_records(preqs, len(parena), lo, hi)
+        if hi == lo:
+            assert len(part) == 0 and ncopies == 0
+            continue
+        assert np.array_equal(part["uri_len"], full["uri_len"][lo:hi])
+        assert np.array_equal(part["base"] + np.uint64(first * plen), full["base"][lo:hi])
+        assert first == lo // C5_POOL and first + ncopies - 1 == (hi - 1) // C5_POOL
+
+
+def test_two_rank_gloo_c5_stream_matches_single_process(tmp_path):
+    mp.spawn(_c5_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    blob, (preqs, parena) = _c5_pool()
+    reqs, plen, _, ncopies, _ = shard.stream_records(preqs, len(parena), 0, C5_STREAM)
+    v, _ = Oracle(blob, 1).match(reqs, _c5_arena(parena, plen, ncopies), nthreads=2)
+    got = np.load(tmp_path / "c5_verdicts.npy")
+    assert got.tobytes() == v.tobytes()
+    loc = v["location_id"][v["location_id"] != 0xFFFFFFFF].astype(np.int64)
+    one = np.bincount(loc, minlength=4096)
+    for step in (1, 2):
+        assert np.array_equal(np.load(tmp_path / f"c5_counters_{step}.npy"), step * one)
+    assert one.sum() > C5_STREAM // 10   # about half the stream is plain http: redirected before a location
