@@ -189,6 +189,9 @@ typedef struct gm_stats_t {
     /* regex locations of large servers (> RLOC_SEQ_MAX): union-DFA slices in LDS (0: the factor
      * prefilter runs them) */
     uint32_t n_rsl_slices;
+    /* servers whose regex locations stay behind the factor prefilter (a regex no union group
+     * can hold): k_rloc answers them */
+    uint32_t n_rk_prefilter;
 } gm_stats_t;
 
 /* Request parsers (Wallarm's) a signature set can declare ("@decoders" line of

@@ -1843,7 +1843,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             std::vector<uint32_t> single;
             form_groups(comps, ord_a, [](uint32_t, uint32_t) { return true; }, gm_a, gd_a, single);
             form_groups(comps, ord_u, [](uint32_t, uint32_t) { return true; }, gm_u, gd_u, single);
-            if (!single.empty()) { h.n_rk_prefilter++; continue; }
+            if (!single.empty()) { h.n_rk_prefilter++; st.n_rk_prefilter++; continue; }
             std::vector<std::vector<uint32_t>> gmem;
             std::vector<MultiDfa> gdfa;
             for (size_t ia = 0, iu = 0; ia < gm_a.size() || iu < gm_u.size();) {

@@ -1492,10 +1492,12 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     const double sc = c->cap_scale;
     auto scaled = [sc](size_t x, size_t lo) { return std::max<size_t>(lo, (size_t)((double)x * sc)); };
     const size_t ccap = scaled(4 * (alen / 64 + 16384) * S->cand_mult, 4 * W);
-    const size_t pcap = scaled(((size_t)n * 2 + 65536) * S->list_mult, 64);
-    const size_t jcap = scaled(((size_t)n + 65536) * S->list_mult, 64);
+    const size_t pcap0 = ((size_t)n * 2 + 65536) * S->list_mult, jcap0 = ((size_t)n + 65536) * S->list_mult;
+    const size_t pcap = scaled(pcap0, 64), jcap = scaled(jcap0, 64);
+    // the dedupe set holds every unique pair and job of the batch (the lists' fallback when they
+    // overflow): sized from the unscaled list capacities
     size_t set_need = 1;
-    while (set_need < 2 * (pcap + jcap)) set_need <<= 1;
+    while (set_need < 2 * (pcap0 + jcap0)) set_need <<= 1;
     size_t scan_tmp = 0;
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
     if ((e = grow(c, s, S->d_blk2rec, S->cap_blk, nblk))) return e;
@@ -2078,8 +2080,11 @@ extern "C" int gm_parse_requests(gm_ctx *c, const uint8_t *wire, const gm_wire_m
     if ((e = grow(c, s, S->d_wsize, S->cap_wsize, (size_t)n + 1))) return e;
     if ((e = grow(c, s, S->d_wbase, S->cap_wbase, (size_t)n + 1))) return e;
     if ((e = grow(c, s, S->d_wtemp, S->cap_wtemp, tmp))) return e;
+    // the parser's waves are persistent (grid-stride): 8 waves per SIMD are resident (WIRE_OCC),
+    // i.e. 8 blocks per CU -- a larger grid would only queue, and its per-wave $uri scratch
+    // (WIRE_SCR each) would hold memory no resident wave uses
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + WIRE_WAVES - 1) / WIRE_WAVES,
-                                                                     (uint32_t)c->cu_count * 16));
+                                                                     (uint32_t)c->cu_count * 8));
     if ((e = grow(c, s, S->d_wscr, S->cap_wscr, (size_t)blocks * WIRE_WAVES * WIRE_SCR))) return e;
     if ((e = grow(c, s, S->d_wsum, S->cap_wsum, (size_t)n * sizeof(WireSum)))) return e;
     WireSum *wsum = reinterpret_cast<WireSum *>(S->d_wsum);

@@ -135,6 +135,11 @@ _EDGE = [
     b"GET / HTTP/1.1\r\nHost: a\r\nX: v \nY: w\r\n\r\n",                    # trailing SP, bare LF
     b"GET / HTTP/1.1\r\nHost: a\r\nX: v\r\r\nY: \r\nZ:\r\n\r\n",             # CR in a value, empties
     b"GET / HTTP/1.1\r\nHost: a\r\nX:  v\r\nY:v\r\n\r\n",                    # two spaces, none
+    b"GET http://[::1]:8080/v6?x=1 HTTP/1.1\r\nHost: other\r\n\r\n",            # IP-literal host
+    b"GET http://[v1.fe80::a+en1]/ HTTP/1.1\r\nHost: x\r\n\r\n",              # literal with sub-delims
+    b"GET http://[::1 HTTP/1.1\r\nHost: a\r\n\r\n",                            # unterminated literal: 400
+    b"GET http://[::1]x/ HTTP/1.1\r\nHost: a\r\n\r\n",                         # junk after ']': 400
+    b"GET http://[a/b]/ HTTP/1.1\r\nHost: a\r\n\r\n",                          # '/' inside: 400
 ]
 
 

@@ -1862,8 +1862,19 @@ static int orc_rl_parse(const uint8_t *b, int n, orc_rl_t *r) {
         if (i == s0 || i + 3 > n || b[i] != ':' || b[i + 1] != '/' || b[i + 2] != '/') return 400;
         i += 3;
         int h0 = i;
-        while (i < n && (isalnum(b[i]) || b[i] == '.' || b[i] == '-')) i++;
-        if (i == h0) return 400;
+        if (i < n && b[i] == '[') {          /* sw_host_ip_literal: "[" ... "]", the brackets kept */
+            for (i++; i < n && b[i] != ']'; i++) {
+                const uint8_t ch = b[i], c = ch | 0x20;
+                if ((ch >= '0' && ch <= '9') || (c >= 'a' && c <= 'z')) continue;
+                if (ch && strchr(":-._~!$&'()*+,;=", ch)) continue;   /* unreserved, sub-delims */
+                return 400;
+            }
+            if (i >= n) return 400;
+            i++;
+        } else {
+            while (i < n && (isalnum(b[i]) || b[i] == '.' || b[i] == '-')) i++;
+            if (i == h0) return 400;
+        }
         r->uhost = b + h0; r->uhost_len = i - h0;
         if (i < n && b[i] == ':') { i++; while (i < n && b[i] >= '0' && b[i] <= '9') i++; }
         if (i >= n) return 400;

@@ -317,11 +317,14 @@ def test_empty_and_generation_swap(eng):
 
 
 def test_c3_regex_locations_parity(eng):
-    """C3: 1k regex locations (factor prefilter path), URIs 32-256 B, 40 % crafted to hit;
-    PCRE-only locations reached in order give GM_ACT_UNSUPPORTED on both sides."""
+    """C3: 1k regex locations, all in union-DFA slices (k_rloc_multi: the stats pin that path, no
+    server is left to the factor prefilter), URIs 32-256 B, 40 % crafted to hit; PCRE-only
+    locations reached in order give GM_ACT_UNSUPPORTED on both sides."""
     regs = workloads.c3_regexes()
     reqs, arena = workloads.gen_c3(50_000, regs)
     got, gh, exp, eh = run_both(eng, workloads.c3_blob(regs), reqs, arena)
+    st = eng.stats()
+    assert st["n_rsl_slices"] > 0 and st["n_rk_prefilter"] == 0, st
     assert_verdicts_equal(got, exp, gh, eh, "c3")
     hit = np.isin(got["location_id"], np.arange(3, len(regs) + 3))
     assert 0.3 < hit.mean() < 0.99
@@ -391,3 +394,39 @@ def test_grpc_return_and_unsupported_constructs_on_gpu(eng):
     assert got[8]["action"] == 2 and got[8]["status"] == 418           # the `if` before it answers first
     eng.load(b, 2)
     assert eng.stats()["n_rejected_other"] == 2
+
+
+def test_regex_locations_factor_prefilter_fallback(eng):
+    """A server whose regex locations include one no union-DFA group can hold (2^11-state DFA,
+    more rows than ALW_GROUP_BYTES) stays on the factor prefilter (k_rloc, gm_compile.cpp): the
+    stats pin the path, and every verdict equals the oracle's -- the big regex, the ones before
+    and after it in config order, and URIs that match none."""
+    pats = [("~", f"^/r{i}/[0-9]+$") for i in range(10)] + [("~", "/[ab]*a[ab]{10}z")] + \
+           [("~*", r"\.JPG$"), ("~", r"^/api/v[0-9]/"), ("~", "/abz")]
+    locs = "".join(f'    location {op} "{p}" {{ return 2{i:02d}; }}\n' for i, (op, p) in enumerate(pats))
+    conf = ("http {\n  server {\n    listen 80 default_server;\n    server_name f.example.com;\n"
+            "    location / { return 404; }\n" + locs + "  }\n}\n")
+    b = blob.make_blob(conf, {})
+    rng = np.random.default_rng(17)
+    uris = []
+    for _ in range(20_000):
+        k = rng.integers(0, 6)
+        if k == 0:
+            uris.append(f"/r{rng.integers(0, 12)}/{rng.integers(0, 99999)}")
+        elif k == 1:
+            tail = "".join(rng.choice(list("ab"), rng.integers(10, 24)))
+            uris.append(f"/q/{tail}{'z' if rng.random() < 0.7 else 'y'}")
+        elif k == 2:
+            uris.append(f"/img/{rng.integers(0, 999)}.{'jpg' if rng.random() < 0.5 else 'JPG'}")
+        elif k == 3:
+            uris.append(f"/api/v{rng.integers(0, 12)}/x")
+        elif k == 4:
+            uris.append("/abz" if rng.random() < 0.5 else "/ab")
+        else:
+            uris.append("/" + "".join(rng.choice(list("abz/r0"), rng.integers(1, 40))))
+    reqs, arena = records.from_dicts([{"host": "f.example.com", "uri": u} for u in uris])
+    got, gh, exp, eh = run_both(eng, b, reqs, arena)
+    st = eng.stats()
+    assert st["n_rk_prefilter"] == 1 and st["n_rsl_slices"] == 0, st
+    assert_verdicts_equal(got, exp, gh, eh, "regex locations, factor prefilter")
+    assert len(np.unique(got["status"])) >= 8

@@ -29,6 +29,10 @@ EDGE_KATS = {
     25: 400, 26: 400, 27: 400, 28: 400,
     29: {"args": b"a=1&b=%zz"},
     30: 414, 31: 400, 32: 400,
+    # IP-literal hosts in the absolute form (nginx sw_host_ip_literal)
+    44: {"uri": b"/v6", "args": b"x=1", "host": b"[::1]", "ruri": b"/v6?x=1"},
+    45: {"uri": b"/", "host": b"[v1.fe80::a+en1]", "ruri": b"/"},
+    46: 400, 47: 400, 48: 400,
 }
 
 
