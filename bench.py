@@ -183,16 +183,18 @@ def main():
         # where the route shares the CUs
         eng_s = engine.Engine(local, profile=True, serial=True)
         eng_s.load(gblob, 1)
-        alone = []
+        alone, alone_route = [], []
         for k in range(1 + 3):
             eng_s.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), arena_len, n, d_out.data_ptr(), d_hits.data_ptr(),
                             hit_cap, stream.cuda_stream)
             eng_s.sync(stream.cuda_stream)
             if k:
                 alone.append(eng_s.stats()["last_ms_scan"])
+                alone_route.append(eng_s.stats()["last_ms_route"])
         eng_s.close()
         a_ms = float(np.mean(alone))
         result["roofline"]["scan_alone_ms"] = a_ms
+        result["stage_ms"]["route_alone"] = float(np.mean(alone_route))
         result["roofline"]["frac_alone"] = zone_bytes / (a_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
     if world == 1 and args.stress_requests > 0:
         del d_arena, d_reqs, d_out, d_hits

@@ -920,6 +920,8 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
 
 // ============================================================================ kernels
 constexpr int ROUTE_BLOCK = 256;
+// k_route's dynamic LDS: the hot route tables it stages (0 when they exceed ROUTE_STAGE_BYTES)
+inline uint32_t route_lds(const GTab &t) { return (t.hot_len + 15u) & ~15u; }
 // per-block location histogram in LDS (generations with more locations count with wave-aggregated
 // global atomics): 2 KiB, so a route block fits beside the WAF scan's 128 KiB Bloom + 24 KiB of
 // record staging in the CU's 160 KiB
@@ -930,7 +932,10 @@ constexpr uint32_t LDS_HIST_MAX = 512;
 // RK: the generation has prefiltered regex locations -- their step is deferred to k_rloc when
 // q.list is set (requests appended to q.list as {index, server}); TAIL: the second pass over
 // q.list, finishing each deferred request with k_rloc's location (q.loc).
-struct RlocQ { uint2 *list; uint32_t *count; int32_t *loc; };
+// st: per deferred request {$uri base (lo, hi), $uri length, server} -- what a union-DFA slice
+// pass needs, 16 B instead of the list entry plus the 64-B record (k_rloc_multi reads it once per
+// slice, and only for requests the slice can still answer)
+struct RlocQ { uint2 *list; uint32_t *count; int32_t *loc; uint4 *st; };
 template <int WPE, bool RK = false, bool TAIL = false>
 __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_route(const gm_req *__restrict__ reqs, uint32_t n,
                                                        const uint8_t *__restrict__ A, uint64_t arena_len,
@@ -946,12 +951,14 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
     __shared__ uint32_t hist[LDS_HIST_MAX];
     // the generation's hot tables in LDS (gm_tables.hpp ROUTE_STAGE_BYTES): every pointer into
     // the hot prefix is rebased onto the block's copy; generic (flat) loads then hit LDS
-    __shared__ uint4 hot[ROUTE_STAGE_BYTES / 16];
+    // (dynamic LDS, route_lds(): the generation's hot_len rounded up to 16 B, so that a route block
+    // beside the WAF scan takes only what this generation's tables need)
+    extern __shared__ uint4 hot[];
     const GTab &t = tg;
     HotTabs h{tg.ports, tg.names, tg.servers, tg.server_ifs, tg.small, tg.locs, tg.name_bytes};
     if (tg.hot_len) {
         const uint4 *src = reinterpret_cast<const uint4 *>(tg.hot_base);
-        for (uint32_t k = threadIdx.x; k < tg.hot_len / 16; k += blockDim.x) hot[k] = src[k];
+        for (uint32_t k = threadIdx.x; k < (tg.hot_len + 15) / 16; k += blockDim.x) hot[k] = src[k];
         const uint8_t *lb = reinterpret_cast<const uint8_t *>(hot);
         auto rb = [&](const void *p) { return lb + (reinterpret_cast<const uint8_t *>(p) - tg.hot_base); };
         h.ports = (const DPort *)rb(tg.ports);
@@ -973,7 +980,11 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
         const uint32_t i = TAIL ? q.list[x].x : x;
         const Rec r = load_rec(reqs + i);
         RoutePre pre;
+#ifdef GM_EXP_ROUTE_NOHOST   // measurement build: no host / URI loads (timing only)
+        for (int k = 0; k < 8; k++) { pre.hw[k] = 0x2E2E2E2Eu + k; pre.uw[k] = 0x2F2F2F2Fu + k; }
+#else
         route_prefetch(A, arena_len, r, pre);
+#endif
         RouteOut o;
         bool pend = false;
         route_one(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
@@ -986,7 +997,11 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
                 uint32_t b = 0;
                 if (lane == (uint32_t)leader) b = atomicAdd(q.count, (uint32_t)__popcll(pm));
                 b = __shfl(b, leader);
-                if (pend) q.list[b + (uint32_t)__popcll(pm & ((1ull << lane) - 1))] = make_uint2(i, o.server);
+                if (pend) {
+                    const uint32_t slot = b + (uint32_t)__popcll(pm & ((1ull << lane) - 1));
+                    q.list[slot] = make_uint2(i, o.server);
+                    q.st[slot] = make_uint4((uint32_t)r.base, (uint32_t)(r.base >> 32), r.uri_len, o.server);
+                }
             }
         }
         uint4 w0, w1;
@@ -1014,7 +1029,11 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
             hcnt[i] = 0;
             if (i + 1 == n) hcnt[n] = 0;
         }
+#ifdef GM_EXP_ROUTE_NOBLK   // measurement build: no blk2rec writes (timing only)
+        if (false) {
+#else
         if (blk2rec) {
+#endif
             // blocks whose start lies in [base_i, base_{i+1}) belong to record i
             uint64_t b0 = (i == 0) ? 0 : r.base;
             uint64_t b1 = (i + 1 < n) ? reqs[i + 1].base : arena_len;
@@ -1111,13 +1130,14 @@ struct Scratch {
     uint8_t *d_utemp = nullptr; size_t cap_utemp = 0;
     uint2 *d_rq = nullptr; size_t cap_rq = 0;            // regex-location requests deferred to k_rloc
     int32_t *d_rql = nullptr; size_t cap_rql = 0;        // and k_rloc's locations
+    uint4 *d_rqs = nullptr; size_t cap_rqs = 0;          // and each one's $uri span + server (k_rloc_multi)
     ~Scratch() {
         for (void *p : {(void *)d_status, (void *)d_blk2rec, (void *)d_cand, (void *)d_surv, (void *)d_pairs,
                         (void *)d_jobs, (void *)d_set, (void *)d_cnt, (void *)d_start, (void *)d_ccnt,
                         (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp, (void *)d_wscr, (void *)d_wsum,
                         (void *)d_pk, (void *)d_pseg, (void *)d_pprog, (void *)d_ppat, (void *)d_ptemp,
                         (void *)d_usize, (void *)d_utemp, (void *)d_sreqs, (void *)d_sarena, (void *)d_sblk,
-                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql})
+                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
         for (auto &e : ev) if (e) (void)hipEventDestroy(e);
@@ -1253,7 +1273,7 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
                                (const void *)k_waf_direct<BLOOM_PK_PERM>, (const void *)k_waf_direct<1>,
                                (const void *)k_waf_direct<2>, (const void *)k_waf_direct<3>};
         for (const void *f : scans)
-            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SCAN_LDS_BYTES) != hipSuccess) {
+            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)SCAN_DYN_LDS) != hipSuccess) {
                 t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
             }
         const void *alws[] = {(const void *)k_waf_always_multi<1>, (const void *)k_waf_always_multi<2>,
@@ -1441,8 +1461,9 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     const bool rk = t.rk_keys || t.n_rsl;
     if (rk) {
         int e2;
-        if ((e2 = grow(c, s, S->d_rq, S->cap_rq, n)) || (e2 = grow(c, s, S->d_rql, S->cap_rql, n))) return e2;
-        q = RlocQ{S->d_rq, S->d_status + RLOC_STATUS_WORD, S->d_rql};
+        if ((e2 = grow(c, s, S->d_rq, S->cap_rq, n)) || (e2 = grow(c, s, S->d_rql, S->cap_rql, n)) ||
+            (e2 = grow(c, s, S->d_rqs, S->cap_rqs, n))) return e2;
+        q = RlocQ{S->d_rq, S->d_status + RLOC_STATUS_WORD, S->d_rql, S->d_rqs};
     }
     auto launch_rloc = [&](hipStream_t rs, uint32_t tail_blocks) -> int {
         // union-DFA slices of the servers that have them (config order: a request answered by one
@@ -1453,10 +1474,10 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
             for (uint32_t k = t.n_alw_slices; k < t.n_alw_slices + t.n_rsl; k++) {
                 const dim3 grid((uint32_t)c->cu_count), blk(1024);
                 switch (sls[k].n_groups) {
-                case 1: k_rloc_multi<1><<<grid, blk, sls[k].len, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen, k); break;
-                case 2: k_rloc_multi<2><<<grid, blk, sls[k].len, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen, k); break;
-                case 3: k_rloc_multi<3><<<grid, blk, sls[k].len, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen, k); break;
-                default: k_rloc_multi<4><<<grid, blk, sls[k].len, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen, k); break;
+                case 1: k_rloc_multi<1><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k); break;
+                case 2: k_rloc_multi<2><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k); break;
+                case 3: k_rloc_multi<3><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k); break;
+                default: k_rloc_multi<4><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k); break;
                 }
                 HIPCHK(c, hipGetLastError());
             }
@@ -1465,14 +1486,14 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         }
         if (t.n_rk_prefilter)
             k_rloc<<<(uint32_t)c->cu_count * 4, RLOC_BLOCK, 0, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen);
-        k_route<3, true, true><<<tail_blocks, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk,
+        k_route<3, true, true><<<tail_blocks, ROUTE_BLOCK, route_lds(t), rs>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk,
                                                                     nullptr, 0, dlen, q);
         HIPCHK(c, hipGetLastError());
         return GM_OK;
     };
     if (!waf) {
-        if (rk) k_route<3, true><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, q);
-        else k_route<3><<<route_blocks, ROUTE_BLOCK, 0, s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen);
+        if (rk) k_route<3, true><<<route_blocks, ROUTE_BLOCK, route_lds(t), s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, q);
+        else k_route<3><<<route_blocks, ROUTE_BLOCK, route_lds(t), s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen);
         HIPCHK(c, hipGetLastError());
         if (rk) {
             const int e4 = launch_rloc(s, route_blocks);
@@ -1560,9 +1581,9 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         // raised issue priority beside the scan: the route's short latency-bound waves finish
         // early instead of stretching past the scan
         if (rk)
-            k_route<5, true><<<nb, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, q);
+            k_route<5, true><<<nb, ROUTE_BLOCK, route_lds(t), rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, q);
         else
-            k_route<5><<<nb, ROUTE_BLOCK, 0, rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen);
+            k_route<5><<<nb, ROUTE_BLOCK, route_lds(t), rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen);
         HIPCHK(c, hipGetLastError());
         int e3;
         if (rk && (e3 = launch_rloc(rs, nb))) return e3;
@@ -1571,20 +1592,27 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         S->route_side = true;
         return GM_OK;
     };
+#ifdef GM_EXP_ROUTE_FIRST   // measurement build: the route beside the scan, enqueued before it (older waves)
+    if (!serial && !route_after && (e = launch_route())) return e;
+#endif
     if (serial && (e = launch_route())) return e;
     if (mark(1)) return GM_E_HIP;
     // persistent scan grid: one 1024-thread workgroup per CU (128 KiB LDS prefilter); every wave
     // owns a contiguous arena range and a private candidate region of wcap records
-    if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
-    else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
-    else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
-    else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
+    if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
+    else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
+    else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
+    else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
     HIPCHK(c, hipGetLastError());
     if (!serial && route_after) {   // the route beside the context filter, after the scan
         HIPCHK(c, hipEventRecord(S->ev_fork, s));
         HIPCHK(c, hipStreamWaitEvent(S->side, S->ev_fork, 0));
     }
+#ifndef GM_EXP_ROUTE_FIRST
     if (!serial && (e = launch_route())) return e;
+#else
+    if (!serial && route_after && (e = launch_route())) return e;
+#endif
     if (mark(2)) return GM_E_HIP;
     const uint32_t bcap = (uint32_t)std::min<size_t>(S->cap_surv / scan_blocks, 0xFFFFFFFFu);
     // the continuation of overflowed candidate / survivor regions (a no-op launch otherwise)
@@ -1645,10 +1673,10 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         dd2.jepoch = S->epoch + 1;
         const uint8_t *SA = S->d_sarena;
         const gm_req *SR = S->d_sreqs;
-        if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
-        else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
-        else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
-        else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
+        if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
+        else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
+        else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
+        else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
         HIPCHK(c, hipGetLastError());
         k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, S->d_ccnt, W, t, S->d_surv, bcap, S->d_ccnt + W,
                                                     S->d_status, S->d_ccnt + 2 * W + scan_blocks);

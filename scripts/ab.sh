@@ -20,7 +20,7 @@ import json, sys
 line = [l for l in open(sys.argv[2]) if l.startswith("{")][-1]
 d = json.loads(line); r = d["roofline"]
 print(f"{sys.argv[1]:>8s} step {d['ms_per_step']:.3f} ms  scan {d['stage_ms']['scan']:.3f} route {d['stage_ms']['route']:.3f} "
-      f"verify {d['stage_ms']['verify']:.3f}  frac {r['frac']:.3f} alone {r.get('scan_alone_ms', 0):.3f} ({r.get('frac_alone', 0):.3f})", flush=True)
+      f"verify {d['stage_ms']['verify']:.3f} ralone {d['stage_ms'].get('route_alone', 0):.3f}  frac {r['frac']:.3f} alone {r.get('scan_alone_ms', 0):.3f} ({r.get('frac_alone', 0):.3f})", flush=True)
 PY
   done
 done
