@@ -519,6 +519,7 @@ struct RouteOut {
     uint32_t server, loc, ups, status;
     uint8_t action, kind, bucket, match;
     uint16_t waf;
+    int32_t pend_best;   // a request deferred to the regex-location kernels: its longest prefix match
 };
 
 // 32 arena bytes starting at `off` (any alignment) as 8 little-endian dwords, from three aligned
@@ -752,6 +753,9 @@ __device__ __noinline__ uint32_t split_generic(const uint8_t *A, const gm_req *r
 struct RoutePre { uint32_t hw[8], uw[8]; };
 __device__ __forceinline__ void route_prefetch(const uint8_t *A, uint64_t alen, const Rec &r, RoutePre &p) {
     const uint64_t f_uri = r.base, f_host = r.base + r.uri_len + r.args_len + r.hdr_len + r.body_len;
+    // (measured: loading all three blocks of both spans unconditionally, so that the compiler
+    // issues the six loads together, made the route slower -- 1.10 vs 0.85 ms per 10M C4 requests
+    // alone: the extra blocks are extra HBM lines)
     load_span_n(A, f_host, alen, min(r.host_len, 32u), p.hw);
     load_span_n(A, f_uri, alen, min(r.uri_len, 32u), p.uw);
 }
@@ -764,11 +768,14 @@ constexpr uint32_t RLOC_STATUS_WORD = 16;   // batch status word: requests defer
 // (URI <= RLOC_URI_CAP, n_rloc <= RLOC_BM_BITS) sets *pend and returns; >= -1 -- k_rloc's answer
 // (the location index, -1 none).  *sid_out: the server chosen (valid whenever *pend is set).
 constexpr int32_t RK_INLINE = -3, RK_DEFER = -2;
+__device__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
+                          RouteOut &o);
 __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const RoutePre &pre,
                           const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb, int32_t rk_in = RK_INLINE,
                           bool *pend = nullptr) {
     o.server = GM_NONE; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0;
     o.action = GM_ACT_NO_LISTENER; o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF;
+    o.pend_best = -1;
     const uint64_t f_uri = r.base, f_host = r.base + r.uri_len + r.args_len + r.hdr_len + r.body_len;
     // ---- listen port
     uint32_t pi = GM_NONE;
@@ -884,11 +891,20 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
             else if (S.rk_on && rk_in == RK_DEFER &&
                      (S.rsl_n || (r.uri_len <= RLOC_URI_CAP && S.n_rloc <= RLOC_BM_BITS))) {
                 *pend = true;
+                o.pend_best = best;
                 return;
             } else loc = rloc_first_match(*t.self, S, sid, u, r.uri_len, rkb);
             if (loc < 0) loc = best;
         }
     }
+    route_loc(A, rp, t, h, loc, o);
+}
+
+// The rest of route_one once the location is known (loc < 0: none): location kinds, rules and
+// split routes, return / proxy.  The regex-location tail pass starts here with k_rloc's answer
+// (or the request's longest prefix match) instead of routing the request again.
+__device__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
+                          RouteOut &o) {
     if (loc < 0) { o.action = GM_ACT_NOT_FOUND; o.status = 404; return; }
     o.loc = (uint32_t)loc;
     DLoc L = h.locs[loc];
@@ -920,12 +936,17 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
 
 // ============================================================================ kernels
 constexpr int ROUTE_BLOCK = 256;
-// k_route's dynamic LDS: the hot route tables it stages (0 when they exceed ROUTE_STAGE_BYTES)
-inline uint32_t route_lds(const GTab &t) { return (t.hot_len + 15u) & ~15u; }
-// per-block location histogram in LDS (generations with more locations count with wave-aggregated
-// global atomics): 2 KiB, so a route block fits beside the WAF scan's 128 KiB Bloom + 24 KiB of
-// record staging in the CU's 160 KiB
-constexpr uint32_t LDS_HIST_MAX = 512;
+// k_route's dynamic LDS: the hot route tables it stages (0 when they exceed ROUTE_STAGE_BYTES),
+// then the per-block location histogram when the generation's locations fit it -- at most
+// LDS_HIST_BESIDE entries beside the WAF scan (2 KiB: a route block fits beside the scan's Bloom
+// filter and record stages in the CU's 160 KiB), LDS_HIST_ALONE otherwise (C3's ~1000 regex
+// locations counted with one global atomic per request took most of the 3.5 ms tail pass)
+constexpr uint32_t LDS_HIST_BESIDE = 512, LDS_HIST_ALONE = 8192;
+inline uint32_t route_hot16(const GTab &t) { return (t.hot_len + 15u) & ~15u; }
+inline uint32_t route_hist_n(const GTab &t, bool beside) {
+    return t.n_locs <= (beside ? LDS_HIST_BESIDE : LDS_HIST_ALONE) ? t.n_locs : 0u;
+}
+inline uint32_t route_lds(const GTab &t, bool beside) { return route_hot16(t) + 4u * route_hist_n(t, beside); }
 
 // WPE: waves per SIMD the register allocation targets (beside the scan's workgroup, a CU has
 // room for route waves only when they are small)
@@ -935,7 +956,9 @@ constexpr uint32_t LDS_HIST_MAX = 512;
 // st: per deferred request {$uri base (lo, hi), $uri length, server} -- what a union-DFA slice
 // pass needs, 16 B instead of the list entry plus the 64-B record (k_rloc_multi reads it once per
 // slice, and only for requests the slice can still answer)
-struct RlocQ { uint2 *list; uint32_t *count; int32_t *loc; uint4 *st; };
+// best: the deferred request's longest prefix match (-1 none), where the tail pass starts when no
+// regex location matched
+struct RlocQ { uint2 *list; uint32_t *count; int32_t *loc; uint4 *st; int32_t *best; };
 template <int WPE, bool RK = false, bool TAIL = false>
 __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_route(const gm_req *__restrict__ reqs, uint32_t n,
                                                        const uint8_t *__restrict__ A, uint64_t arena_len,
@@ -943,12 +966,12 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
                                                        unsigned long long *__restrict__ counters,
                                                        uint32_t *__restrict__ blk2rec, uint32_t nblk,
                                                        uint32_t *__restrict__ hcnt, int prio,
-                                                       const uint64_t *__restrict__ dlen, RlocQ q = RlocQ{}) {
+                                                       const uint64_t *__restrict__ dlen, uint32_t hist_n,
+                                                       RlocQ q = RlocQ{}) {
     if (dlen) arena_len = *dlen;   // gm_batch.arena_len_dev: the length a producer wrote on the device
     // beside the WAF scan: issue priority over the scan's waves, so the route's short
     // latency-bound waves finish early instead of stretching past the scan (GM_ROUTE_PRIO)
     if (prio) __builtin_amdgcn_s_setprio(2);
-    __shared__ uint32_t hist[LDS_HIST_MAX];
     // the generation's hot tables in LDS (gm_tables.hpp ROUTE_STAGE_BYTES): every pointer into
     // the hot prefix is rebased onto the block's copy; generic (flat) loads then hit LDS
     // (dynamic LDS, route_lds(): the generation's hot_len rounded up to 16 B, so that a route block
@@ -969,26 +992,42 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
         h.locs = (const DLoc *)rb(tg.locs);
         h.name_bytes = rb(tg.name_bytes);
     }
-    const bool use_hist = t.n_locs <= LDS_HIST_MAX;
+    // the location histogram after the hot tables (hist_n = route_hist_n(): 0 = global atomics)
+    uint32_t *hist = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(hot) + ((tg.hot_len + 15u) & ~15u));
+    const bool use_hist = hist_n != 0;
     if (use_hist) for (uint32_t k = threadIdx.x; k < t.n_locs; k += blockDim.x) hist[k] = 0;
     // RK: servers with many regex locations -- the prefilter's key bit filter in LDS
     __shared__ uint32_t rkb[RK ? RK_BLOOM_WORDS : 1];
     if (RK) for (uint32_t k = threadIdx.x; k < RK_BLOOM_WORDS; k += blockDim.x) rkb[k] = t.rk_bloom[k];
     __syncthreads();
     const uint32_t nn = TAIL ? *q.count : n;
-    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nn; x += gridDim.x * blockDim.x) {
-        const uint32_t i = TAIL ? q.list[x].x : x;
-        const Rec r = load_rec(reqs + i);
-        RoutePre pre;
-#ifdef GM_EXP_ROUTE_NOHOST   // measurement build: no host / URI loads (timing only)
-        for (int k = 0; k < 8; k++) { pre.hw[k] = 0x2E2E2E2Eu + k; pre.uw[k] = 0x2F2F2F2Fu + k; }
-#else
-        route_prefetch(A, arena_len, r, pre);
-#endif
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nn; x += stride) {
+        uint32_t i = x;
         RouteOut o;
         bool pend = false;
-        route_one(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
-                  TAIL ? q.loc[x] : (RK && q.list ? RK_DEFER : RK_INLINE), &pend);
+        Rec r{};
+        if (TAIL) {
+            // a deferred request: its location is k_rloc's answer, else its longest prefix match
+            // (saved by the first pass); only the location's own step runs again
+            const uint2 e = q.list[x];
+            i = e.x;
+            int32_t loc = q.loc[x];
+            if (loc < 0) loc = q.best[x];
+            o.server = e.y; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0; o.action = GM_ACT_NO_LISTENER;
+            o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF; o.pend_best = -1;
+            route_loc(A, reqs + i, t, h, loc, o);
+        } else {
+            r = load_rec(reqs + i);
+            RoutePre pre;
+#ifdef GM_EXP_ROUTE_NOHOST   // measurement build: no host / URI loads (timing only)
+            for (int k = 0; k < 8; k++) { pre.hw[k] = 0x2E2E2E2Eu + k; pre.uw[k] = 0x2F2F2F2Fu + k; }
+#else
+            route_prefetch(A, arena_len, r, pre);
+#endif
+            route_one(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
+                      RK && q.list ? RK_DEFER : RK_INLINE, &pend);
+        }
         if (RK && !TAIL) {   // deferred to k_rloc: appended, one atomic per wave
             const unsigned long long pm = __ballot(pend);
             if (pm) {
@@ -1001,6 +1040,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
                     const uint32_t slot = b + (uint32_t)__popcll(pm & ((1ull << lane) - 1));
                     q.list[slot] = make_uint2(i, o.server);
                     q.st[slot] = make_uint4((uint32_t)r.base, (uint32_t)(r.base >> 32), r.uri_len, o.server);
+                    q.best[slot] = o.pend_best;
                 }
             }
         }
@@ -1012,17 +1052,23 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
         w1.w = o.status;
         uint4 *dst = reinterpret_cast<uint4 *>(out + i);
         if (!pend) { dst[0] = w0; dst[1] = w1; }
-        // per-location counter, aggregated over the wave: one atomic per distinct location
-        unsigned long long todo = __ballot(o.loc != GM_NONE);
-        while (todo) {
-            const int leader = __ffsll(todo) - 1;
-            const uint32_t lk = __shfl(o.loc, leader);
-            const unsigned long long same = __ballot(o.loc == lk) & todo;
-            if ((threadIdx.x & 63) == (uint32_t)leader) {
-                if (use_hist) atomicAdd(&hist[lk], (uint32_t)__popcll(same));
-                else atomicAdd(&counters[lk], (unsigned long long)__popcll(same));
+        // per-location counter: the wave's first location in one atomic for all its lanes (the
+        // common case: most of a wave's requests share a location), every other lane its own
+        // (a loop over the distinct locations ran ~50 rounds per wave on C3)
+        {
+            const bool has = o.loc != GM_NONE;
+            const unsigned long long act = __ballot(has);
+            if (act) {
+                const int leader = __ffsll(act) - 1;
+                const uint32_t lk = __shfl(o.loc, leader);
+                const unsigned long long same = __ballot(has && o.loc == lk);
+                const bool lead = (threadIdx.x & 63) == (uint32_t)leader, own = has && o.loc != lk;
+                if (lead || own) {
+                    const uint32_t ck = lead ? lk : o.loc, cv = lead ? (uint32_t)__popcll(same) : 1u;
+                    if (use_hist) atomicAdd(&hist[ck], cv);
+                    else atomicAdd(&counters[ck], (unsigned long long)cv);
+                }
             }
-            todo &= ~same;
         }
         if (TAIL) continue;
         if (hcnt) {   // the WAF stages' per-request hit counts start the batch at zero
@@ -1131,13 +1177,14 @@ struct Scratch {
     uint2 *d_rq = nullptr; size_t cap_rq = 0;            // regex-location requests deferred to k_rloc
     int32_t *d_rql = nullptr; size_t cap_rql = 0;        // and k_rloc's locations
     uint4 *d_rqs = nullptr; size_t cap_rqs = 0;          // and each one's $uri span + server (k_rloc_multi)
+    int32_t *d_rqb = nullptr; size_t cap_rqb = 0;        // and its longest prefix match (the tail pass)
     ~Scratch() {
         for (void *p : {(void *)d_status, (void *)d_blk2rec, (void *)d_cand, (void *)d_surv, (void *)d_pairs,
                         (void *)d_jobs, (void *)d_set, (void *)d_cnt, (void *)d_start, (void *)d_ccnt,
                         (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp, (void *)d_wscr, (void *)d_wsum,
                         (void *)d_pk, (void *)d_pseg, (void *)d_pprog, (void *)d_ppat, (void *)d_ptemp,
                         (void *)d_usize, (void *)d_utemp, (void *)d_sreqs, (void *)d_sarena, (void *)d_sblk,
-                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs})
+                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
         for (auto &e : ev) if (e) (void)hipEventDestroy(e);
@@ -1282,6 +1329,14 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
                               (const void *)k_rloc_multi<3>, (const void *)k_rloc_multi<4>};
         for (const void *f : alws)
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ALWAYS_LDS_BYTES) != hipSuccess) {
+                t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
+            }
+        // the route's hot tables + location histogram (route_lds)
+        const void *routes[] = {(const void *)k_route<3, true, true>, (const void *)k_route<3, true>,
+                                (const void *)k_route<3>, (const void *)k_route<5, true>, (const void *)k_route<5>};
+        for (const void *f : routes)
+            if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(ROUTE_STAGE_BYTES + 4 * LDS_HIST_ALONE)) != hipSuccess) {
                 t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
             }
         int cus = 0;
@@ -1462,8 +1517,8 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     if (rk) {
         int e2;
         if ((e2 = grow(c, s, S->d_rq, S->cap_rq, n)) || (e2 = grow(c, s, S->d_rql, S->cap_rql, n)) ||
-            (e2 = grow(c, s, S->d_rqs, S->cap_rqs, n))) return e2;
-        q = RlocQ{S->d_rq, S->d_status + RLOC_STATUS_WORD, S->d_rql, S->d_rqs};
+            (e2 = grow(c, s, S->d_rqs, S->cap_rqs, n)) || (e2 = grow(c, s, S->d_rqb, S->cap_rqb, n))) return e2;
+        q = RlocQ{S->d_rq, S->d_status + RLOC_STATUS_WORD, S->d_rql, S->d_rqs, S->d_rqb};
     }
     auto launch_rloc = [&](hipStream_t rs, uint32_t tail_blocks) -> int {
         // union-DFA slices of the servers that have them (config order: a request answered by one
@@ -1486,14 +1541,14 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         }
         if (t.n_rk_prefilter)
             k_rloc<<<(uint32_t)c->cu_count * 4, RLOC_BLOCK, 0, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen);
-        k_route<3, true, true><<<tail_blocks, ROUTE_BLOCK, route_lds(t), rs>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk,
-                                                                    nullptr, 0, dlen, q);
+        k_route<3, true, true><<<tail_blocks, ROUTE_BLOCK, route_lds(t, false), rs>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk,
+                                                                    nullptr, 0, dlen, route_hist_n(t, false), q);
         HIPCHK(c, hipGetLastError());
         return GM_OK;
     };
     if (!waf) {
-        if (rk) k_route<3, true><<<route_blocks, ROUTE_BLOCK, route_lds(t), s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, q);
-        else k_route<3><<<route_blocks, ROUTE_BLOCK, route_lds(t), s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen);
+        if (rk) k_route<3, true><<<route_blocks, ROUTE_BLOCK, route_lds(t, false), s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), q);
+        else k_route<3><<<route_blocks, ROUTE_BLOCK, route_lds(t, false), s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false));
         HIPCHK(c, hipGetLastError());
         if (rk) {
             const int e4 = launch_rloc(s, route_blocks);
@@ -1581,9 +1636,9 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         // raised issue priority beside the scan: the route's short latency-bound waves finish
         // early instead of stretching past the scan
         if (rk)
-            k_route<5, true><<<nb, ROUTE_BLOCK, route_lds(t), rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, q);
+            k_route<5, true><<<nb, ROUTE_BLOCK, route_lds(t, !serial), rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial), q);
         else
-            k_route<5><<<nb, ROUTE_BLOCK, route_lds(t), rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen);
+            k_route<5><<<nb, ROUTE_BLOCK, route_lds(t, !serial), rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial));
         HIPCHK(c, hipGetLastError());
         int e3;
         if (rk && (e3 = launch_rloc(rs, nb))) return e3;

@@ -263,13 +263,13 @@ __host__ __device__ inline uint32_t peer_draw(uint64_t lo, uint64_t hi, uint32_t
 // (Cp = C rounded up to even), then the state's emit mask and end mask (u32 each).  A transition
 // is the target row's byte offset in the group | ALW_EMIT (bit 0) when the target emits: the step
 // needs no multiply, and row 0 (the dead state) is all zeros.
-constexpr uint32_t ALWAYS_LDS_BYTES = 128 * 1024;
-constexpr uint32_t ALW_GROUP_BYTES = 32 * 1024;   // row byte offsets fit a u16 with the flag bit
+constexpr uint32_t ALWAYS_LDS_BYTES = 160 * 1024;
+constexpr uint32_t ALW_GROUP_BYTES = 64 * 1024 - 64;   // row byte offsets fit a u16 with the flag bit
 constexpr uint32_t ALW_GROUP_MAX = 32;
 constexpr uint32_t ALW_SLICE_GROUPS = 4;
 constexpr uint32_t ALW_BUILD_STATES = 8192;   // product states before minimisation
 constexpr uint32_t ALW_EMIT = 1;
-constexpr uint32_t ALW_ROW_MASK = 0x7FFE;
+constexpr uint32_t ALW_ROW_MASK = 0xFFFE;
 struct DAlwGroup {
     uint32_t tr_off;         // byte offset of row 0 from the slice start
     uint32_t mask_off;       // byte offset of the emit mask within a row (2 Cp); the end mask follows

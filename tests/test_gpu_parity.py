@@ -397,11 +397,11 @@ def test_grpc_return_and_unsupported_constructs_on_gpu(eng):
 
 
 def test_regex_locations_factor_prefilter_fallback(eng):
-    """A server whose regex locations include one no union-DFA group can hold (2^11-state DFA,
+    """A server whose regex locations include one no union-DFA group can hold (2^12-state DFA,
     more rows than ALW_GROUP_BYTES) stays on the factor prefilter (k_rloc, gm_compile.cpp): the
     stats pin the path, and every verdict equals the oracle's -- the big regex, the ones before
     and after it in config order, and URIs that match none."""
-    pats = [("~", f"^/r{i}/[0-9]+$") for i in range(10)] + [("~", "/[ab]*a[ab]{10}z")] + \
+    pats = [("~", f"^/r{i}/[0-9]+$") for i in range(10)] + [("~", "/[ab]*a[ab]{11}z")] + \
            [("~*", r"\.JPG$"), ("~", r"^/api/v[0-9]/"), ("~", "/abz")]
     locs = "".join(f'    location {op} "{p}" {{ return 2{i:02d}; }}\n' for i, (op, p) in enumerate(pats))
     conf = ("http {\n  server {\n    listen 80 default_server;\n    server_name f.example.com;\n"
