@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 5u   /* 5: gm_update_upstream / gm_peers_migrate; 4: union-DFA stats */
+#define GM_ABI_VERSION 6u   /* 6: n_rsl_reversed; 5: gm_update_upstream / gm_peers_migrate; 4: union-DFA stats */
 
 /* ---------------------------------------------------------------- status codes */
 #define GM_OK            0
@@ -192,6 +192,8 @@ typedef struct gm_stats_t {
     /* servers whose regex locations stay behind the factor prefilter (a regex no union group
      * can hold): k_rloc answers them */
     uint32_t n_rk_prefilter;
+    /* of n_rsl_slices: slices of X$ regex locations run backwards from the URI's end */
+    uint32_t n_rsl_reversed;
 } gm_stats_t;
 
 /* Request parsers (Wallarm's) a signature set can declare ("@decoders" line of

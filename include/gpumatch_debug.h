@@ -12,6 +12,9 @@ extern "C" {
 /* Compile `pat` with the engine's regex compiler and run the DFA on the host:
  * 1 match, 0 no match, < 0 rejected (-1 PCRE-only, -2 unsupported, -3 syntax, -4 too big). */
 int gm_debug_regex(const char *pat, int caseless, const uint8_t *subject, size_t n);
+/* The reversed DFA of an X$ pattern (compile_regex_reversed) run over the subject from its last
+ * byte backwards: 1 match, 0 no match, -1 not of the X$ form (or too big). */
+int gm_debug_regex_rev(const char *pat, int caseless, const uint8_t *subject, size_t n);
 /* Required-literal factors ('\n'-separated, case-folded) the WAF prefilter uses for `pat`;
  * returns the shortest factor length (0 = none), < 0 if rejected. */
 int gm_debug_regex_factors(const char *pat, int caseless, char *out, size_t cap);

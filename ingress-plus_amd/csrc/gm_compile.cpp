@@ -1331,6 +1331,10 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     std::vector<DServerIf> sifs;
     std::vector<DRegexLoc> rlocs;
     std::vector<std::vector<std::string>> rloc_factors;   // parallel to rlocs: >= 4-byte factors
+    // parallel to rlocs: the DFA of ^(\n)?rev(X) for an unanchored X$ (n_states 0: none) --
+    // union-DFA slices of these run backwards from the URI's end (gm_regex.hpp
+    // compile_regex_reversed) and die within a few bytes, where the forward search reads it all
+    std::vector<Dfa> rloc_rev;
     auto new_node = [&]() { nodes.push_back(DNode{-1, -1, -1, 0}); return (uint32_t)nodes.size() - 1; };
     auto walk = [&](uint32_t root, const std::string &p) {
         uint32_t cur = root;
@@ -1450,6 +1454,11 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 if (d < 0 || sup) dl.kind = LK_UNSUPPORTED;   // sup: the DFA is a superset
                 rlocs.push_back(DRegexLoc{d >= 0 ? (uint32_t)d : GM_NONE, (uint32_t)lid});
                 rloc_factors.push_back(std::move(fac));
+                Dfa rv;
+                if (d >= 0 && !sup && !(C.dfas[d].flags & DFA_ANCHOR_START) &&
+                    compile_regex_reversed(L.path, L.kind == RXI, 4096, rv))
+                    rloc_rev.push_back(std::move(rv));
+                else rloc_rev.push_back(Dfa{});
             }
         }
         D.n_rloc = (uint32_t)rlocs.size() - D.first_rloc;
@@ -1836,13 +1845,22 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             // anchored (^) and unanchored regexes in separate groups, each in config order: a
             // union of anchored regexes dies within a few bytes of most URIs; the groups are then
             // ordered by their first (lowest) member
-            std::vector<uint32_t> ord_a, ord_u;
-            for (uint32_t k = 0; k < D.n_rloc; k++) (comps[k]->anchored_start ? ord_a : ord_u).push_back(k);
-            std::vector<std::vector<uint32_t>> gm_a, gm_u;
-            std::vector<MultiDfa> gd_a, gd_u;
+            // X$ regexes with a reversed DFA form groups of their own (run backwards: slices
+            // flagged ALW_SLICE_REVERSED, packed first -- they are cheap, and the matches they
+            // find let later slices skip requests)
+            std::vector<uint32_t> ord_a, ord_u, ord_r;
+            std::vector<const Dfa *> rcomps(D.n_rloc, nullptr);
+            for (uint32_t k = 0; k < D.n_rloc; k++) {
+                const Dfa &rv = rloc_rev[D.first_rloc + k];
+                if (rv.n_states > 0) { rcomps[k] = &rv; ord_r.push_back(k); }
+                else (comps[k]->anchored_start ? ord_a : ord_u).push_back(k);
+            }
+            std::vector<std::vector<uint32_t>> gm_a, gm_u, gm_r;
+            std::vector<MultiDfa> gd_a, gd_u, gd_r;
             std::vector<uint32_t> single;
             form_groups(comps, ord_a, [](uint32_t, uint32_t) { return true; }, gm_a, gd_a, single);
             form_groups(comps, ord_u, [](uint32_t, uint32_t) { return true; }, gm_u, gd_u, single);
+            form_groups(rcomps, ord_r, [](uint32_t, uint32_t) { return true; }, gm_r, gd_r, single);
             if (!single.empty()) { h.n_rk_prefilter++; st.n_rk_prefilter++; continue; }
             std::vector<std::vector<uint32_t>> gmem;
             std::vector<MultiDfa> gdfa;
@@ -1853,6 +1871,12 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             }
             D.rsl_first = (uint32_t)alw_slices.size();
             const uint32_t fr = D.first_rloc;
+            if (!gm_r.empty()) {
+                pack_slices(gm_r, gd_r, [&](size_t j, size_t k) { return fr + gm_r[j][k]; },
+                            [](size_t, size_t) { return 1u; }, (uint32_t)Sv.id);
+                for (size_t k = D.rsl_first; k < alw_slices.size(); k++) alw_slices[k].flags |= ALW_SLICE_REVERSED;
+                st.n_rsl_reversed += (uint32_t)(alw_slices.size() - D.rsl_first);
+            }
             pack_slices(gmem, gdfa, [&](size_t j, size_t k) { return fr + gmem[j][k]; },
                         [](size_t, size_t) { return 1u; }, (uint32_t)Sv.id);
             D.rsl_n = (uint32_t)alw_slices.size() - D.rsl_first;

@@ -577,10 +577,65 @@ FI factors(const std::vector<Node> &N, int n) {
     return r;
 }
 
+// ---------------------------------------------------------------- DFA construction
+// Reversal of a pattern X$ (no '^', its only '$' the last item of the top-level sequence): the
+// regex ^(\n)?rev(X) over the reversed subject.  X$ matches s (PCRE search: X ends at the end of
+// s, or right before a final '\n') iff rev(X) matches a prefix of rev(s), or of rev(s) after its
+// leading '\n' -- an anchored search that dies within a few bytes of most subjects.
+int reverse_node(std::vector<Node> &N, int n) {
+    Node x = N[n];
+    if (x.k == Node::CAT) {
+        std::vector<int> kids;
+        for (auto it = x.kids.rbegin(); it != x.kids.rend(); ++it) kids.push_back(reverse_node(N, *it));
+        x.kids = kids;
+    } else if (x.k == Node::ALT || x.k == Node::REP) {
+        for (int &k : x.kids) k = reverse_node(N, k);
+    }
+    N.push_back(x);
+    return (int)N.size() - 1;
+}
+bool has_anchor(const std::vector<Node> &N, int n) {
+    const Node &x = N[n];
+    if (x.k == Node::BOL || x.k == Node::EOL) return true;
+    for (int k : x.kids) if (has_anchor(N, k)) return true;
+    return false;
+}
+int reverse_tail_anchored(std::vector<Node> &N, int root) {
+    const Node r = N[root];
+    if (r.k != Node::CAT || r.kids.empty() || N[r.kids.back()].k != Node::EOL) return -1;
+    for (size_t q = 0; q + 1 < r.kids.size(); q++) if (has_anchor(N, r.kids[q])) return -1;
+    Node body; body.k = Node::CAT;
+    for (size_t q = 0; q + 1 < r.kids.size(); q++) body.kids.push_back(r.kids[q]);
+    N.push_back(body);
+    const int rb = reverse_node(N, (int)N.size() - 1);
+    Node bol; bol.k = Node::BOL;
+    N.push_back(bol);
+    const int nb = (int)N.size() - 1;
+    Node nl; nl.k = Node::SET; nl.set['\n'] = true;
+    N.push_back(nl);
+    Node opt; opt.k = Node::REP; opt.kids = {(int)N.size() - 1}; opt.mn = 0; opt.mx = 1;
+    N.push_back(opt);
+    const int no = (int)N.size() - 1;
+    Node cat; cat.k = Node::CAT; cat.kids = {nb, no, rb};
+    N.push_back(cat);
+    return (int)N.size() - 1;
+}
+
+RegexInfo compile_impl(const std::string &pattern, bool caseless, int max_states, bool reversed);
 }  // namespace
 
-// ---------------------------------------------------------------- DFA construction
 RegexInfo compile_regex(const std::string &pattern, bool caseless, int max_states) {
+    return compile_impl(pattern, caseless, max_states, false);
+}
+bool compile_regex_reversed(const std::string &pattern, bool caseless, int max_states, Dfa &out) {
+    RegexInfo r = compile_impl(pattern, caseless, max_states, true);
+    if (r.status != RX_OK) return false;
+    out = std::move(r.dfa);
+    return true;
+}
+
+namespace {
+RegexInfo compile_impl(const std::string &pattern, bool caseless, int max_states, bool reversed) {
     RegexInfo out;
     Parser P(pattern);
     P.icase = caseless;
@@ -591,6 +646,10 @@ RegexInfo compile_regex(const std::string &pattern, bool caseless, int max_state
         return out;
     }
     if (!check_anchors(P.nodes, root, true, true)) { out.status = RX_UNSUPPORTED; out.error = "anchor position"; return out; }
+    if (reversed) {
+        root = reverse_tail_anchored(P.nodes, root);
+        if (root < 0) { out.status = RX_UNSUPPORTED; out.error = "not X$"; return out; }
+    }
 
     NfaBuilder B(P.nodes);
     auto f = B.build(root);
@@ -710,6 +769,7 @@ RegexInfo compile_regex(const std::string &pattern, bool caseless, int max_state
         return true;
     };
     if (!build(true, out.dfa)) { out.status = RX_TOO_BIG; out.error = "dfa too big"; return out; }
+    if (reversed) { out.status = RX_OK; return out; }
 
     FI fi = factors(P.nodes, root);
     std::vector<std::string> best = fi.best;
@@ -731,6 +791,7 @@ RegexInfo compile_regex(const std::string &pattern, bool caseless, int max_state
     out.status = RX_OK;
     return out;
 }
+}  // namespace
 
 bool dfa_search(const Dfa &d, const uint8_t *s, size_t n) {
     int st = 1;
@@ -894,6 +955,13 @@ extern "C" int gm_debug_regex(const char *pat, int caseless, const uint8_t *subj
     return gm::dfa_search(ri.dfa, subj, n) ? 1 : 0;
 }
 
+extern "C" int gm_debug_regex_rev(const char *pat, int caseless, const uint8_t *subj, size_t n) {
+    gm::Dfa d;
+    if (!gm::compile_regex_reversed(pat, caseless != 0, 4096, d)) return -1;
+    std::vector<uint8_t> r(subj, subj + n);
+    std::reverse(r.begin(), r.end());
+    return gm::dfa_search(d, r.data(), r.size()) ? 1 : 0;
+}
 extern "C" int gm_debug_regex_factors(const char *pat, int caseless, char *out, size_t cap) {
     gm::RegexInfo ri = gm::compile_regex(pat, caseless != 0);
     if (ri.status != gm::RX_OK) return -(int)ri.status;

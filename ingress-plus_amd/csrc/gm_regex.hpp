@@ -44,6 +44,10 @@ struct RegexInfo {
 };
 
 RegexInfo compile_regex(const std::string &pattern, bool caseless, int max_states = 8192);
+// X$ (no '^'; its only '$' ends the top-level sequence): the DFA of ^(\n)?rev(X), which run over
+// the subject's bytes from the last one backwards answers "X$ matches" (PCRE search semantics) and
+// dies within a few bytes of most subjects.  false: not of that form, or too big.
+bool compile_regex_reversed(const std::string &pattern, bool caseless, int max_states, Dfa &out);
 
 // Union of search DFAs (compile_regex().dfa each): one pass over a subject answers "which of
 // them match".  A state is (every component's state, the components that matched on entering

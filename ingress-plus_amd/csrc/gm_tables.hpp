@@ -286,8 +286,9 @@ struct DAlwSlice {
     uint32_t zones;          // zones some group scans
     uint32_t server;         // regex-location slices: the server (GM_NONE: always-run regexes)
     uint32_t min_member;     // regex-location slices: the lowest regex-location index it holds
-    uint32_t pad;
+    uint32_t flags;          // ALW_SLICE_REVERSED: X$ regexes run backwards (compile_regex_reversed)
 };
+constexpr uint32_t ALW_SLICE_REVERSED = 1;
 
 struct TabHeader {
     uint32_t magic, version;

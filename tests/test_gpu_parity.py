@@ -318,13 +318,14 @@ def test_empty_and_generation_swap(eng):
 
 def test_c3_regex_locations_parity(eng):
     """C3: 1k regex locations, all in union-DFA slices (k_rloc_multi: the stats pin that path, no
-    server is left to the factor prefilter), URIs 32-256 B, 40 % crafted to hit; PCRE-only
-    locations reached in order give GM_ACT_UNSUPPORTED on both sides."""
+    server is left to the factor prefilter; the X$ ones in reversed slices that run from the URI's
+    end), URIs 32-256 B, 40 % crafted to hit; PCRE-only locations reached in order give
+    GM_ACT_UNSUPPORTED on both sides."""
     regs = workloads.c3_regexes()
     reqs, arena = workloads.gen_c3(50_000, regs)
     got, gh, exp, eh = run_both(eng, workloads.c3_blob(regs), reqs, arena)
     st = eng.stats()
-    assert st["n_rsl_slices"] > 0 and st["n_rk_prefilter"] == 0, st
+    assert st["n_rsl_slices"] > 0 and st["n_rk_prefilter"] == 0 and st["n_rsl_reversed"] > 0, st
     assert_verdicts_equal(got, exp, gh, eh, "c3")
     hit = np.isin(got["location_id"], np.arange(3, len(regs) + 3))
     assert 0.3 < hit.mean() < 0.99
@@ -430,3 +431,32 @@ def test_regex_locations_factor_prefilter_fallback(eng):
     assert st["n_rk_prefilter"] == 1 and st["n_rsl_slices"] == 0, st
     assert_verdicts_equal(got, exp, gh, eh, "regex locations, factor prefilter")
     assert len(np.unique(got["status"])) >= 8
+
+
+def test_regex_locations_reversed_slices(eng):
+    """X$ regex locations in reversed union-DFA slices (^(\\n)?rev(X) run from the URI's last byte
+    backwards) beside forward anchored / unanchored ones, in config order: URIs ending in '\\n'
+    ('$' before a final newline), empty URIs, matches of several patterns (the first in config
+    order wins) -- every verdict equals the oracle's."""
+    pats = [("~", r"\.php$"), ("~", "^/a/[0-9]+"), ("~*", r"/(img|css)/[a-z0-9]+\.(png|jpg)$"), ("~", "/b/c"),
+            ("~", "x[0-9]{2,4}$"), ("~", "^/q$"), ("~", "(foo|bar)+baz$"), ("~", r"/v[0-9]/"),
+            ("~", "[^/]+/z$"), ("~", "/a/1"), ("~*", "END$"), ("~", "a.b$")]
+    locs = "".join(f'    location {op} "{p}" {{ return 2{i:02d}; }}\n' for i, (op, p) in enumerate(pats))
+    conf = ("http {\n  server {\n    listen 80 default_server;\n    server_name r.example.com;\n"
+            "    location / { return 404; }\n" + locs + "  }\n}\n")
+    b = blob.make_blob(conf, {})
+    rng = np.random.default_rng(23)
+    parts = ["/a", "/b", "/c", "/img", "/css", "/q", "/v1", "/v22", "/foo", "/bar", "/z", "/x12", "/x1234",
+             "/1", "/42", "baz", ".php", ".PNG", ".jpg", "END", "end", "a.b", "a_b", "foobarbaz"]
+    uris = ["", "\n", "/q", "/q\n", "/q\n\n", "/x.php\n", "/a/1", "/end\n", "/a.b", "/a.b\n"]
+    for _ in range(30_000):
+        u = "".join(parts[int(k)] for k in rng.integers(0, len(parts), int(rng.integers(1, 7))))
+        if rng.random() < 0.1:
+            u += "\n"
+        uris.append(u)
+    reqs, arena = records.from_dicts([{"host": "r.example.com", "uri": u} for u in uris])
+    got, gh, exp, eh = run_both(eng, b, reqs, arena)
+    st = eng.stats()
+    assert st["n_rsl_reversed"] > 0 and st["n_rk_prefilter"] == 0, st
+    assert_verdicts_equal(got, exp, gh, eh, "reversed regex-location slices")
+    assert len(np.unique(got["status"])) >= 10

@@ -97,6 +97,36 @@ def test_regex_dfa_matches_pcre_on_random_subjects():
             assert got == pcre_match(pat, s, ci), (pat, ci, s)
 
 
+def test_reversed_regex_matches_pcre():
+    """X$ regex locations run backwards from the URI's end as ^(\\n)?rev(X) (gm_regex.hpp
+    compile_regex_reversed): same answer as PCRE's forward search, the final-newline rule of '$'
+    included; forms other than X$ are refused."""
+    import random
+    L = ctypes.CDLL(engine.LIB_PATH)
+    L.gm_debug_regex_rev.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
+    extra = [("abc$", False), ("(a|bc)d*$", False), ("x[0-9]{2,3}$", True), ("a?$", False),
+             (r"\.(php|html?)$", True), ("(foo|bar)+baz$", False), ("a.b$", False), ("[^/]+$", False)]
+    for pat in ("^/a$", "abc", "a$|b", "(a$)b", "$"):
+        assert L.gm_debug_regex_rev(pat.encode(), 0, b"x", 1) == -1, pat
+    regs = workloads.c3_regexes()
+    cases = extra + [(r[0], r[1]) for r in regs if not r[2] and not r[4] and r[5]]
+    rng = random.Random(5)
+    seeds = [b"", b"\n", b"abc\n", b"xabc", b"a\nb", b"ab\n\n", b"x12\n", b"foobaz", b"/v1/x.PHP", b"a.b\n"]
+    n_hit = 0
+    for pat, ci in cases:
+        own = [r for r in regs if r[0] == pat]
+        subjects = list(seeds) + [workloads.c3_uri(rng, regs, True).encode() for _ in range(12)]
+        subjects += [workloads.c3_uri(rng, own, True).encode() for _ in range(6)] if own else []
+        subjects += [x + b"\n" for x in subjects[-3:]]
+        for s in subjects:
+            got = L.gm_debug_regex_rev(pat.encode(), 1 if ci else 0, s, len(s))
+            assert got >= 0, pat
+            exp = pcre_match(pat, s, ci)
+            assert got == exp, (pat, ci, s)
+            n_hit += exp
+    assert len(cases) > 100 and n_hit > 300
+
+
 def test_regex_factors():
     L = ctypes.CDLL(engine.LIB_PATH)
     L.gm_debug_regex_factors.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
