@@ -192,8 +192,9 @@ typedef struct gm_stats_t {
     /* servers whose regex locations stay behind the factor prefilter (a regex no union group
      * can hold): k_rloc answers them */
     uint32_t n_rk_prefilter;
-    /* of n_rsl_slices: slices of X$ regex locations run backwards from the URI's end */
-    uint32_t n_rsl_reversed;
+    /* of n_rsl_slices: slices of X$ regex locations run backwards from the URI's end, and forward
+     * slices run only for requests whose $uri holds one of their regexes' factors */
+    uint32_t n_rsl_reversed, n_rsl_pref;
 } gm_stats_t;
 
 /* Request parsers (Wallarm's) a signature set can declare ("@decoders" line of

@@ -1331,6 +1331,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     std::vector<DServerIf> sifs;
     std::vector<DRegexLoc> rlocs;
     std::vector<std::vector<std::string>> rloc_factors;   // parallel to rlocs: >= 4-byte factors
+    std::vector<uint8_t> rsl_pbit;   // parallel to rlocs (filled below): k_rloc_pref's mask bit, 0xFF none
     // parallel to rlocs: the DFA of ^(\n)?rev(X) for an unanchored X$ (n_states 0: none) --
     // union-DFA slices of these run backwards from the URI's end (gm_regex.hpp
     // compile_regex_reversed) and die within a few bytes, where the forward search reads it all
@@ -1818,6 +1819,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     // superset DFA, one without any DFA matches at once (a DFA whose start state accepts).  A
     // server with a regex no group can hold keeps the factor prefilter.
     {
+        rsl_pbit.assign(rlocs.size(), 0xFF);
         Dfa match_all;
         match_all.n_states = 2; match_all.n_classes = 1;
         match_all.trans.assign(2, 0); match_all.trans[1] = 1;
@@ -1848,41 +1850,65 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             // X$ regexes with a reversed DFA form groups of their own (run backwards: slices
             // flagged ALW_SLICE_REVERSED, packed first -- they are cheap, and the matches they
             // find let later slices skip requests)
-            std::vector<uint32_t> ord_a, ord_u, ord_r;
+            // The slices, in this order: reversed (X$), anchored, unanchored without a factor,
+            // unanchored with factors (prefiltered, below) -- cheap slices first, so that the
+            // matches they find let the costly ones skip requests; within a kind, config order
+            std::vector<uint32_t> ord_a, ord_un, ord_uf, ord_r;
             std::vector<const Dfa *> rcomps(D.n_rloc, nullptr);
             for (uint32_t k = 0; k < D.n_rloc; k++) {
                 const Dfa &rv = rloc_rev[D.first_rloc + k];
                 if (rv.n_states > 0) { rcomps[k] = &rv; ord_r.push_back(k); }
-                else (comps[k]->anchored_start ? ord_a : ord_u).push_back(k);
+                else if (comps[k]->anchored_start) ord_a.push_back(k);
+                else if (rlocs[D.first_rloc + k].dfa != GM_NONE && !rloc_factors[D.first_rloc + k].empty())
+                    ord_uf.push_back(k);
+                else ord_un.push_back(k);
             }
-            std::vector<std::vector<uint32_t>> gm_a, gm_u, gm_r;
-            std::vector<MultiDfa> gd_a, gd_u, gd_r;
+            std::vector<std::vector<uint32_t>> gm_a, gm_un, gm_uf, gm_r;
+            std::vector<MultiDfa> gd_a, gd_un, gd_uf, gd_r;
             std::vector<uint32_t> single;
-            form_groups(comps, ord_a, [](uint32_t, uint32_t) { return true; }, gm_a, gd_a, single);
-            form_groups(comps, ord_u, [](uint32_t, uint32_t) { return true; }, gm_u, gd_u, single);
-            form_groups(rcomps, ord_r, [](uint32_t, uint32_t) { return true; }, gm_r, gd_r, single);
+            auto all = [](uint32_t, uint32_t) { return true; };
+            form_groups(comps, ord_a, all, gm_a, gd_a, single);
+            form_groups(comps, ord_un, all, gm_un, gd_un, single);
+            form_groups(comps, ord_uf, all, gm_uf, gd_uf, single);
+            form_groups(rcomps, ord_r, all, gm_r, gd_r, single);
             if (!single.empty()) { h.n_rk_prefilter++; st.n_rk_prefilter++; continue; }
-            std::vector<std::vector<uint32_t>> gmem;
-            std::vector<MultiDfa> gdfa;
-            for (size_t ia = 0, iu = 0; ia < gm_a.size() || iu < gm_u.size();) {
-                const bool take_a = iu == gm_u.size() || (ia < gm_a.size() && gm_a[ia][0] < gm_u[iu][0]);
-                if (take_a) { gmem.push_back(gm_a[ia]); gdfa.push_back(std::move(gd_a[ia])); ia++; }
-                else { gmem.push_back(gm_u[iu]); gdfa.push_back(std::move(gd_u[iu])); iu++; }
-            }
             D.rsl_first = (uint32_t)alw_slices.size();
             const uint32_t fr = D.first_rloc;
-            if (!gm_r.empty()) {
-                pack_slices(gm_r, gd_r, [&](size_t j, size_t k) { return fr + gm_r[j][k]; },
-                            [](size_t, size_t) { return 1u; }, (uint32_t)Sv.id);
-                for (size_t k = D.rsl_first; k < alw_slices.size(); k++) alw_slices[k].flags |= ALW_SLICE_REVERSED;
-                st.n_rsl_reversed += (uint32_t)(alw_slices.size() - D.rsl_first);
-            }
-            pack_slices(gmem, gdfa, [&](size_t j, size_t k) { return fr + gmem[j][k]; },
-                        [](size_t, size_t) { return 1u; }, (uint32_t)Sv.id);
+            auto pack_kind = [&](std::vector<std::vector<uint32_t>> &gmk, std::vector<MultiDfa> &gdk, uint32_t flags) {
+                const size_t s0 = alw_slices.size();
+                if (!gmk.empty())
+                    pack_slices(gmk, gdk, [&](size_t j, size_t k) { return fr + gmk[j][k]; },
+                                [](size_t, size_t) { return 1u; }, (uint32_t)Sv.id);
+                for (size_t k = s0; k < alw_slices.size(); k++) alw_slices[k].flags |= flags;
+                return (uint32_t)(alw_slices.size() - s0);
+            };
+            st.n_rsl_reversed += pack_kind(gm_r, gd_r, ALW_SLICE_REVERSED);
+            pack_kind(gm_a, gd_a, 0);
+            pack_kind(gm_un, gd_un, 0);
+            pack_kind(gm_uf, gd_uf, 0);
             D.rsl_n = (uint32_t)alw_slices.size() - D.rsl_first;
             for (uint32_t k = D.rsl_first; k < D.rsl_first + D.rsl_n; k++)
                 alw_slices[k].min_member = alw_rule[alw[alw_slices[k].first_group].first];
             st.n_rsl_slices += D.rsl_n;
+            // forward slices of unanchored regexes that all have >= 4-byte factors run only for
+            // the requests whose $uri holds a factor of one of them: k_rloc_pref sets bit
+            // (slice - rsl_first) & 63 of a request's mask per factor found (the rk tables above)
+            for (uint32_t s2 = D.rsl_first; s2 < D.rsl_first + D.rsl_n; s2++) {
+                DAlwSlice &sl = alw_slices[s2];
+                if (sl.flags & ALW_SLICE_REVERSED) continue;
+                std::vector<uint32_t> mem;
+                for (uint32_t g = sl.first_group; g < sl.first_group + sl.n_groups; g++)
+                    for (uint32_t k = 0; k < (uint32_t)__builtin_popcount(alw[g].zone_mask[0]); k++)
+                        mem.push_back(alw_rule[alw[g].first + k]);
+                bool pref = !mem.empty();
+                for (uint32_t m : mem)
+                    if (rlocs[m].dfa == GM_NONE || rloc_factors[m].empty() || comps[m - fr]->anchored_start) pref = false;
+                if (!pref) continue;
+                const uint32_t bit = (s2 - D.rsl_first) & 63u;
+                sl.flags |= ALW_SLICE_PREF | bit << 8;
+                for (uint32_t m : mem) rsl_pbit[m] = (uint8_t)bit;
+                st.n_rsl_pref++;
+            }
         }
     }
     h.n_always_lds = (uint32_t)always_grouped.size();
@@ -1914,6 +1940,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_always = I.put(always);
     h.off_alw = I.put(alw); h.off_alw_slices = I.put(alw_slices); h.off_alw_pack = I.put(alw_pack);
     h.off_alw_rule = I.put(alw_rule);
+    rsl_pbit.resize((rsl_pbit.size() + 3) & ~size_t(3), 0xFF);
+    h.off_rsl_pbit = I.put(rsl_pbit);
     h.n_rk_cap = rkcap; h.n_rk_ids = (uint32_t)rk_ids.size(); h.n_rk_ents_keys = (uint32_t)rk_lists.size();
     h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_rk_ents = I.put(rk_ents); h.off_rk_bloom = I.put(rk_bloom);
     h.n_ups = (uint32_t)dups.size(); h.n_peers = (uint32_t)peer_init.size();
@@ -2073,6 +2101,7 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.alw_slices = (const DAlwSlice *)(b + h.off_alw_slices);
     t.alw_pack = b + h.off_alw_pack;
     t.alw_rule = (const uint32_t *)(b + h.off_alw_rule);
+    t.rsl_pbit = b + h.off_rsl_pbit;
     t.n_always_lds = h.n_always_lds; t.n_alw_groups = h.n_alw_groups; t.n_alw_slices = h.n_alw_slices;
     t.n_rsl = h.n_rsl; t.n_rk_prefilter = h.n_rk_prefilter;
     t.n_ports = h.n_ports;

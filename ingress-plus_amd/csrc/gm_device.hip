@@ -768,7 +768,7 @@ constexpr uint32_t RLOC_STATUS_WORD = 16;   // batch status word: requests defer
 // (URI <= RLOC_URI_CAP, n_rloc <= RLOC_BM_BITS) sets *pend and returns; >= -1 -- k_rloc's answer
 // (the location index, -1 none).  *sid_out: the server chosen (valid whenever *pend is set).
 constexpr int32_t RK_INLINE = -3, RK_DEFER = -2;
-__device__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
+__device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
                           RouteOut &o);
 __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const RoutePre &pre,
                           const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb, int32_t rk_in = RK_INLINE,
@@ -903,7 +903,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
 // The rest of route_one once the location is known (loc < 0: none): location kinds, rules and
 // split routes, return / proxy.  The regex-location tail pass starts here with k_rloc's answer
 // (or the request's longest prefix match) instead of routing the request again.
-__device__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
+__device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
                           RouteOut &o) {
     if (loc < 0) { o.action = GM_ACT_NOT_FOUND; o.status = 404; return; }
     o.loc = (uint32_t)loc;
@@ -1178,13 +1178,14 @@ struct Scratch {
     int32_t *d_rql = nullptr; size_t cap_rql = 0;        // and k_rloc's locations
     uint4 *d_rqs = nullptr; size_t cap_rqs = 0;          // and each one's $uri span + server (k_rloc_multi)
     int32_t *d_rqb = nullptr; size_t cap_rqb = 0;        // and its longest prefix match (the tail pass)
+    unsigned long long *d_rqm = nullptr; size_t cap_rqm = 0;   // and its prefiltered-slice mask
     ~Scratch() {
         for (void *p : {(void *)d_status, (void *)d_blk2rec, (void *)d_cand, (void *)d_surv, (void *)d_pairs,
                         (void *)d_jobs, (void *)d_set, (void *)d_cnt, (void *)d_start, (void *)d_ccnt,
                         (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp, (void *)d_wscr, (void *)d_wsum,
                         (void *)d_pk, (void *)d_pseg, (void *)d_pprog, (void *)d_ppat, (void *)d_ptemp,
                         (void *)d_usize, (void *)d_utemp, (void *)d_sreqs, (void *)d_sarena, (void *)d_sblk,
-                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb})
+                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
         for (auto &e : ev) if (e) (void)hipEventDestroy(e);
@@ -1517,7 +1518,8 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     if (rk) {
         int e2;
         if ((e2 = grow(c, s, S->d_rq, S->cap_rq, n)) || (e2 = grow(c, s, S->d_rql, S->cap_rql, n)) ||
-            (e2 = grow(c, s, S->d_rqs, S->cap_rqs, n)) || (e2 = grow(c, s, S->d_rqb, S->cap_rqb, n))) return e2;
+            (e2 = grow(c, s, S->d_rqs, S->cap_rqs, n)) || (e2 = grow(c, s, S->d_rqb, S->cap_rqb, n)) ||
+            (e2 = grow(c, s, S->d_rqm, S->cap_rqm, n))) return e2;
         q = RlocQ{S->d_rq, S->d_status + RLOC_STATUS_WORD, S->d_rql, S->d_rqs, S->d_rqb};
     }
     auto launch_rloc = [&](hipStream_t rs, uint32_t tail_blocks) -> int {
@@ -1525,14 +1527,21 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         // slice skips the later ones), then the factor prefilter for the others
         if (t.n_rsl) {
             HIPCHK(c, hipMemsetAsync(q.loc, 0xFF, (size_t)n * 4, rs));
+            // the factor masks of the prefiltered slices' requests (gm_rloc.inc k_rloc_pref)
+            const unsigned long long *pm = nullptr;
+            if (g->stats.n_rsl_pref) {
+                k_rloc_pref<<<(uint32_t)c->cu_count * 8, 256, 0, rs>>>(A, alen, t, q.st, q.count, S->d_rqm, dlen);
+                HIPCHK(c, hipGetLastError());
+                pm = S->d_rqm;
+            }
             const DAlwSlice *sls = reinterpret_cast<const DAlwSlice *>(g->host_image.data() + g->hdr.off_alw_slices);
             for (uint32_t k = t.n_alw_slices; k < t.n_alw_slices + t.n_rsl; k++) {
                 const dim3 grid((uint32_t)c->cu_count), blk(1024);
                 switch (sls[k].n_groups) {
-                case 1: k_rloc_multi<1><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k); break;
-                case 2: k_rloc_multi<2><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k); break;
-                case 3: k_rloc_multi<3><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k); break;
-                default: k_rloc_multi<4><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k); break;
+                case 1: k_rloc_multi<1><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k, pm); break;
+                case 2: k_rloc_multi<2><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k, pm); break;
+                case 3: k_rloc_multi<3><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k, pm); break;
+                default: k_rloc_multi<4><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k, pm); break;
                 }
                 HIPCHK(c, hipGetLastError());
             }

@@ -289,6 +289,9 @@ struct DAlwSlice {
     uint32_t flags;          // ALW_SLICE_REVERSED: X$ regexes run backwards (compile_regex_reversed)
 };
 constexpr uint32_t ALW_SLICE_REVERSED = 1;
+// a forward slice of unanchored regexes that all have factors: it runs only for requests whose
+// k_rloc_pref mask has bit (flags >> 8) & 63
+constexpr uint32_t ALW_SLICE_PREF = 2;
 
 struct TabHeader {
     uint32_t magic, version;
@@ -322,6 +325,7 @@ struct TabHeader {
                                                                  // after the n_alw_slices
     uint32_t n_rk_prefilter, pad_rkp;   // rk_on servers left to the factor prefilter (rsl_n 0)
     uint64_t off_alw, off_alw_slices, off_alw_pack, off_alw_rule;
+    uint64_t off_rsl_pbit;         // u8 per regex location: its prefiltered slice's mask bit (0xFF none)
 };
 // The route's hot tables -- ports, the three name tables, servers, server ifs, small-location
 // lists, locations and the name strings -- are laid out first and contiguously in the image;
@@ -347,6 +351,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const DLocUri *loc_uri;
     uint32_t decoders;
     const DAlwGroup *alw; const DAlwSlice *alw_slices; const uint8_t *alw_pack; const uint32_t *alw_rule;
+    const uint8_t *rsl_pbit;
     uint32_t n_always_lds, n_alw_groups, n_alw_slices, n_rsl, n_rk_prefilter;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;

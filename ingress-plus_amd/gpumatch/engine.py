@@ -35,7 +35,7 @@ STATS_FIELDS64 = ["table_bytes", "lds_bytes_scan", "last_candidates", "last_pair
 STATS_FIELDS_MS = ["last_ms_route", "last_ms_scan", "last_ms_verify", "last_ms_tail"]
 STATS_FIELDS_WAF = ["n_waf_keys", "bloom_pk", "bloom_fp_ppm", "last_ctx_pass", "last_jobs", "n_peers",
                     "n_upstreams_deferred", "decoders", "n_alw_groups", "n_alw_states", "n_alw_slices",
-                    "n_alw_single", "n_rsl_slices", "n_rk_prefilter", "n_rsl_reversed"]
+                    "n_alw_single", "n_rsl_slices", "n_rk_prefilter", "n_rsl_reversed", "n_rsl_pref"]
 GM_CREATE_PROFILE = 0x2
 GM_CREATE_SERIAL = 0x4
 
