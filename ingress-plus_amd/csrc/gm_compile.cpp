@@ -1741,7 +1741,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                            auto val, auto zones, uint32_t server) {
         auto pad16 = [&]() { alw_pack.resize((alw_pack.size() + 15) & ~size_t(15), 0); };
         for (size_t g0 = 0; g0 < gmem.size();) {
-            size_t g1 = g0, bytes = 1024;
+            size_t g1 = g0, bytes = 2048;
             while (g1 < gmem.size() && g1 - g0 < ALW_SLICE_GROUPS && bytes + tab_bytes(gdfa[g1]) + 16 <= ALWAYS_LDS_BYTES)
                 bytes += tab_bytes(gdfa[g1++]) + 16;
             DAlwSlice sl{};
@@ -1749,11 +1749,13 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             sl.first_group = (uint32_t)alw.size();
             sl.n_groups = (uint32_t)(g1 - g0);
             sl.server = server;
-            std::vector<uint32_t> clsq(256, 0);
+            // clsq[b]: byte b's class in groups 0..3 (a byte each); clsq[256 + b]: groups 4..7
+            std::vector<uint32_t> clsq(512, 0);
             for (size_t j = g0; j < g1; j++)
-                for (int b = 0; b < 256; b++) clsq[b] |= (uint32_t)gdfa[j].cls[b] << (8 * (j - g0));
+                for (int b = 0; b < 256; b++)
+                    clsq[((j - g0) >= 4 ? 256 : 0) + b] |= (uint32_t)gdfa[j].cls[b] << (8 * ((j - g0) & 3));
             const uint8_t *cb = reinterpret_cast<const uint8_t *>(clsq.data());
-            alw_pack.insert(alw_pack.end(), cb, cb + 1024);
+            alw_pack.insert(alw_pack.end(), cb, cb + 2048);
             for (size_t j = g0; j < g1; j++) {
                 const MultiDfa &m = gdfa[j];
                 const size_t S = (size_t)m.n_states, Cn = (size_t)m.n_classes, Cp = Cn + (Cn & 1), R = Cp + 4;
@@ -1944,6 +1946,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_rsl_pbit = I.put(rsl_pbit);
     h.n_rk_cap = rkcap; h.n_rk_ids = (uint32_t)rk_ids.size(); h.n_rk_ents_keys = (uint32_t)rk_lists.size();
     h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_rk_ents = I.put(rk_ents); h.off_rk_bloom = I.put(rk_bloom);
+    h.n_rk_ents_n = (uint32_t)rk_ents.size();
     h.n_ups = (uint32_t)dups.size(); h.n_peers = (uint32_t)peer_init.size();
     h.n_key_parts = (uint32_t)key_parts.size(); h.n_points = (uint32_t)points.size();
     h.off_ups = I.put(dups); h.off_key_parts = I.put(key_parts); h.off_points = I.put(points);

@@ -958,7 +958,9 @@ inline uint32_t route_lds(const GTab &t, bool beside) { return route_hot16(t) + 
 // slice, and only for requests the slice can still answer)
 // best: the deferred request's longest prefix match (-1 none), where the tail pass starts when no
 // regex location matched
-struct RlocQ { uint2 *list; uint32_t *count; int32_t *loc; uint4 *st; int32_t *best; };
+// u: its $uri's first 32 bytes (two uint4; the slices' first two 16-byte steps read them instead
+// of an arena line each)
+struct RlocQ { uint2 *list; uint32_t *count; int32_t *loc; uint4 *st; int32_t *best; uint4 *u; };
 template <int WPE, bool RK = false, bool TAIL = false>
 __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_route(const gm_req *__restrict__ reqs, uint32_t n,
                                                        const uint8_t *__restrict__ A, uint64_t arena_len,
@@ -1007,6 +1009,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
         RouteOut o;
         bool pend = false;
         Rec r{};
+        RoutePre pre;
         if (TAIL) {
             // a deferred request: its location is k_rloc's answer, else its longest prefix match
             // (saved by the first pass); only the location's own step runs again
@@ -1019,7 +1022,6 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
             route_loc(A, reqs + i, t, h, loc, o);
         } else {
             r = load_rec(reqs + i);
-            RoutePre pre;
 #ifdef GM_EXP_ROUTE_NOHOST   // measurement build: no host / URI loads (timing only)
             for (int k = 0; k < 8; k++) { pre.hw[k] = 0x2E2E2E2Eu + k; pre.uw[k] = 0x2F2F2F2Fu + k; }
 #else
@@ -1041,6 +1043,8 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
                     q.list[slot] = make_uint2(i, o.server);
                     q.st[slot] = make_uint4((uint32_t)r.base, (uint32_t)(r.base >> 32), r.uri_len, o.server);
                     q.best[slot] = o.pend_best;
+                    q.u[2 * slot] = make_uint4(pre.uw[0], pre.uw[1], pre.uw[2], pre.uw[3]);
+                    q.u[2 * slot + 1] = make_uint4(pre.uw[4], pre.uw[5], pre.uw[6], pre.uw[7]);
                 }
             }
         }
@@ -1052,22 +1056,24 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
         w1.w = o.status;
         uint4 *dst = reinterpret_cast<uint4 *>(out + i);
         if (!pend) { dst[0] = w0; dst[1] = w1; }
-        // per-location counter: the wave's first location in one atomic for all its lanes (the
-        // common case: most of a wave's requests share a location), every other lane its own
-        // (a loop over the distinct locations ran ~50 rounds per wave on C3)
+        // per-location counter: the wave's first few distinct locations in one atomic each for all
+        // their lanes (most waves: one to three locations), any lane left after four rounds its
+        // own atomic (C3's ~50 distinct locations per wave took a round each)
         {
-            const bool has = o.loc != GM_NONE;
-            const unsigned long long act = __ballot(has);
-            if (act) {
-                const int leader = __ffsll(act) - 1;
+            unsigned long long todo = __ballot(o.loc != GM_NONE);
+            for (int round = 0; todo && round < 4; round++) {
+                const int leader = __ffsll(todo) - 1;
                 const uint32_t lk = __shfl(o.loc, leader);
-                const unsigned long long same = __ballot(has && o.loc == lk);
-                const bool lead = (threadIdx.x & 63) == (uint32_t)leader, own = has && o.loc != lk;
-                if (lead || own) {
-                    const uint32_t ck = lead ? lk : o.loc, cv = lead ? (uint32_t)__popcll(same) : 1u;
-                    if (use_hist) atomicAdd(&hist[ck], cv);
-                    else atomicAdd(&counters[ck], (unsigned long long)cv);
+                const unsigned long long same = __ballot(o.loc == lk) & todo;
+                if ((threadIdx.x & 63) == (uint32_t)leader) {
+                    if (use_hist) atomicAdd(&hist[lk], (uint32_t)__popcll(same));
+                    else atomicAdd(&counters[lk], (unsigned long long)__popcll(same));
                 }
+                todo &= ~same;
+            }
+            if ((todo >> (threadIdx.x & 63)) & 1ull) {
+                if (use_hist) atomicAdd(&hist[o.loc], 1u);
+                else atomicAdd(&counters[o.loc], 1ull);
             }
         }
         if (TAIL) continue;
@@ -1080,9 +1086,13 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
 #else
         if (blk2rec) {
 #endif
-            // blocks whose start lies in [base_i, base_{i+1}) belong to record i
+            // blocks whose start lies in [base_i, base_{i+1}) belong to record i (base_{i+1}: the
+            // next lane's record, which it holds; lane 63 and the last request read it)
             uint64_t b0 = (i == 0) ? 0 : r.base;
-            uint64_t b1 = (i + 1 < n) ? reqs[i + 1].base : arena_len;
+            const uint32_t nb_lo = (uint32_t)__shfl_down((int)(uint32_t)r.base, 1);
+            const uint32_t nb_hi = (uint32_t)__shfl_down((int)(uint32_t)(r.base >> 32), 1);
+            const bool nxt_lane = (threadIdx.x & 63) != 63 && x + 1 < nn;
+            uint64_t b1 = (i + 1 < n) ? (nxt_lane ? ((uint64_t)nb_hi << 32 | nb_lo) : reqs[i + 1].base) : arena_len;
             uint64_t k0 = (b0 + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
             uint64_t k1 = (b1 + (1u << BLK_SHIFT) - 1) >> BLK_SHIFT;
             if (i + 1 == n) k1 = nblk;
@@ -1177,6 +1187,7 @@ struct Scratch {
     uint2 *d_rq = nullptr; size_t cap_rq = 0;            // regex-location requests deferred to k_rloc
     int32_t *d_rql = nullptr; size_t cap_rql = 0;        // and k_rloc's locations
     uint4 *d_rqs = nullptr; size_t cap_rqs = 0;          // and each one's $uri span + server (k_rloc_multi)
+    uint4 *d_rqu = nullptr; size_t cap_rqu = 0;          // and its $uri's first 32 bytes (+ a pad block)
     int32_t *d_rqb = nullptr; size_t cap_rqb = 0;        // and its longest prefix match (the tail pass)
     unsigned long long *d_rqm = nullptr; size_t cap_rqm = 0;   // and its prefiltered-slice mask
     ~Scratch() {
@@ -1185,7 +1196,7 @@ struct Scratch {
                         (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp, (void *)d_wscr, (void *)d_wsum,
                         (void *)d_pk, (void *)d_pseg, (void *)d_pprog, (void *)d_ppat, (void *)d_ptemp,
                         (void *)d_usize, (void *)d_utemp, (void *)d_sreqs, (void *)d_sarena, (void *)d_sblk,
-                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm})
+                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm, (void *)d_rqu})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
         for (auto &e : ev) if (e) (void)hipEventDestroy(e);
@@ -1326,12 +1337,20 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
             }
         const void *alws[] = {(const void *)k_waf_always_multi<1>, (const void *)k_waf_always_multi<2>,
                               (const void *)k_waf_always_multi<3>, (const void *)k_waf_always_multi<4>,
+                              (const void *)k_waf_always_multi<5>, (const void *)k_waf_always_multi<6>,
+                              (const void *)k_waf_always_multi<7>, (const void *)k_waf_always_multi<8>,
                               (const void *)k_rloc_multi<1>, (const void *)k_rloc_multi<2>,
-                              (const void *)k_rloc_multi<3>, (const void *)k_rloc_multi<4>};
+                              (const void *)k_rloc_multi<3>, (const void *)k_rloc_multi<4>,
+                              (const void *)k_rloc_multi<5>, (const void *)k_rloc_multi<6>,
+                              (const void *)k_rloc_multi<7>, (const void *)k_rloc_multi<8>};
         for (const void *f : alws)
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ALWAYS_LDS_BYTES) != hipSuccess) {
                 t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
             }
+        if (hipFuncSetAttribute((const void *)k_rloc_pref, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)RLOC_PREF_LDS) != hipSuccess) {
+            t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
+        }
         // the route's hot tables + location histogram (route_lds)
         const void *routes[] = {(const void *)k_route<3, true, true>, (const void *)k_route<3, true>,
                                 (const void *)k_route<3>, (const void *)k_route<5, true>, (const void *)k_route<5>};
@@ -1481,7 +1500,11 @@ static int launch_always(gm_ctx *c, hipStream_t s, const Generation *g, const ui
         case 1: k_waf_always_multi<1><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
         case 2: k_waf_always_multi<2><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
         case 3: k_waf_always_multi<3><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
-        default: k_waf_always_multi<4><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
+        case 4: k_waf_always_multi<4><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
+        case 5: k_waf_always_multi<5><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
+        case 6: k_waf_always_multi<6><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
+        case 7: k_waf_always_multi<7><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
+        default: k_waf_always_multi<8><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
         }
         HIPCHK(c, hipGetLastError());
     }
@@ -1519,8 +1542,8 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         int e2;
         if ((e2 = grow(c, s, S->d_rq, S->cap_rq, n)) || (e2 = grow(c, s, S->d_rql, S->cap_rql, n)) ||
             (e2 = grow(c, s, S->d_rqs, S->cap_rqs, n)) || (e2 = grow(c, s, S->d_rqb, S->cap_rqb, n)) ||
-            (e2 = grow(c, s, S->d_rqm, S->cap_rqm, n))) return e2;
-        q = RlocQ{S->d_rq, S->d_status + RLOC_STATUS_WORD, S->d_rql, S->d_rqs, S->d_rqb};
+            (e2 = grow(c, s, S->d_rqm, S->cap_rqm, n)) || (e2 = grow(c, s, S->d_rqu, S->cap_rqu, 2 * (size_t)n + 1))) return e2;
+        q = RlocQ{S->d_rq, S->d_status + RLOC_STATUS_WORD, S->d_rql, S->d_rqs, S->d_rqb, S->d_rqu};
     }
     auto launch_rloc = [&](hipStream_t rs, uint32_t tail_blocks) -> int {
         // union-DFA slices of the servers that have them (config order: a request answered by one
@@ -1529,8 +1552,11 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
             HIPCHK(c, hipMemsetAsync(q.loc, 0xFF, (size_t)n * 4, rs));
             // the factor masks of the prefiltered slices' requests (gm_rloc.inc k_rloc_pref)
             const unsigned long long *pm = nullptr;
-            if (g->stats.n_rsl_pref) {
-                k_rloc_pref<<<(uint32_t)c->cu_count * 8, 256, 0, rs>>>(A, alen, t, q.st, q.count, S->d_rqm, dlen);
+            const size_t pref_lds = 4u * RK_BLOOM_WORDS + sizeof(DRlocKey) * ((size_t)t.rk_mask + 1) +
+                                    sizeof(PrefEnt) * (size_t)g->hdr.n_rk_ents_n;
+            if (GM_RLOC_PREF && g->stats.n_rsl_pref && pref_lds <= RLOC_PREF_LDS) {
+                k_rloc_pref<<<(uint32_t)c->cu_count, 1024, pref_lds, rs>>>(A, alen, t, q.st, q.count, S->d_rqm,
+                                                                              dlen, g->hdr.n_rk_ents_n);
                 HIPCHK(c, hipGetLastError());
                 pm = S->d_rqm;
             }
@@ -1538,10 +1564,14 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
             for (uint32_t k = t.n_alw_slices; k < t.n_alw_slices + t.n_rsl; k++) {
                 const dim3 grid((uint32_t)c->cu_count), blk(1024);
                 switch (sls[k].n_groups) {
-                case 1: k_rloc_multi<1><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k, pm); break;
-                case 2: k_rloc_multi<2><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k, pm); break;
-                case 3: k_rloc_multi<3><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k, pm); break;
-                default: k_rloc_multi<4><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.count, q.loc, dlen, k, pm); break;
+                case 1: k_rloc_multi<1><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
+                case 2: k_rloc_multi<2><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
+                case 3: k_rloc_multi<3><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
+                case 4: k_rloc_multi<4><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
+                case 5: k_rloc_multi<5><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
+                case 6: k_rloc_multi<6><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
+                case 7: k_rloc_multi<7><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
+                default: k_rloc_multi<8><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
                 }
                 HIPCHK(c, hipGetLastError());
             }

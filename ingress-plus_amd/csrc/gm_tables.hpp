@@ -266,7 +266,7 @@ __host__ __device__ inline uint32_t peer_draw(uint64_t lo, uint64_t hi, uint32_t
 constexpr uint32_t ALWAYS_LDS_BYTES = 160 * 1024;
 constexpr uint32_t ALW_GROUP_BYTES = 64 * 1024 - 64;   // row byte offsets fit a u16 with the flag bit
 constexpr uint32_t ALW_GROUP_MAX = 32;
-constexpr uint32_t ALW_SLICE_GROUPS = 4;
+constexpr uint32_t ALW_SLICE_GROUPS = 8;
 constexpr uint32_t ALW_BUILD_STATES = 8192;   // product states before minimisation
 constexpr uint32_t ALW_EMIT = 1;
 constexpr uint32_t ALW_ROW_MASK = 0xFFFE;
@@ -326,6 +326,7 @@ struct TabHeader {
     uint32_t n_rk_prefilter, pad_rkp;   // rk_on servers left to the factor prefilter (rsl_n 0)
     uint64_t off_alw, off_alw_slices, off_alw_pack, off_alw_rule;
     uint64_t off_rsl_pbit;         // u8 per regex location: its prefiltered slice's mask bit (0xFF none)
+    uint32_t n_rk_ents_n, pad_rke; // DRlocEnt entries (k_rloc_pref stages them in LDS)
 };
 // The route's hot tables -- ports, the three name tables, servers, server ifs, small-location
 // lists, locations and the name strings -- are laid out first and contiguously in the image;
