@@ -1762,15 +1762,28 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 DAlwGroup g{};
                 g.tr_off = (uint32_t)(alw_pack.size() - sl.off);
                 g.mask_off = (uint32_t)(2 * Cp);
-                g.start_row = (uint32_t)(2 * R);
+                // states renumbered: the dead state 0, the others, then the emitting ones (an emit
+                // mask, or the target of a transition flagged MDFA_EMIT) from row emit_row on
+                std::vector<uint8_t> emits(S, 0);
+                for (size_t q = 1; q < S; q++) {
+                    if (m.emit[q]) emits[q] = 1;
+                    for (size_t c = 0; c < Cn; c++)
+                        if (m.trans[q * Cn + c] & MDFA_EMIT) emits[m.trans[q * Cn + c] & 0x3FFF] = 1;
+                }
+                emits[0] = 0;
+                std::vector<uint32_t> perm(S, 0);
+                uint32_t nid = 1;
+                for (size_t q = 1; q < S; q++) if (!emits[q]) perm[q] = nid++;
+                g.emit_row = (uint32_t)(2 * R * nid);
+                for (size_t q = 1; q < S; q++) if (emits[q]) perm[q] = nid++;
+                g.start_row = (uint32_t)(2 * R * perm[1]);
                 std::vector<uint16_t> rows(S * R, 0);
                 for (size_t q = 1; q < S; q++) {
-                    for (size_t c = 0; c < Cn; c++) {
-                        const uint16_t e = m.trans[q * Cn + c];
-                        rows[q * R + c] = (uint16_t)(2 * R * (e & 0x3FFF) | ((e & MDFA_EMIT) ? ALW_EMIT : 0));
-                    }
-                    rows[q * R + Cp] = (uint16_t)m.emit[q]; rows[q * R + Cp + 1] = (uint16_t)(m.emit[q] >> 16);
-                    rows[q * R + Cp + 2] = (uint16_t)m.endm[q]; rows[q * R + Cp + 3] = (uint16_t)(m.endm[q] >> 16);
+                    const size_t o = (size_t)perm[q] * R;
+                    for (size_t c = 0; c < Cn; c++)
+                        rows[o + c] = (uint16_t)(2 * R * perm[m.trans[q * Cn + c] & 0x3FFF]);
+                    rows[o + Cp] = (uint16_t)m.emit[q]; rows[o + Cp + 1] = (uint16_t)(m.emit[q] >> 16);
+                    rows[o + Cp + 2] = (uint16_t)m.endm[q]; rows[o + Cp + 3] = (uint16_t)(m.endm[q] >> 16);
                 }
                 const uint8_t *rb = reinterpret_cast<const uint8_t *>(rows.data());
                 alw_pack.insert(alw_pack.end(), rb, rb + rows.size() * 2);

@@ -261,15 +261,18 @@ __host__ __device__ inline uint32_t peer_draw(uint64_t lo, uint64_t hi, uint32_t
 // Slice pack (16-B aligned): clsq u32[256] (byte b's class in group j of the slice = byte j of
 // clsq[b]) | per group, its rows.  A row (state) is Cp + 4 u16: the transitions of the C classes
 // (Cp = C rounded up to even), then the state's emit mask and end mask (u32 each).  A transition
-// is the target row's byte offset in the group | ALW_EMIT (bit 0) when the target emits: the step
-// needs no multiply, and row 0 (the dead state) is all zeros.
+// is the target row's byte offset in the group: the step needs no multiply, and row 0 (the dead
+// state) is all zeros.  The emitting states are numbered last, from row emit_row on: a chain
+// entered one within a chunk iff the largest row it took there is >= emit_row (one max per step,
+// no flag bit to strip).
 constexpr uint32_t ALWAYS_LDS_BYTES = 160 * 1024;
 constexpr uint32_t ALW_GROUP_BYTES = 64 * 1024 - 64;   // row byte offsets fit a u16 with the flag bit
 constexpr uint32_t ALW_GROUP_MAX = 32;
-constexpr uint32_t ALW_SLICE_GROUPS = 8;
+#ifndef GM_ALW_SLICE_GROUPS
+#define GM_ALW_SLICE_GROUPS 8
+#endif
+constexpr uint32_t ALW_SLICE_GROUPS = GM_ALW_SLICE_GROUPS;
 constexpr uint32_t ALW_BUILD_STATES = 8192;   // product states before minimisation
-constexpr uint32_t ALW_EMIT = 1;
-constexpr uint32_t ALW_ROW_MASK = 0xFFFE;
 struct DAlwGroup {
     uint32_t tr_off;         // byte offset of row 0 from the slice start
     uint32_t mask_off;       // byte offset of the emit mask within a row (2 Cp); the end mask follows
@@ -278,7 +281,7 @@ struct DAlwGroup {
     uint32_t zone_mask[4];   // members (bit k) that scan zone z
     uint32_t first;          // member k's rule id: alw_rule[first + k]
     uint32_t zones;          // zones some member scans
-    uint32_t pad;
+    uint32_t emit_row;       // byte offset of the first emitting state's row (rows past it emit too)
 };
 struct DAlwSlice {
     uint32_t off, len;       // bytes of the pack
