@@ -2217,6 +2217,9 @@ extern "C" int gm_parse_requests(gm_ctx *c, const uint8_t *wire, const gm_wire_m
                                                    arena_len_dev, S->d_status + PARSE_STATUS_WORD, S->d_wscr,
                                                    wsum);
     HIPCHK(c, hipGetLastError());
+    k_wire_emit_full<<<blocks, 64 * WIRE_WAVES, 0, s>>>(wire, msgs, n, S->d_wsize, S->d_wbase, reqs, arena, arena_cap,
+                                                        S->d_wscr, wsum);
+    HIPCHK(c, hipGetLastError());
     return GM_OK;
 }
 
