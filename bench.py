@@ -29,6 +29,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def check_build(st, args):
+    """Refuse a library built with measurement or tuning macros (gm_stats.build_flags: GM_BUILD_EXPERIMENT,
+    GM_BUILD_TUNING) unless asked; such a build is an A/B variant, not the shipped pipeline."""
+    if st["build_flags"] and not args.allow_nondefault_build:
+        raise SystemExit(f"bench.py: the loaded libgpumatch.so is a non-default build (build_flags "
+                         f"{st['build_flags']:#x}); rebuild it with `make` or pass --allow-nondefault-build")
+    if st.get("scratch_scale", 1.0) != 1.0:
+        raise SystemExit(f"bench.py: scratch capacities are scaled ({st['scratch_scale']}): not the default context")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -49,6 +59,9 @@ def main():
                          "over the ranks with the hit counters all-reduced (--stream, --batch)")
     ap.add_argument("--stream", type=int, default=100_000_000, help="c5: requests in the whole stream")
     ap.add_argument("--batch", type=int, default=10_000_000, help="c5: requests per gm_match_batch")
+    ap.add_argument("--allow-nondefault-build", action="store_true",
+                    help="measure a library built with measurement / tuning macros (gm_stats build_flags != 0); "
+                         "the line is then marked \"build\": \"nondefault\" and is not a headline number")
     args = ap.parse_args()
     if args.config == "c5":
         return c5_main(args)
@@ -72,6 +85,7 @@ def main():
     eng = engine.Engine(local, profile=True, serial=args.serial)
     eng.load(gblob, 1)
     st = eng.stats()
+    check_build(st, args)
     log(f"[rank {rank}] generation: {st['n_sigs']} rules ({st['n_sig_literals']} lit, {st['n_sig_regex']} re), "
         f"table {st['table_bytes'] / 1e6:.1f} MB, compile+load {time.time() - t0:.1f}s")
 
@@ -177,6 +191,8 @@ def main():
                      "algorithmic_bytes_per_launch": zone_bytes},
     }
     result["roofline"].update(profiled(zone_bytes))
+    if st["build_flags"]:
+        result["build"] = f"nondefault (build_flags {st['build_flags']:#x})"
     if world == 1 and not args.serial and not args.no_alone:
         # the scan kernel alone (GM_CREATE_SERIAL: the route first, then the scan on its own), on
         # the same resident batch: its own roofline fraction beside the in-pipeline one above,
@@ -228,6 +244,7 @@ def c5_main(args):
     blob = workloads.c5_blob()
     eng = engine.Engine(local, profile=True)
     eng.load(blob, 1)
+    check_build(eng.stats(), args)
     preqs, parena = workloads.gen_c5(min(args.pool, 200_000))
     lo, hi = shard.shard_bounds(args.stream, world, rank)
     reqs, plen, first, ncopies, alen = shard.stream_records(preqs, len(parena), lo, hi)
@@ -327,7 +344,8 @@ def stress_leg(torch, engine, records, workloads, args, local):
         e.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), alen, n, d_out.data_ptr(), d_hits.data_ptr(), cap, s)
         e.sync(s)
     steps = max(1, min(args.steps, 5))
-    # warmup: a batch that overflows the stream's WAF buffers is void and grows them (gm_sync)
+    # warmup: a batch whose hits overflow d_hits returns GM_E_OVERFLOW with no counters committed and
+    # grows the stream's buffers (gm_sync); the retry is a whole batch
     ok, tries = 0, 0
     while ok < max(1, args.warmup) and tries < 12:
         tries += 1

@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 6u   /* 6: n_rsl_reversed; 5: gm_update_upstream / gm_peers_migrate; 4: union-DFA stats */
+#define GM_ABI_VERSION 7u   /* 7: GM_ACT_TOO_LARGE, GM_REQ_CHUNKED, gm_rejects, build flags; 6: n_rsl_reversed;
+                               5: gm_update_upstream / gm_peers_migrate; 4: union-DFA stats */
 
 /* ---------------------------------------------------------------- status codes */
 #define GM_OK            0
@@ -49,6 +50,10 @@ extern "C" {
 #define GM_CREATE_SERIAL        0x4u  /* measurement: run the route stage alone before the WAF scan */
                                       /* (default: beside it on a side stream), so each stage's     */
                                       /* HIP-event time is its own                                  */
+/* test hook: the internal WAF buffers (candidates, survivors, pairs, jobs) at 2^-k of their default
+ * capacity, k = 1..31 (bits 8..15), so the overflow continuations run on batches small enough for
+ * the oracle; reported in gm_stats_t.scratch_scale */
+#define GM_CREATE_SCRATCH_SHIFT(k) (((uint32_t)(k) & 0xFFu) << 8)
 
 /* ---------------------------------------------------------------- packed request record
  * One 64-byte header per request; payload bytes live in one byte arena.  The payload of a
@@ -88,6 +93,9 @@ typedef struct gm_req {
 #define GM_REQ_INVALID 0x08u  /* the wire parser rejected the request (gm_parse_requests): the  */
                               /* HTTP status nginx answers is in pad0[1] | pad0[2] << 8, and   */
                               /* gm_match_batch answers GM_ACT_BAD_REQUEST with that status     */
+#define GM_REQ_CHUNKED 0x10u  /* the body came chunked (Transfer-Encoding: chunked; body_len =  */
+                              /* the decoded length): client_max_body_size applies when the     */
+                              /* proxying location reads it, not to a Content-Length up front   */
 
 typedef struct gm_batch {
     const gm_req  *reqs;      /* n headers (device pointer unless GM_BATCH_HOST)          */
@@ -133,7 +141,9 @@ enum {
     GM_ACT_UNSUPPORTED  = 8,  /* location uses a construct the compiler rejected, or the   */
                               /* regex search reached a PCRE-only regex location whose     */
                               /* superset pattern matches: the data plane defers to nginx  */
-    GM_ACT_NO_LISTENER  = 9   /* no server listens on the port / TLS on a plain port      */
+    GM_ACT_NO_LISTENER  = 9,  /* no server listens on the port / TLS on a plain port      */
+    GM_ACT_TOO_LARGE    = 10  /* 413: the body exceeds client_max_body_size (nginx.ingress.tmpl:175, */
+                              /* nginx.virtualserver.tmpl:93) -- no WAF phase, nothing proxied */
 };
 
 enum { GM_ROUTE_NONE = 0, GM_ROUTE_PLAIN = 1, GM_ROUTE_SPLIT = 2, GM_ROUTE_RULES = 3 };
@@ -163,7 +173,10 @@ typedef struct gm_stats_t {
     uint32_t n_sig_regex;
     uint32_t n_sig_regex_always;  /* regexes with no >=4-byte required factor           */
     uint32_t n_rejected_pcre;     /* regexes using PCRE-only constructs (rejected)      */
-    uint32_t n_rejected_other;    /* other constructs rejected (snippets, nested loc...) */
+    uint32_t n_rejected_other;    /* other constructs rejected: every directive outside the     */
+                                  /* known-neutral set (snippets: deny, auth_basic, ...), nested */
+                                  /* locations; the requests reaching one are GM_ACT_UNSUPPORTED */
+                                  /* (gm_rejects lists them)                                    */
     uint32_t n_dfa_states;
     uint32_t n_counters;          /* n_locations + n_sigs                               */
     uint64_t table_bytes;         /* device table bytes of the generation               */
@@ -195,7 +208,19 @@ typedef struct gm_stats_t {
     /* of n_rsl_slices: slices of X$ regex locations run backwards from the URI's end, and forward
      * slices run only for requests whose $uri holds one of their regexes' factors */
     uint32_t n_rsl_reversed, n_rsl_pref;
+    /* servers with a realip configuration (set_real_ip_from ...), and the build: GM_BUILD_* bits of
+     * the measurement / test variants compiled into this library (0 = the product build) */
+    uint32_t n_realip;
+    uint32_t build_flags;
+    /* the internal WAF capacity scale in effect (GM_CREATE_SCRATCH_SHIFT test hook; 1.0 normally) */
+    float    scratch_scale;
+    uint32_t reserved_stats[5];
 } gm_stats_t;
+
+/* gm_stats_t.build_flags: measurement / test variants compiled into the library.  bench.py refuses
+ * a non-zero value unless told it measures a variant. */
+#define GM_BUILD_EXPERIMENT   0x1u   /* a GM_EXP_* measurement macro (timing only) */
+#define GM_BUILD_TUNING       0x2u   /* a non-default GM_SCAN_* / GM_ROUTE_* / GM_RLOC_* / GM_WIRE_* value */
 
 /* Request parsers (Wallarm's) a signature set can declare ("@decoders" line of
  * the GM_ENTRY_SIGS text); wallarm_parser_disable <name> (annotations.go:320-329,
@@ -369,6 +394,11 @@ int         gm_peers_migrate(gm_ctx *ctx, const gm_peer_state *old_state, uint32
 int         gm_peer_address(gm_ctx *ctx, uint32_t peer, char *buf, size_t cap, uint32_t *upstream_id);
 
 int         gm_stats(gm_ctx *ctx, gm_stats_t *out);
+/* The constructs the live generation's compile rejected (n_rejected_other / n_rejected_pcre), one
+ * per line, "context: directive args" -- the Manager wrapper logs them after Reload (SURVEY §8 b:
+ * counted and logged, never a Reload error).  Returns the text's length (written up to cap - 1
+ * bytes, NUL-terminated), or a negative GM_E_*. */
+int         gm_rejects(gm_ctx *ctx, char *buf, size_t cap);
 /* Message of the calling thread's last failing call (thread-local; ctx is not consulted). */
 const char *gm_last_error(gm_ctx *ctx);
 

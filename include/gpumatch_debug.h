@@ -40,6 +40,9 @@ int gm_debug_waf_lit_bytes(struct gm_ctx *ctx, uint32_t row, uint8_t *out, size_
 int64_t gm_debug_waf_prefilter(struct gm_ctx *ctx, const uint8_t *A, size_t len, uint64_t *out, size_t cap);
 /* The same followed by k_waf_verify's stage-2 context filter: the windows that reach the exact check. */
 int64_t gm_debug_waf_prefilter2(struct gm_ctx *ctx, const uint8_t *A, size_t len, uint64_t *out, size_t cap);
+/* The realip address rules on the host (gm_inet.hpp, the code the device runs): `text` parsed as
+ * ngx_parse_addr_port -> "<ngx_sock_ntop text> <port>" into out; -1 if it is not an address. */
+int gm_debug_inet(const uint8_t *text, size_t n, char *out, size_t cap);
 #ifdef __cplusplus
 }
 #endif

@@ -18,6 +18,7 @@
 #include <set>
 #include <unordered_map>
 
+#include "gm_inet.hpp"
 #include "gm_regex.hpp"
 
 namespace gm {
@@ -137,6 +138,8 @@ struct Loc {
     LocKind kind = PFX;
     std::string path;
     bool has_proxy = false, has_return = false, nested = false;
+    bool unknown = false;        // a directive outside the known-neutral set (default-deny)
+    std::string cmbs;            // client_max_body_size given here ("" inherit)
     std::string ups, err418;
     std::string pass_uri;        // the URI part of proxy_pass (nginx.org/rewrites), "" none
     uint32_t parser_off = 0;     // wallarm_parser_disable in the location (DEC_* bits)
@@ -145,10 +148,20 @@ struct Loc {
     int code = 0;
     int waf = -1;
 };
-struct SIf { std::string var; int op = 0; std::string val; int code = 0; bool ret_only = false; };
+// nocount: an http-level deferral repeated in every server (counted once, at the http block)
+struct SIf { std::string var; int op = 0; std::string val; int code = 0; bool ret_only = false; bool nocount = false; };
+// realip settings of a server (or the http block, which servers inherit, ngx_http_realip_merge_loc_conf)
+struct RealIpIR {
+    std::vector<std::string> from;   // set_real_ip_from values, config order
+    std::string header;              // real_ip_header value ("" unset)
+    int recursive = -1;              // real_ip_recursive (-1 unset)
+    bool bad = false;                // a value the engine does not model (a duplicate header)
+};
 struct Server {
     int id = 0, waf = GM_WAF_OFF;
     uint32_t parser_off = 0;     // server-level wallarm_parser_disable (DEC_* bits)
+    std::string cmbs;            // server-level client_max_body_size ("" inherit)
+    RealIpIR rip;
     std::vector<std::pair<int, int>> listens;   // port, flags (1 ssl, 2 default)
     std::vector<std::string> names;
     std::vector<SIf> ifs;
@@ -182,7 +195,41 @@ struct Model {
     std::vector<std::string> upstreams;
     int http_waf = GM_WAF_OFF;
     uint32_t rejected_other = 0, rejected_pcre = 0;
+    std::string http_cmbs;       // http-level client_max_body_size ("" = nginx's default 1m)
+    RealIpIR http_rip;
+    bool http_unknown = false;   // an http-level directive outside the known set: every server defers
+    std::vector<std::string> reject_log;   // "context: directive" of every construct rejected
 };
+
+// ---- default-deny.  The directives the compile knows to leave a request's
+// verdict alone: what goes upstream (proxy_* / grpc_*), TLS, logging, response headers, timeouts,
+// buffers, Wallarm tuning -- everything the reference templates emit besides the directives the
+// engine models (version1/nginx.ingress.tmpl, version2/nginx.virtualserver.tmpl, version1/nginx.tmpl
+// and their Plus variants).  Any other directive reaching a request (snippets: `deny all;`,
+// `auth_basic`, `limit_except`, `internal`, `root` ...) makes it GM_ACT_UNSUPPORTED, counted in
+// n_rejected_other and listed by gm_rejects.  Restated in oracle/gm_oracle.c (neutral_directive).
+bool neutral_directive(const std::string &n, int ctx /* 0 http, 1 server, 2 location */) {
+    static const char *pre[] = {"proxy_", "grpc_", "ssl_", "gzip", "http2_", "open_file_cache", "sub_filter",
+                                "keepalive_", "wallarm_"};
+    for (const char *p : pre) if (n.rfind(p, 0) == 0) return true;
+    static const std::set<std::string> any = {
+        "add_header", "add_trailer", "access_log", "error_log", "log_not_found", "log_subrequest",
+        "default_type", "charset", "charset_types", "source_charset", "override_charset", "expires", "etag",
+        "send_timeout", "client_body_timeout", "client_body_buffer_size", "client_body_temp_path",
+        "client_header_timeout", "sendfile", "sendfile_max_chunk", "tcp_nodelay", "tcp_nopush",
+        "server_tokens", "status_zone", "chunked_transfer_encoding", "output_buffers", "postpone_output",
+        "lingering_close", "lingering_time", "lingering_timeout", "reset_timedout_connection", "resolver",
+        "resolver_timeout", "auth_jwt_key_file", "auth_jwt_leeway", "port_in_redirect",
+        "server_name_in_redirect", "absolute_redirect", "msie_padding", "msie_refresh"};
+    if (any.count(n)) return true;
+    if (ctx == 2) return n == "health_check";
+    static const std::set<std::string> http = {
+        "log_format", "server_names_hash_max_size", "server_names_hash_bucket_size", "variables_hash_max_size",
+        "variables_hash_bucket_size", "types_hash_max_size", "types_hash_bucket_size", "map_hash_max_size",
+        "map_hash_bucket_size", "limit_req_zone", "limit_conn_zone", "proxy_cache_path", "geo", "match",
+        "js_include", "js_import", "keyval_zone", "types"};
+    return ctx == 0 && http.count(n);
+}
 
 int waf_mode(const std::string &s) {
     if (s == "monitoring") return GM_WAF_MONITORING;
@@ -198,18 +245,26 @@ struct Builder {
     const std::vector<std::vector<Dir>> &confd;
     explicit Builder(Model &m, const std::vector<std::vector<Dir>> &c) : M(m), confd(c) {}
 
+    // a rejected construct: counted (n_rejected_other) and listed for the Manager's log (gm_rejects)
+    void reject(const std::string &where, const Dir &k) {
+        std::string t = where + ": ";
+        for (size_t q = 0; q < k.a.size() && q < 3; q++) t += (q ? " " : "") + k.a[q];
+        M.reject_log.push_back(t);
+    }
+
     void location(Server &S, const Dir &d) {
         Loc L;
         L.id = (int)M.locs.size(); L.server = S.id;
         if (d.a.size() == 3) {
             const std::string &m = d.a[1];
             L.kind = m == "=" ? EXACT : m == "^~" ? NOREGEX : m == "~" ? RX : m == "~*" ? RXI : PFX;
-            if (L.kind == PFX) M.rejected_other++;
+            if (L.kind == PFX) { M.rejected_other++; reject("location", d); }
             L.path = d.a[2];
         } else if (d.a.size() == 2) {
             L.path = d.a[1];
             L.kind = (!L.path.empty() && L.path[0] == '@') ? NAMED : PFX;
         }
+        const std::string where = "location " + L.path;
         for (const Dir &k : d.body) {
             if (k.a.empty()) continue;
             const std::string &n = k.a[0];
@@ -229,17 +284,40 @@ struct Builder {
                 L.code = isdigit((unsigned char)k.a[1][0]) ? atoi(k.a[1].c_str()) : 302;
             } else if (n == "error_page" && k.a.size() == 4 && k.a[1] == "418" && k.a[2] == "=") {
                 L.err418 = k.a[3];
+            } else if (n == "error_page" && k.a.size() >= 3 && k.a.back().rfind("@grpcerror", 0) == 0) {
+                // the gRPC error pages (version1/nginx.ingress.tmpl:121-133): a named location that
+                // answers the same status, so the verdict does not change
             } else if (n == "wallarm_mode" && k.a.size() == 2) {
                 L.waf = waf_mode(k.a[1]);
             } else if (n == "wallarm_parser_disable" && k.a.size() == 2) {
                 L.parser_off |= decoder_bit(k.a[1]); L.has_pd = true;
+            } else if (n == "client_max_body_size" && k.a.size() == 2) {
+                L.cmbs = k.a[1];
             } else if (n == "location" || n == "if" || n == "rewrite") {
                 L.nested = true;
+                reject(where, k);
+            } else if (n == "auth_jwt" && k.a.size() == 2 && k.a[1] == "off") {
+            } else if (!neutral_directive(n, 2)) {
+                L.unknown = true;
+                reject(where, k);
             }
         }
-        if (L.nested) M.rejected_other++;
+        if (L.nested || L.unknown) M.rejected_other++;
         M.locs.push_back(L);
         S.locs.push_back(L.id);
+    }
+
+    // realip directives of a server or the http block; false: not one
+    static bool realip_dir(RealIpIR &R, const Dir &k) {
+        const std::string &n = k.a[0];
+        if (n == "set_real_ip_from" && k.a.size() == 2) { R.from.push_back(k.a[1]); return true; }
+        if (n == "real_ip_header" && k.a.size() == 2) {
+            if (!R.header.empty()) R.bad = true;   // nginx: "is duplicate" (a config error)
+            R.header = k.a[1];
+            return true;
+        }
+        if (n == "real_ip_recursive" && k.a.size() == 2) { R.recursive = k.a[1] == "on" ? 1 : 0; return true; }
+        return false;
     }
 
     void server(const Dir &d) {
@@ -250,6 +328,13 @@ struct Builder {
             if (k.a.size() == 2 && k.a[0] == "wallarm_mode") S.waf = waf_mode(k.a[1]);
             if (k.a.size() == 2 && k.a[0] == "wallarm_parser_disable") S.parser_off |= decoder_bit(k.a[1]);
         }
+        auto defer_here = [&](const Dir &k) {
+            // a construct outside the modelled subset: a request that reaches it in the server's
+            // directive order defers to nginx (GM_ACT_UNSUPPORTED), counted
+            SIf f; f.var = "$uri"; f.op = -1;
+            S.ifs.push_back(f);
+            reject("server", k);
+        };
         for (const Dir &k : d.body) {
             if (k.a.empty()) continue;
             const std::string &n = k.a[0];
@@ -275,13 +360,17 @@ struct Builder {
                     if (a.back().size() == 1) a.pop_back(); else a.back().pop_back();
                 }
                 SIf f;
-                bool has_ret = false;
-                for (const Dir &r : k.body)
+                bool has_ret = false, other = false;
+                for (const Dir &r : k.body) {
                     if (r.a.size() >= 2 && r.a[0] == "return") {
                         has_ret = true;
                         f.code = isdigit((unsigned char)r.a[1][0]) ? atoi(r.a[1].c_str()) : 302;
+                    } else if (!(r.a.size() >= 2 && r.a[0] == "set" && r.a[1] == "$hsts_header_val")) {
+                        other = true;
                     }
-                if (!has_ret) continue;
+                }
+                if (other) { defer_here(k); continue; }
+                if (!has_ret) continue;   // the HSTS `if` (nginx.ingress.tmpl:66-71) only sets a header value
                 if (a.size() == 1) { f.var = a[0]; f.op = 0; }
                 else if (a.size() == 3) {
                     f.var = a[0]; f.val = a[2];
@@ -293,13 +382,17 @@ struct Builder {
                 SIf f; f.ret_only = true;
                 f.code = isdigit((unsigned char)k.a[1][0]) ? atoi(k.a[1].c_str()) : 302;
                 S.ifs.push_back(f);
-            } else if (n == "rewrite") {
-                // server-level rewrite (server snippets): not compiled -- a request reaching it
-                // in the server rewrite phase defers to nginx (GM_ACT_UNSUPPORTED), counted
-                SIf f; f.var = "$uri"; f.op = -1;
-                S.ifs.push_back(f);
             } else if (n == "location" && k.block) {
                 location(S, k);
+            } else if (n == "client_max_body_size" && k.a.size() == 2) {
+                S.cmbs = k.a[1];
+            } else if (realip_dir(S.rip, k)) {
+            } else if (n == "set" && k.a.size() >= 2 && k.a[1] == "$hsts_header_val") {
+            } else if (n == "error_page" && k.a.size() >= 3 && k.a.back().rfind("@grpcerror", 0) == 0) {
+            } else if (n == "auth_jwt" && k.a.size() == 2 && k.a[1] == "off") {
+            } else if (n == "rewrite" || !neutral_directive(n, 1)) {
+                // (a server-level rewrite, server snippets: not compiled either)
+                defer_here(k);
             }
         }
         M.servers.push_back(std::move(S));
@@ -350,6 +443,13 @@ struct Builder {
             const std::string &n = d.a[0];
             if (n == "include" && d.a.size() == 2 && d.a[1].find("conf.d/") != std::string::npos) {
                 for (auto &f : confd) http(f);
+            } else if (n == "include" && d.a.size() == 2 &&
+                       (d.a[1] == "/etc/nginx/mime.types" || d.a[1] == "mime.types" ||
+                        d.a[1] == "/etc/nginx/config-version.conf")) {
+                // MIME types; the config-version server (verify.go:81-92, a unix-socket listener)
+            } else if (n == "client_max_body_size" && d.a.size() == 2) {
+                M.http_cmbs = d.a[1];
+            } else if (realip_dir(M.http_rip, d)) {
             } else if (n == "wallarm_mode" && d.a.size() == 2) {
                 M.http_waf = waf_mode(d.a[1]);
             } else if (n == "upstream" && d.block && d.a.size() == 2) {
@@ -384,6 +484,12 @@ struct Builder {
                 M.splits[s.var] = s;
             } else if (n == "server" && d.block) {
                 server(d);
+            } else if (!neutral_directive(n, 0)) {
+                // applies to every server (access-phase directives, http snippets): every request
+                // defers after its server's rewrite phase
+                if (!M.http_unknown) M.rejected_other++;
+                M.http_unknown = true;
+                reject("http", d);
             }
         }
     }
@@ -458,6 +564,53 @@ static std::string relax_pcre_only(const std::string &p) {
 }
 
 uint32_t pow2_at_least(size_t n) { uint32_t c = 16; while (c < n) c <<= 1; return c; }
+
+// client_max_body_size (ngx_parse_offset): decimal digits with an optional k / m / g suffix;
+// 0 = no limit.  BODY_UNLIMITED for 0 and for limits no u32 body length can pass; -1: not a size
+int64_t parse_body_max(const std::string &v) {
+    if (v.empty()) return -1;
+    size_t n = v.size();
+    uint64_t scale = 1;
+    const char u = v[n - 1];
+    if (u == 'k' || u == 'K') { scale = 1024; n--; }
+    else if (u == 'm' || u == 'M') { scale = 1024 * 1024; n--; }
+    else if (u == 'g' || u == 'G') { scale = 1024ull * 1024 * 1024; n--; }
+    if (n == 0) return -1;
+    uint64_t x = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (v[i] < '0' || v[i] > '9') return -1;
+        x = x * 10 + (uint64_t)(v[i] - '0');
+        if (x > (1ull << 40)) return BODY_UNLIMITED;   // past any u32 body length either way
+    }
+    x *= scale;
+    return x == 0 || x >= BODY_UNLIMITED ? (int64_t)BODY_UNLIMITED : (int64_t)x;
+}
+
+// ngx_ptocidr: "addr[/bits]" -> family + masked network-order bytes; false: not an address
+// (nginx would resolve a host name here: the engine does not)
+bool parse_cidr(const std::string &t, DCidr &c) {
+    memset(&c, 0, sizeof c);
+    const size_t sl = t.find('/');
+    const std::string a = sl == std::string::npos ? t : t.substr(0, sl);
+    uint8_t b[16] = {0}, m[16] = {0};
+    const uint32_t fam = ngx_parse_addr((const uint8_t *)a.data(), (uint32_t)a.size(), b);
+    if (!fam) return false;
+    const uint32_t nb = fam == 4 ? 4 : 16;
+    int64_t bits = (int64_t)nb * 8;
+    if (sl != std::string::npos) {
+        bits = ngx_atoi_dec((const uint8_t *)t.data() + sl + 1, (uint32_t)(t.size() - sl - 1));
+        if (bits < 0 || bits > (int64_t)nb * 8) return false;
+    }
+    for (uint32_t i = 0; i < nb; i++) {
+        const int64_t k = bits - 8 * (int64_t)i;
+        m[i] = k >= 8 ? 0xFF : k <= 0 ? 0 : (uint8_t)(0xFF << (8 - k));
+        b[i] &= m[i];   // nginx warns "low address bits are meaningless" and clears them
+    }
+    c.family = fam;
+    memcpy(c.addr, b, 16);
+    memcpy(c.mask, m, 16);
+    return true;
+}
 
 struct Compiler {
     Model &M;
@@ -1160,6 +1313,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
 
     Compiler C(M, st);
     st.n_rejected_other += M.rejected_other;
+    R.rejects = M.reject_log;
 
     // ---- upstreams: sorted unique name table
     std::vector<std::string> ups = M.upstreams;
@@ -1353,10 +1507,58 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     };
     auto is_redirect = [](int code) { return code == 301 || code == 302 || code == 303 || code == 307 || code == 308; };
     (void)is_redirect;
+    std::vector<DRealIp> realips;
+    std::vector<DCidr> cidrs;
+    auto body_of = [&](const std::string &own, const Server &S, bool &bad) -> uint32_t {
+        // client_max_body_size in effect: the location's, else the server's, else the http
+        // block's, else nginx's default 1m (ngx_http_core_merge_loc_conf)
+        const std::string &v = !own.empty() ? own : !S.cmbs.empty() ? S.cmbs : !M.http_cmbs.empty() ? M.http_cmbs
+                                                                                                         : std::string("1m");
+        const int64_t x = parse_body_max(v);
+        bad = x < 0;
+        return x < 0 ? BODY_UNLIMITED : (uint32_t)x;
+    };
     for (auto &S : M.servers) {
         DServer &D = dservers[S.id];
         D.trie_root = new_node();
         D.waf_mode = (uint32_t)S.waf;
+        bool sbad = false;
+        D.body_max = body_of("", S, sbad);
+        if (sbad) { S.ifs.insert(S.ifs.begin(), SIf{"$uri", -1}); R.rejects.push_back("server: client_max_body_size " + S.cmbs); }
+        // realip in effect (ngx_http_realip_merge_loc_conf: the server's set_real_ip_from list,
+        // else the http block's; header and recursion merged one by one)
+        D.realip = GM_NONE;
+        {
+            const RealIpIR &a = S.rip, &h = M.http_rip;
+            const std::vector<std::string> &from = !a.from.empty() ? a.from : h.from;
+            const std::string hdr = !a.header.empty() ? a.header : !h.header.empty() ? h.header : std::string("X-Real-IP");
+            const int rec = a.recursive >= 0 ? a.recursive : h.recursive >= 0 ? h.recursive : 0;
+            if (!from.empty()) {
+                DRealIp ri{};
+                ri.recursive = (uint32_t)rec;
+                ri.first_cidr = (uint32_t)cidrs.size();
+                bool bad = a.bad || h.bad;
+                for (const std::string &f : from) {
+                    if (f.rfind("unix:", 0) == 0) continue;   // never a TCP client
+                    DCidr c;
+                    if (!parse_cidr(f, c)) { bad = true; continue; }
+                    cidrs.push_back(c);
+                }
+                ri.n_cidr = (uint32_t)cidrs.size() - ri.first_cidr;
+                // (strcmp, case-sensitive: ngx_http_realip)
+                if (hdr == "X-Real-IP") ri.type = RIP_XREALIP;
+                else if (hdr == "X-Forwarded-For") ri.type = RIP_XFWD;
+                else if (hdr == "proxy_protocol") ri.type = RIP_PROXY;
+                else { ri.type = RIP_HEADER; ri.hdr_off = C.put_bytes(lower(hdr)); ri.hdr_len = (uint32_t)hdr.size(); }
+                // the address nginx would use is unknown to the engine: a hostname in
+                // set_real_ip_from, or the PROXY protocol header the records do not carry --
+                // requests whose verdict reads $remote_addr / $remote_port defer
+                if (bad) { ri.type = RIP_UNKNOWN; st.n_rejected_other++; R.rejects.push_back("server: set_real_ip_from (not an address)"); }
+                D.realip = (uint32_t)realips.size();
+                realips.push_back(ri);
+            }
+        }
+        if (M.http_unknown) { SIf f; f.var = "$uri"; f.op = -1; f.nocount = true; S.ifs.push_back(f); }
         D.first_if = (uint32_t)sifs.size();
         for (auto &f : S.ifs) {
             DServerIf x{};
@@ -1364,7 +1566,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             if (f.ret_only) x.op = SIF_RETURN;
             else {
                 int s = C.src(f.var);
-                if (s < 0 || f.op < 0) { x.op = 0xFF; st.n_rejected_other++; }
+                if (s < 0 || f.op < 0) { x.op = 0xFF; if (!f.nocount) st.n_rejected_other++; }
                 else {
                     x.src = (uint32_t)s;
                     if (f.op == 0) x.op = 4;   // truthy: non-empty and not "0"
@@ -1405,7 +1607,12 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             dl.upstream = GM_NONE;
             dl.noregex = L.kind == NOREGEX;
             dl.is_named = L.kind == NAMED;
-            if (L.nested) dl.kind = LK_UNSUPPORTED;
+            bool lbad = false;
+            dl.body_max = body_of(L.cmbs, S, lbad);
+            if (lbad) { L.unknown = true; st.n_rejected_other++; R.rejects.push_back("location " + L.path + ": client_max_body_size " + L.cmbs); }
+            // a nested `location` can change which location's limit applies: no 413 decided here
+            if (L.nested) dl.body_max = BODY_UNLIMITED;
+            if (L.nested || L.unknown) dl.kind = LK_UNSUPPORTED;
             else if (L.has_return && L.code == 418 && !L.err418.empty()) {
                 std::vector<std::string> vv;
                 int route = -1;
@@ -1452,7 +1659,9 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 std::vector<std::string> fac;
                 bool sup = false;
                 int d = C.regex(L.path, L.kind == RXI, nullptr, &fac, &sup);
-                if (d < 0 || sup) dl.kind = LK_UNSUPPORTED;   // sup: the DFA is a superset
+                // sup: the DFA is a superset -- the location is reached only maybe, so its limit
+                // is not applied either
+                if (d < 0 || sup) { dl.kind = LK_UNSUPPORTED; dl.body_max = BODY_UNLIMITED; }
                 rlocs.push_back(DRegexLoc{d >= 0 ? (uint32_t)d : GM_NONE, (uint32_t)lid});
                 rloc_factors.push_back(std::move(fac));
                 Dfa rv;
@@ -1957,6 +2166,10 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_alw_rule = I.put(alw_rule);
     rsl_pbit.resize((rsl_pbit.size() + 3) & ~size_t(3), 0xFF);
     h.off_rsl_pbit = I.put(rsl_pbit);
+    // (before the upstream section: gm_update_upstream copies everything before it unchanged)
+    h.n_realip = (uint32_t)realips.size(); h.n_cidrs = (uint32_t)cidrs.size();
+    st.n_realip = h.n_realip;
+    h.off_realip = I.put(realips); h.off_cidrs = I.put(cidrs);
     h.n_rk_cap = rkcap; h.n_rk_ids = (uint32_t)rk_ids.size(); h.n_rk_ents_keys = (uint32_t)rk_lists.size();
     h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_rk_ents = I.put(rk_ents); h.off_rk_bloom = I.put(rk_bloom);
     h.n_rk_ents_n = (uint32_t)rk_ents.size();
@@ -2118,6 +2331,8 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.alw_pack = b + h.off_alw_pack;
     t.alw_rule = (const uint32_t *)(b + h.off_alw_rule);
     t.rsl_pbit = b + h.off_rsl_pbit;
+    t.realip = (const DRealIp *)(b + h.off_realip);
+    t.cidrs = (const DCidr *)(b + h.off_cidrs);
     t.n_always_lds = h.n_always_lds; t.n_alw_groups = h.n_alw_groups; t.n_alw_slices = h.n_alw_slices;
     t.n_rsl = h.n_rsl; t.n_rk_prefilter = h.n_rk_prefilter;
     t.n_ports = h.n_ports;

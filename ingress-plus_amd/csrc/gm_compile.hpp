@@ -29,6 +29,7 @@ struct CompileResult {
     std::vector<uint32_t> peer_ups;        // per global peer id: its upstream id
     std::vector<UpstreamMeta> ups_meta;    // per upstream id
     std::vector<uint32_t> peer_map;        // update_upstream: new peer id -> old peer id or GM_NONE
+    std::vector<std::string> rejects;      // every rejected construct, "context: directive" (gm_rejects)
 };
 
 CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen);

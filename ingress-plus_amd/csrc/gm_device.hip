@@ -29,6 +29,7 @@
 
 #include "../../include/gpumatch.h"
 #include "gm_compile.hpp"
+#include "gm_inet.hpp"
 #include "gm_tables.hpp"
 
 using namespace gm;
@@ -67,7 +68,9 @@ struct Val {
     int cnt;
     uint32_t total;
     bool overflow;
-    __device__ void clear() { cnt = 0; total = 0; overflow = false; }
+    bool unknown;            // a value the engine cannot know ($remote_addr under realip from the
+                             // PROXY protocol header): the step that reads it defers the request
+    __device__ void clear() { cnt = 0; total = 0; overflow = false; unknown = false; }
     __device__ void add(const uint8_t *q, uint32_t len) {
         if (len == 0) return;
         if (cnt == MAXSEG) { overflow = true; return; }
@@ -79,19 +82,34 @@ __constant__ uint8_t c_const[64] = "httpsonh2; , ?HTTP/2.0HTTP/1.0HTTP/1.1 01234
 // offsets into c_const: "http" 0, "https" 0(5), "on" 5, "h2" 7, "; " 9, ", " 11, "?" 13,
 // "HTTP/2.0" 14, "HTTP/1.0" 22, "HTTP/1.1" 30, " " 38, hex digits 39
 
+// realip outcome of a request (computed on first use): the connection address stays, the module
+// replaced it (ra: the new address, its text and port), or the engine cannot know it
+enum : uint32_t { RIPS_SAME = 1, RIPS_NEW = 2, RIPS_UNKNOWN = 3 };
 struct Ctx {
     const uint8_t *A;
     Rec r;
     uint64_t uri, args, hdrs, body, host, method, ruri, raddr;
     uint8_t scratch[48];   // $request_id hex / $remote_port digits
+    uint32_t rip;          // the server's DRealIp (GM_NONE: none)
+    uint32_t rip_state;    // RIPS_*
+    InetAddr ra, ra_tmp;   // (ra: the connection address, then the one the module takes)
+    uint32_t ra_len;
+    uint8_t ra_txt[48];
 };
 
-__device__ void ctx_init(Ctx &c, const uint8_t *A, const Rec &r) {
+__device__ void realip_eval(Ctx &c, const GTab &t);
+// rip: the server's realip settings -- evaluated here, at the top of the out-of-line step that
+// needs the request's variables, where little else is live (called from deep inside the variable
+// lookup, the call chain raised the route kernel's register allocation past its occupancy target)
+__device__ __forceinline__ void ctx_init(Ctx &c, const uint8_t *A, const Rec &r, const GTab *t = nullptr,
+                                         uint32_t rip = GM_NONE) {
     c.A = A; c.r = r;
     uint64_t o = r.base;
     c.uri = o; o += r.uri_len; c.args = o; o += r.args_len; c.hdrs = o; o += r.hdr_len;
     c.body = o; o += r.body_len; c.host = o; o += r.host_len; c.method = o; o += r.method_len;
     c.ruri = o; o += r.ruri_len; c.raddr = o;
+    c.rip = rip; c.rip_state = RIPS_SAME;
+    if (rip != GM_NONE) realip_eval(c, *t);
 }
 
 // exact per-byte flags (bit 7 of each byte) of the zero bytes of x
@@ -154,6 +172,13 @@ __device__ bool hdr_next(const uint8_t *A, HdrIt &it, uint64_t &ns, uint32_t &nl
     return false;
 }
 
+// header name vs a lowercase name, case-insensitively (the headers_in hash: lowcase_key)
+__device__ bool hdr_name_ci(const uint8_t *A, uint64_t ns, uint32_t nl, const uint8_t *want, uint32_t wl) {
+    if (nl != wl) return false;
+    for (uint32_t i = 0; i < nl; i++) if (lc(A[ns + i]) != want[i]) return false;
+    return true;
+}
+
 // header name vs variable suffix (lowercase, '-' -> '_'), ngx_http_variable_unknown_header
 __device__ bool hdr_name_is(const uint8_t *A, uint64_t ns, uint32_t nl, const uint8_t *var, uint32_t vl) {
     if (nl != vl) return false;
@@ -179,7 +204,11 @@ __device__ void get_var(Ctx &c, const GTab &t, uint32_t src_id, Val &v) {
         case V_ARGS: v.add(A + c.args, r.args_len); break;
         case V_URI: v.add(A + c.uri, r.uri_len); break;
         case V_REQUEST_BODY: break;
-        case V_REMOTE_ADDR: v.add(A + c.raddr, r.raddr_len); break;
+        case V_REMOTE_ADDR:
+            if (c.rip_state == RIPS_UNKNOWN) v.unknown = true;
+            else if (c.rip_state == RIPS_NEW) v.add(c.ra_txt, c.ra_len);
+            else v.add(A + c.raddr, r.raddr_len);
+            break;
         case V_HOST: v.add(A + c.host, r.host_len); break;
         case V_REQUEST_URI:
         case V_REQUEST:
@@ -205,6 +234,13 @@ __device__ void get_var(Ctx &c, const GTab &t, uint32_t src_id, Val &v) {
         case V_REMOTE_PORT:
         case V_SERVER_PORT: {
             uint32_t x = s.var == V_REMOTE_PORT ? r.rport : r.port;
+            if (s.var == V_REMOTE_PORT) {
+                if (c.rip_state == RIPS_UNKNOWN) { v.unknown = true; break; }
+                if (c.rip_state == RIPS_NEW) {
+                    x = c.ra.port;
+                    if (x == 0) break;   // ngx_http_variable_remote_port: no port -> ""
+                }
+            }
             uint8_t tmp[6]; int k = 0;
             do { tmp[k++] = (uint8_t)('0' + x % 10); x /= 10; } while (x);
             for (int i = 0; i < k; i++) c.scratch[i] = tmp[k - 1 - i];
@@ -276,6 +312,94 @@ __device__ void get_var(Ctx &c, const GTab &t, uint32_t src_id, Val &v) {
             p = amp + 1;
         }
     }
+}
+
+// ---- ngx_http_realip_module (post-read phase, nginx 1.17.3), for a server that configures it
+// (set_real_ip_from, version1/nginx.ingress.tmpl:46-49, version2/nginx.virtualserver.tmpl:64-72).
+// The client address comes from X-Real-IP (the first such header), a named header (the first),
+// or X-Forwarded-For (every such header, the last one first).  A trusted (set_real_ip_from)
+// connection address is replaced by the header's last address; with real_ip_recursive on, the
+// list is walked leftwards past every trusted address (ngx_http_get_forwarded_addr).  $remote_addr
+// then shows the new address as ngx_sock_ntop text, $remote_port its port (or "").  Out of line,
+// run once per request that reads the address.  (The connection address is the record's raddr
+// text; one that does not parse as an address is never trusted.)
+// (register-light: the addresses live in the lane's Ctx -- private memory -- and the tables are read
+// in place, so this rare step does not raise the route kernel's register allocation)
+// out-of-line leaves: each keeps its own small register frame, so the call chain under
+// realip_eval stays under the route kernel's occupancy target
+__device__ __noinline__ bool d_parse_addr_port(const uint8_t *p, uint32_t n, InetAddr &a) { return ngx_parse_addr_port(p, n, a); }
+__device__ __noinline__ uint32_t d_parse_addr(const uint8_t *p, uint32_t n, uint8_t *b) { return ngx_parse_addr(p, n, b); }
+__device__ __noinline__ uint32_t d_addr_text(const InetAddr &a, uint8_t *out) { return ngx_addr_text(a, out); }
+__device__ __noinline__ bool rip_trusted(const GTab &t, const DRealIp *R, const InetAddr &a) {
+    if (!a.fam) return false;
+    for (uint32_t k = 0; k < R->n_cidr; k++) {
+        const DCidr *c = t.cidrs + R->first_cidr + k;
+        if (cidr_match1(a, c->family, reinterpret_cast<const uint8_t *>(c->addr), reinterpret_cast<const uint8_t *>(c->mask)))
+            return true;
+    }
+    return false;
+}
+// ngx_http_get_forwarded_addr_internal over one header value, its recursion as a loop:
+// 0 declined (a unchanged), 1 ok, 2 done (a = the last address taken); na: scratch
+constexpr int RIP_DECLINED = 0, RIP_OK = 1, RIP_DONE = 2;
+__device__ __forceinline__ int rip_forwarded(const GTab &t, const DRealIp *R, const uint8_t *x, uint32_t len, InetAddr &a,
+                                          InetAddr &na) {
+    for (int depth = 0;; depth++) {
+        if (!rip_trusted(t, R, a) || len == 0) return depth ? RIP_DONE : RIP_DECLINED;
+        uint32_t e = len;   // trailing ' ' and ',' (never the first byte)
+        while (e > 1 && (x[e - 1] == ' ' || x[e - 1] == ',')) e--;
+        uint32_t st = e - 1;   // the last address starts after the separator before it (byte 0
+        while (st > 0) {       // is never taken for a separator)
+            if (x[st] == ' ' || x[st] == ',') { st++; break; }
+            st--;
+        }
+        if (!d_parse_addr_port(x + st, e - st, na)) return depth ? RIP_DONE : RIP_DECLINED;
+        a = na;
+        if (R->recursive && st > 0) { len = st - 1; continue; }
+        return RIP_OK;
+    }
+}
+__device__ __noinline__ void realip_eval(Ctx &c, const GTab &t) {
+    const DRealIp *R = t.realip + c.rip;
+    const uint8_t *A = c.A;
+    InetAddr &a = c.ra;
+    a.port = 0;
+    a.fam = c.r.raddr_len <= 45 ? d_parse_addr(A + c.raddr, c.r.raddr_len, a.b) : 0u;
+    c.rip_state = RIPS_SAME;
+    const uint32_t type = R->type;
+    if (type == RIP_UNKNOWN) { c.rip_state = RIPS_UNKNOWN; return; }
+    if (type == RIP_PROXY) {   // the PROXY protocol address is not in the record
+        if (rip_trusted(t, R, a)) c.rip_state = RIPS_UNKNOWN;
+        return;
+    }
+    int rc = RIP_DECLINED;
+    HdrIt it{c.hdrs, c.hdrs + c.r.hdr_len};
+    uint64_t ns, vs; uint32_t nl, vl;
+    if (type == RIP_XFWD) {
+        // every X-Forwarded-For line, the last first (nginx's headers_in.x_forwarded_for array)
+        uint32_t nh = 0;
+        while (hdr_next(A, it, ns, nl, vs, vl)) nh += hdr_name_ci(A, ns, nl, (const uint8_t *)"x-forwarded-for", 15);
+        bool found = false;
+        for (uint32_t k = nh; k-- > 0;) {
+            HdrIt j{c.hdrs, c.hdrs + c.r.hdr_len};
+            uint32_t seen = 0;
+            while (hdr_next(A, j, ns, nl, vs, vl))
+                if (hdr_name_ci(A, ns, nl, (const uint8_t *)"x-forwarded-for", 15) && seen++ == k) break;
+            rc = rip_forwarded(t, R, A + vs, vl, a, c.ra_tmp);
+            if (!R->recursive) break;
+            if (rc == RIP_DECLINED && found) { rc = RIP_DONE; break; }
+            if (rc != RIP_OK) break;
+            found = true;
+        }
+    } else {
+        const uint8_t *want = type == RIP_XREALIP ? (const uint8_t *)"x-real-ip" : t.bytes + R->hdr_off;
+        const uint32_t wl = type == RIP_XREALIP ? 9u : R->hdr_len;
+        while (hdr_next(A, it, ns, nl, vs, vl))
+            if (hdr_name_ci(A, ns, nl, want, wl)) { rc = rip_forwarded(t, R, A + vs, vl, a, c.ra_tmp); break; }
+    }
+    if (rc == RIP_DECLINED) return;
+    c.ra_len = d_addr_text(a, c.ra_txt);
+    c.rip_state = RIPS_NEW;
 }
 
 __device__ bool val_eq(const Val &v, const uint8_t *key, uint32_t kl, bool nocase) {
@@ -357,9 +481,6 @@ __device__ __noinline__ int32_t rloc_prefiltered(const GTab &t, const DServer &S
                                                  uint32_t ulen, const uint32_t *rkb) {
     auto run = [&](uint32_t k) -> bool {
         const DRegexLoc rl = t.rlocs[S.first_rloc + k];
-#ifdef GM_EXP_NO_DFA
-        return true;
-#endif
 #ifdef GM_EXP_COUNT
         uint32_t steps = 0;
         const uint64_t t0 = __builtin_readcyclecounter();
@@ -379,11 +500,7 @@ __device__ __noinline__ int32_t rloc_prefiltered(const GTab &t, const DServer &S
 #pragma unroll
         for (int j = 0; j < RK_K; j++) c[j] = GM_NONE;
         uint32_t w = 0;
-        uint32_t scan_len = ulen;
-#ifdef GM_EXP_NO_COLLECT
-        scan_len = 0;
-#endif
-        for (uint32_t i = 0; i < scan_len; i++) {
+        for (uint32_t i = 0; i < ulen; i++) {
             w = (w >> 8) | ((uint32_t)u[i] << 24);
             if (i < 3) continue;
             const uint32_t key = fold4(w);
@@ -671,13 +788,16 @@ __device__ __noinline__ uint32_t host_wildcards(const uint8_t *h, int hl, const 
 // Generic (variable-reading) steps live in non-inlined functions so that the Ctx / Val
 // lane-private arrays only exist on these paths (scratch), never on the host/URI fast path.
 // server rewrite `if` on a request variable: 1 hit, 0 miss
-__device__ __noinline__ int server_if_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t if_idx) {
+// (-1: the variable's value is unknown to the engine -- the request defers)
+__device__ __noinline__ int server_if_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t if_idx,
+                                             uint32_t rip) {
     const Rec r = load_rec(rp);
     const DServerIf f = t.server_ifs[if_idx];
     Ctx c;
-    ctx_init(c, A, r);
+    ctx_init(c, A, r, &t, rip);
     Val v;
     get_var(c, t, f.src, v);
+    if (v.unknown) return -1;
     if (f.op == SIF_EQ) return val_eq(v, t.bytes + f.val_off, f.val_len, false);
     if (f.op == SIF_NE) return !val_eq(v, t.bytes + f.val_off, f.val_len, false);
     if (f.op == 4) return v.total && !(v.total == 1 && v.p[0][0] == '0');
@@ -685,12 +805,14 @@ __device__ __noinline__ int server_if_generic(const uint8_t *A, const gm_req *rp
     return f.op == 5 ? m : !m;
 }
 
-// rules route (compiled map chains) -> result index (0xFF default)
-__device__ __noinline__ uint8_t rules_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t rules_idx) {
+// rules route (compiled map chains) -> result index (0xFF default; -1 a condition read a value the
+// engine cannot know)
+__device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t rules_idx,
+                                          uint32_t rip) {
     const Rec r = load_rec(rp);
     const DRules R = t.rules[rules_idx];
     Ctx c;
-    ctx_init(c, A, r);
+    ctx_init(c, A, r, &t, rip);
     Val v;
     // header / cookie / argument values are looked up once per request, not once per condition
     // that reads them (every match of a rules route repeats the route's conditions); variables
@@ -717,6 +839,7 @@ __device__ __noinline__ uint8_t rules_generic(const uint8_t *A, const gm_req *rp
                     vp = &v;
                 }
             }
+            if (vp->unknown) return -1;
             bool m;
             if (cd.is_regex) m = vp->total > 0 && dfa_run_val(t, cd.dfa, *vp);
             else m = val_eq(*vp, t.bytes + cd.key_off, cd.key_len, true);
@@ -728,13 +851,15 @@ __device__ __noinline__ uint8_t rules_generic(const uint8_t *A, const gm_req *rp
 }
 
 // split_clients: murmur2 of the source -> part index (0xFF none, 0xFFFFFFFF unsupported value)
-__device__ __noinline__ uint32_t split_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t split_idx) {
+__device__ __noinline__ uint32_t split_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t split_idx,
+                                               uint32_t rip) {
     const Rec r = load_rec(rp);
     const DSplit Sp = t.splits[split_idx];
     Ctx c;
-    ctx_init(c, A, r);
+    ctx_init(c, A, r, &t, rip);
     Val v;
     get_var(c, t, Sp.src, v);
+    if (v.unknown) return 0xFFFFFFFFu;
     uint8_t buf[64];
     bool ok;
     const uint32_t hsh = murmur2_val(v, buf, ok);
@@ -769,7 +894,11 @@ constexpr uint32_t RLOC_STATUS_WORD = 16;   // batch status word: requests defer
 // (the location index, -1 none).  *sid_out: the server chosen (valid whenever *pend is set).
 constexpr int32_t RK_INLINE = -3, RK_DEFER = -2;
 __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
-                          RouteOut &o);
+                          RouteOut &o, uint32_t blen, uint32_t rflags);
+// client_max_body_size exceeded: 413, nothing proxied, no WAF phase
+__device__ __forceinline__ void too_large(RouteOut &o) {
+    o.action = GM_ACT_TOO_LARGE; o.status = 413; o.ups = GM_NONE; o.waf = GM_WAF_OFF;
+}
 __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const RoutePre &pre,
                           const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb, int32_t rk_in = RK_INLINE,
                           bool *pend = nullptr) {
@@ -816,7 +945,11 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
         if (f.op == SIF_RETURN) hit = true;
         else if (f.op == SIF_FLAGS) hit = (f.tt >> (r.flags & 3)) & 1u;
         else if (f.op == 0xFF) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; return; }
-        else hit = server_if_generic(A, rp, *t.self, S.first_if + i) != 0;
+        else {
+            const int g = server_if_generic(A, rp, *t.self, S.first_if + i, S.realip);
+            if (g < 0) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; return; }
+            hit = g != 0;
+        }
         if (hit) { o.action = is_redirect(f.code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = f.code; return; }
     }
     // ---- location: trie walk (exact, longest prefix, auto_redirect), then regex locations.
@@ -882,7 +1015,14 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
     int32_t loc = -1;
     if (full) {
         if (fexact >= 0) loc = fexact;
-        else if (far >= 0) { o.loc = (uint32_t)far; o.action = GM_ACT_AUTO_301; o.status = 301; return; }
+        else if (far >= 0) {
+            // (the location found is the redirect's target: its client_max_body_size is checked
+            // before the redirect, ngx_http_core_find_config_phase)
+            o.loc = (uint32_t)far;
+            if (!(r.flags & GM_REQ_CHUNKED) && r.body_len > h.locs[far].body_max) too_large(o);
+            else { o.action = GM_ACT_AUTO_301; o.status = 301; }
+            return;
+        }
     }
     if (loc < 0) {
         if (best >= 0 && h.locs[best].noregex) loc = best;
@@ -897,26 +1037,37 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
             if (loc < 0) loc = best;
         }
     }
-    route_loc(A, rp, t, h, loc, o);
+    route_loc(A, rp, t, h, loc, o, r.body_len, r.flags);
 }
 
 // The rest of route_one once the location is known (loc < 0: none): location kinds, rules and
 // split routes, return / proxy.  The regex-location tail pass starts here with k_rloc's answer
 // (or the request's longest prefix match) instead of routing the request again.
+// client_max_body_size: a Content-Length body is checked against the location found (the
+// server's limit when none) before that location's rewrite phase (ngx_http_core_find_config_phase);
+// a chunked body only when it is read -- by the proxying location, the final one after an
+// internal redirect (the chunked body filter)
 __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
-                          RouteOut &o) {
-    if (loc < 0) { o.action = GM_ACT_NOT_FOUND; o.status = 404; return; }
+                          RouteOut &o, uint32_t blen, uint32_t rflags) {
+    const bool chunked = rflags & GM_REQ_CHUNKED;
+    if (loc < 0) {
+        if (!chunked && blen > h.servers[o.server].body_max) { too_large(o); return; }
+        o.action = GM_ACT_NOT_FOUND; o.status = 404; return;
+    }
     o.loc = (uint32_t)loc;
     DLoc L = h.locs[loc];
+    if (!chunked && blen > L.body_max) { too_large(o); return; }
     uint32_t fin = (uint32_t)loc;
     if (L.kind == LK_IRL_RULES) {
         const DRules R = t.rules[L.route];
-        const uint8_t idx = rules_generic(A, rp, *t.self, L.route);
-        o.kind = GM_ROUTE_RULES; o.match = idx;
+        const int idx = rules_generic(A, rp, *t.self, L.route, h.servers[o.server].realip);
+        o.kind = GM_ROUTE_RULES;
+        if (idx < 0) { o.action = GM_ACT_UNSUPPORTED; return; }
+        o.match = (uint8_t)idx;
         fin = idx == 0xFF ? R.default_target : t.rtargets[R.first_target + idx];
     } else if (L.kind == LK_IRL_SPLIT) {
         o.kind = GM_ROUTE_SPLIT;
-        const uint32_t k = split_generic(A, rp, *t.self, L.route);
+        const uint32_t k = split_generic(A, rp, *t.self, L.route, h.servers[o.server].realip);
         if (k == 0xFFFFFFFFu) { o.action = GM_ACT_UNSUPPORTED; return; }
         fin = GM_NONE;
         if (k != 0xFFu) { o.bucket = (uint8_t)k; fin = t.parts[t.splits[L.route].first_part + k].target; }
@@ -931,11 +1082,18 @@ __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, co
     if (L.kind == LK_RETURN) { o.action = is_redirect(L.ret_code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = L.ret_code; return; }
     if (L.kind != LK_PROXY) { o.action = GM_ACT_NOT_FOUND; o.status = 404; return; }
     if (fin == (uint32_t)loc) o.kind = GM_ROUTE_PLAIN;
+    if (chunked && blen > L.body_max) { too_large(o); return; }
     o.action = GM_ACT_PROXY; o.status = 0; o.ups = L.upstream; o.waf = L.waf_mode;
 }
 
 // ============================================================================ kernels
 constexpr int ROUTE_BLOCK = 256;
+// register target (waves per SIMD) of the route beside the WAF scan: the scan's workgroup holds
+// 4 waves per SIMD, and the route's waves share what registers they leave
+#define GM_ROUTE_WPE_SHIPPED 5
+#ifndef GM_ROUTE_WPE
+#define GM_ROUTE_WPE GM_ROUTE_WPE_SHIPPED
+#endif
 // k_route's dynamic LDS: the hot route tables it stages (0 when they exceed ROUTE_STAGE_BYTES),
 // then the per-block location histogram when the generation's locations fit it -- at most
 // LDS_HIST_BESIDE entries beside the WAF scan (2 KiB: a route block fits beside the scan's Bloom
@@ -1019,14 +1177,11 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
             if (loc < 0) loc = q.best[x];
             o.server = e.y; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0; o.action = GM_ACT_NO_LISTENER;
             o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF; o.pend_best = -1;
-            route_loc(A, reqs + i, t, h, loc, o);
+            const uint32_t *rw = reinterpret_cast<const uint32_t *>(reqs + i);   // body_len, flags
+            route_loc(A, reqs + i, t, h, loc, o, rw[5], rw[9] & 0xFF);
         } else {
             r = load_rec(reqs + i);
-#ifdef GM_EXP_ROUTE_NOHOST   // measurement build: no host / URI loads (timing only)
-            for (int k = 0; k < 8; k++) { pre.hw[k] = 0x2E2E2E2Eu + k; pre.uw[k] = 0x2F2F2F2Fu + k; }
-#else
             route_prefetch(A, arena_len, r, pre);
-#endif
             route_one(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
                       RK && q.list ? RK_DEFER : RK_INLINE, &pend);
         }
@@ -1081,11 +1236,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
             hcnt[i] = 0;
             if (i + 1 == n) hcnt[n] = 0;
         }
-#ifdef GM_EXP_ROUTE_NOBLK   // measurement build: no blk2rec writes (timing only)
-        if (false) {
-#else
         if (blk2rec) {
-#endif
             // blocks whose start lies in [base_i, base_{i+1}) belong to record i (base_{i+1}: the
             // next lane's record, which it holds; lane 63 and the last request read it)
             uint64_t b0 = (i == 0) ? 0 : r.base;
@@ -1129,6 +1280,7 @@ struct Generation {
     std::vector<std::string> peer_addrs;   // gm_peer_address
     std::vector<uint32_t> peer_ups;
     std::vector<UpstreamMeta> ups_meta;     // gm_update_upstream
+    std::vector<std::string> rejects;       // gm_rejects
     // gm_update_upstream -> gm_peers_migrate: new peer id -> the previous table's peer id (GM_NONE:
     // a new server), and the previous table's peer count
     uint32_t *d_peer_map = nullptr;
@@ -1212,7 +1364,7 @@ struct gm_ctx {
     int dev = 0;
     uint32_t flags = 0;
     int cu_count = 256;
-    double cap_scale = 1.0;                   // GM_SCRATCH_SCALE (test hook): internal WAF capacities
+    double cap_scale = 1.0;                   // GM_CREATE_SCRATCH_SHIFT (test hook): internal WAF capacities
     std::shared_mutex gen_mu;                 // shared: enqueueing batches; exclusive: the swap
     Generation *gen = nullptr;
     std::mutex scr_mu;                        // the stream -> scratch map only
@@ -1320,10 +1472,7 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
     gm_ctx *c = new gm_ctx();
     c->dev = hip_device;
     c->flags = flags;
-    if (const char *sc = getenv("GM_SCRATCH_SCALE")) {
-        const double v = atof(sc);
-        if (v > 0 && v <= 1) c->cap_scale = v;
-    }
+    if (const uint32_t k = (flags >> 8) & 0xFFu) c->cap_scale = k < 32 ? 1.0 / (double)(1ull << k) : 1.0;
     if (!(flags & GM_CREATE_COMPILE_ONLY)) {
         if (hipSetDevice(hip_device) != hipSuccess) { t_err = "hipSetDevice failed"; delete c; return nullptr; }
         // the WAF scan's Bloom filter is dynamic LDS beyond the 64 KiB default
@@ -1353,7 +1502,7 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
         }
         // the route's hot tables + location histogram (route_lds)
         const void *routes[] = {(const void *)k_route<3, true, true>, (const void *)k_route<3, true>,
-                                (const void *)k_route<3>, (const void *)k_route<5, true>, (const void *)k_route<5>};
+                                (const void *)k_route<3>, (const void *)k_route<GM_ROUTE_WPE, true>, (const void *)k_route<GM_ROUTE_WPE>};
         for (const void *f : routes)
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)(ROUTE_STAGE_BYTES + 4 * LDS_HIST_ALONE)) != hipSuccess) {
@@ -1396,6 +1545,7 @@ static int publish(gm_ctx *c, CompileResult &R, uint32_t gen, bool same_counters
     g->peer_addrs = std::move(R.peer_addrs);
     g->peer_ups = std::move(R.peer_ups);
     g->ups_meta = std::move(R.ups_meta);
+    g->rejects = std::move(R.rejects);
     g->n_counters = g->stats.n_counters;
     if (!(c->flags & GM_CREATE_COMPILE_ONLY)) {
         HIPCHK(c, hipSetDevice(c->dev));
@@ -1459,20 +1609,40 @@ int gm_update_upstream(gm_ctx *c, const char *upstream, const char *const *serve
         if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
         live.image = g->host_image; live.hdr = g->hdr; live.stats = g->stats;
         live.peer_addrs = g->peer_addrs; live.peer_ups = g->peer_ups; live.ups_meta = g->ups_meta;
+        live.rejects = g->rejects;
         gen = g->stats.gen;
     }
     CompileResult R = update_upstream(live, upstream, addrs);
     if (!R.ok) return fail(c, R.code, R.err);
+    R.rejects = live.rejects;
     // (two concurrent updates: the second publishes over the first's tables -- the Manager calls
     // UpdateServersInPlus one upstream at a time, configurator.go:442,467,489)
     return publish(c, R, gen, true);
 }
+
+// The measurement / tuning variants compiled in (gm_stats_t.build_flags): a bench line can show it
+// came from the product build.  Every GM_EXP_* macro is a measurement (timing) variant; the
+// tuning macros count when they differ from the shipped values.
+static constexpr uint32_t kBuildFlags =
+#if defined(GM_EXP_COUNT) || defined(GM_EXP_CMASK) || defined(GM_EXP_ROUTE_AFTER) || defined(GM_EXP_ROUTE_FIRST) || \
+    defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_SCAN_NOBRANCH) || defined(GM_SCAN_VMASK)
+    GM_BUILD_EXPERIMENT |
+#endif
+#if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != 32 || \
+    GM_ROUTE_BPC != 2 || GM_ROUTE_PRIO != 0 || GM_ROUTE_WPE != GM_ROUTE_WPE_SHIPPED || GM_EXP_GRIDMUL != 8 || \
+    GM_EXP_WPE != 3 || GM_RLOC_CTX != 1 || GM_RLOC_PREF != 0 || GM_ALW_SLICE_GROUPS != 8 || GM_WIRE_WPE != 8 || \
+    GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1
+    GM_BUILD_TUNING |
+#endif
+    0u;
 
 int gm_stats(gm_ctx *c, gm_stats_t *out) {
     if (!c || !out) return fail(c, GM_E_INVAL, "null argument");
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
     *out = c->gen->stats;
+    out->build_flags = kBuildFlags;
+    out->scratch_scale = (float)c->cap_scale;
     std::lock_guard<std::mutex> l2(c->last_mu);
     out->last_candidates = c->last_candidates;
     out->last_pairs = c->last_pairs;
@@ -1482,6 +1652,20 @@ int gm_stats(gm_ctx *c, gm_stats_t *out) {
     out->last_ms_route = c->last_ms[0]; out->last_ms_scan = c->last_ms[1];
     out->last_ms_verify = c->last_ms[2]; out->last_ms_tail = c->last_ms[3];
     return GM_OK;
+}
+
+int gm_rejects(gm_ctx *c, char *buf, size_t cap) {
+    if (!c) return fail(c, GM_E_INVAL, "null ctx");
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
+    std::string t;
+    for (const std::string &r : c->gen->rejects) { t += r; t += '\n'; }
+    if (buf && cap) {
+        const size_t k = std::min(cap - 1, t.size());
+        memcpy(buf, t.data(), k);
+        buf[k] = 0;
+    }
+    return (int)std::min<size_t>(t.size(), 0x7FFFFFFF);
 }
 
 // Enqueue one batch on stream s (device pointers).  No host synchronisation: every size a later
@@ -1602,7 +1786,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     // truncated silently
     const uint32_t scan_blocks = (uint32_t)c->cu_count;
     const uint32_t W = scan_blocks * SCAN_WAVES;
-    // (GM_SCRATCH_SCALE, a test hook: scales these defaults, so the overflow continuations run on
+    // (GM_CREATE_SCRATCH_SHIFT, a test hook: scales these defaults, so the overflow continuations run on
     // batches small enough for the oracle)
     const double sc = c->cap_scale;
     auto scaled = [sc](size_t x, size_t lo) { return std::max<size_t>(lo, (size_t)((double)x * sc)); };
@@ -1675,9 +1859,9 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         // raised issue priority beside the scan: the route's short latency-bound waves finish
         // early instead of stretching past the scan
         if (rk)
-            k_route<5, true><<<nb, ROUTE_BLOCK, route_lds(t, !serial), rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial), q);
+            k_route<GM_ROUTE_WPE, true><<<nb, ROUTE_BLOCK, route_lds(t, !serial), rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial), q);
         else
-            k_route<5><<<nb, ROUTE_BLOCK, route_lds(t, !serial), rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial));
+            k_route<GM_ROUTE_WPE><<<nb, ROUTE_BLOCK, route_lds(t, !serial), rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial));
         HIPCHK(c, hipGetLastError());
         int e3;
         if (rk && (e3 = launch_rloc(rs, nb))) return e3;
@@ -1961,6 +2145,15 @@ extern "C" int gm_debug_waf_keys(gm_ctx *c, uint32_t *out, size_t cap) {
     for (uint32_t i = 0; i < h.n_lit_buckets_cap; i++)
         if (b[i].count) { if (k < cap) out[k] = b[i].key; k++; }
     return (int)k;
+}
+
+extern "C" int gm_debug_inet(const uint8_t *text, size_t n, char *out, size_t cap) {
+    InetAddr a;
+    if (!text || !out || n > 0xFFFF || !ngx_parse_addr_port(text, (uint32_t)n, a)) return -1;
+    uint8_t t[48];
+    const uint32_t k = ngx_addr_text(a, t);
+    const int w = snprintf(out, cap, "%.*s %u", (int)k, (const char *)t, a.port);
+    return w;
 }
 
 // The last batch's device status words (gm_waf.inc STATUS_WORDS: counts and profiling counters),

@@ -51,6 +51,31 @@ struct DServer {
     uint32_t sl_first, sl_n;      // small-server location list (DSmallLoc), sl_n = 0: trie walk
     uint32_t rsl_first, rsl_n;    // rk_on servers: union-DFA slices of the regex locations
                                   // (DAlwSlice, config order; rsl_n = 0: the factor prefilter)
+    uint32_t realip;              // DRealIp index (set_real_ip_from ...), GM_NONE: none
+    uint32_t body_max;            // client_max_body_size of the server level (a request that
+                                  // matches no location), BODY_UNLIMITED: none
+};
+// client_max_body_size (version1/nginx.ingress.tmpl:175, version2/nginx.virtualserver.tmpl:93):
+// a body longer than this gets 413; 0 (nginx's "no limit") and limits >= 4 GiB never trigger
+constexpr uint32_t BODY_UNLIMITED = 0xFFFFFFFFu;
+// ngx_http_realip_module (set_real_ip_from / real_ip_header / real_ip_recursive,
+// version1/nginx.ingress.tmpl:46-49, version2/nginx.virtualserver.tmpl:64-72, ConfigMap keys
+// configmaps.go:153-169): the header the client address is taken from, and the trusted proxies
+// RIP_PROXY: real_ip_header proxy_protocol (the PROXY header's address is not in a record);
+// RIP_UNKNOWN: a set_real_ip_from value that is not an address (nginx resolves host names)
+enum : uint32_t { RIP_XREALIP = 1, RIP_XFWD = 2, RIP_PROXY = 3, RIP_HEADER = 4, RIP_UNKNOWN = 5 };
+struct DRealIp {
+    uint32_t type;           // RIP_*
+    uint32_t recursive;      // real_ip_recursive on
+    uint32_t first_cidr, n_cidr;   // DCidr list (set_real_ip_from, config order)
+    uint32_t hdr_off, hdr_len;     // RIP_HEADER: the lowercased header name (bytes pool)
+    uint32_t pad[2];
+};
+struct DCidr {
+    uint32_t family;         // 4 or 6
+    uint32_t addr[4];        // network-order bytes, packed little-endian per dword (masked)
+    uint32_t mask[4];
+    uint32_t pad[3];
 };
 // A server whose location names all fit 16 bytes and whose trie has at most SMALL_LOCS_MAX
 // nodes carrying a location gets those nodes as a flat list: the route compares the URI's
@@ -107,6 +132,9 @@ struct DLoc {
     uint32_t upstream;       // GM_NONE if not a known upstream
     uint32_t ret_code;
     uint32_t route;          // DSplit / DRules index for IRLs
+    uint32_t body_max;       // client_max_body_size in effect here (BODY_UNLIMITED: none, or a
+                             // location whose own identity is uncertain: nested / PCRE-only)
+    uint32_t pad;
 };
 
 // The upstream request URI of a proxying location (§8 f1, nginx.org/rewrites: the URI part of
@@ -330,6 +358,8 @@ struct TabHeader {
     uint64_t off_alw, off_alw_slices, off_alw_pack, off_alw_rule;
     uint64_t off_rsl_pbit;         // u8 per regex location: its prefiltered slice's mask bit (0xFF none)
     uint32_t n_rk_ents_n, pad_rke; // DRlocEnt entries (k_rloc_pref stages them in LDS)
+    uint32_t n_realip, n_cidrs;    // realip configurations and their set_real_ip_from entries
+    uint64_t off_realip, off_cidrs;
 };
 // The route's hot tables -- ports, the three name tables, servers, server ifs, small-location
 // lists, locations and the name strings -- are laid out first and contiguously in the image;
@@ -356,6 +386,7 @@ struct GTab {                // device pointers, built on host from the image ba
     uint32_t decoders;
     const DAlwGroup *alw; const DAlwSlice *alw_slices; const uint8_t *alw_pack; const uint32_t *alw_rule;
     const uint8_t *rsl_pbit;
+    const DRealIp *realip; const DCidr *cidrs;
     uint32_t n_always_lds, n_alw_groups, n_alw_slices, n_rsl, n_rk_prefilter;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;

@@ -69,6 +69,9 @@ def default_config_params() -> dict:
         "Wallarm": None,
         "ServerSnippets": [],
         "LocationSnippets": [],
+        # realip (config_params.go:60-62, ConfigMap set-real-ip-from / real-ip-header /
+        # real-ip-recursive, configmaps.go:153-169)
+        "SetRealIPFrom": [], "RealIPHeader": "", "RealIPRecursive": False,
         "HSTS": False, "HSTSMaxAge": 2592000, "HSTSIncludeSubdomains": False, "HSTSBehindProxy": False,
     }
 
@@ -127,6 +130,11 @@ def _go_atoi(v):
     return int(s) if _GO_INT.fullmatch(s) else None
 
 
+def _string_slice(v, sep):
+    """parsing_helpers.go:80-87 GetMapKeyAsStringSlice: strings.Split(value, sep)."""
+    return str(v).split(sep)
+
+
 def parse_annotations(ing: dict, base: dict) -> dict:
     """annotations.go:57-333, restricted to keys that change the request verdict:
     redirect-to-https (:176-182), ssl-redirect (:184-190), listen ports (:266-273),
@@ -156,6 +164,10 @@ def parse_annotations(ing: dict, base: dict) -> dict:
             p["MaxFails"] = v
     if "nginx.org/fail-timeout" in ann:   # annotations.go:291-293
         p["FailTimeout"] = ann["nginx.org/fail-timeout"]
+    # annotations.go:132-146 (GetMapKeyAsStringSlice with "\n")
+    for key, field in (("nginx.org/server-snippets", "ServerSnippets"), ("nginx.org/location-snippets", "LocationSnippets")):
+        if key in ann:
+            p[field] = _string_slice(ann[key], "\n")
     if "nginx.org/client-max-body-size" in ann:
         p["ClientMaxBodySize"] = ann["nginx.org/client-max-body-size"]
     for key, field in (("nginx.org/listen-ports", "Ports"), ("nginx.org/listen-ports-ssl", "SSLPorts")):
@@ -262,7 +274,8 @@ def _create_location(path, upstream, p, rewrite=""):
     return {"Path": path, "Upstream": upstream, "ProxyConnectTimeout": p["ProxyConnectTimeout"],
             "ProxyReadTimeout": p["ProxyReadTimeout"], "ClientMaxBodySize": p["ClientMaxBodySize"],
             "Rewrite": rewrite, "SSL": False, "GRPC": False, "Websocket": False,
-            "ProxyBuffering": p["ProxyBuffering"], "Wallarm": None, "MinionIngress": None}
+            "ProxyBuffering": p["ProxyBuffering"], "Wallarm": None, "MinionIngress": None,
+            "LocationSnippets": list(p["LocationSnippets"])}
 
 
 def generate_nginx_cfg(ing_ex: dict, pems: dict, is_minion: bool, base: dict) -> dict:
@@ -288,7 +301,10 @@ def generate_nginx_cfg(ing_ex: dict, pems: dict, is_minion: bool, base: dict) ->
                   "StatusZone": host,
                   "Ports": list(p["Ports"]), "SSLPorts": list(p["SSLPorts"]), "Wallarm": p["Wallarm"],
                   "SSL": False, "SSLCertificate": "", "SSLCertificateKey": "", "SSLCiphers": "",
-                  "GRPCOnly": False, "ServerSnippets": list(p["ServerSnippets"])}
+                  "GRPCOnly": False, "ServerSnippets": list(p["ServerSnippets"]),
+                  # ingress.go:100-102
+                  "RealIPHeader": p["RealIPHeader"], "SetRealIPFrom": list(p["SetRealIPFrom"]),
+                  "RealIPRecursive": p["RealIPRecursive"]}
         if host in pems:
             pem = pems[host]
             server.update(SSL=True, SSLCertificate=pem, SSLCertificateKey=pem)
@@ -463,7 +479,8 @@ def _vs_location(path, ups, p):
     """virtualserver.go:231-245 generateLocation."""
     return {"Path": path, "ProxyConnectTimeout": p["ProxyConnectTimeout"],
             "ProxyReadTimeout": p["ProxyReadTimeout"], "ClientMaxBodySize": p["ClientMaxBodySize"],
-            "ProxyBuffering": p["ProxyBuffering"], "ProxyPass": f"http://{ups}"}
+            "ProxyBuffering": p["ProxyBuffering"], "ProxyPass": f"http://{ups}",
+            "Snippets": list(p["LocationSnippets"])}                    # virtualserver.go:231
 
 
 def generate_split_route_config(route, prefix, safe, index, p):
@@ -567,6 +584,9 @@ def generate_virtual_server_config(vs_ex: dict, pem_name: str, base: dict) -> di
             add(r, rpre)
     return {"Upstreams": ups, "SplitClients": splits, "Maps": maps,
             "Server": {"ServerName": spec["host"], "ProxyProtocol": p["ProxyProtocol"],
+                       # virtualserver.go:187-189
+                       "SetRealIPFrom": list(p["SetRealIPFrom"]), "RealIPHeader": p["RealIPHeader"],
+                       "RealIPRecursive": p["RealIPRecursive"],
                        "SSL": generate_ssl_config(spec.get("tls"), pem_name, p),
                        "RedirectToHTTPSBasedOnXForwarderProto": p["RedirectToHTTPS"],
                        "ServerTokens": p["ServerTokens"], "Snippets": list(p["ServerSnippets"]),
@@ -890,6 +910,12 @@ def render_ingress(cfg: dict) -> str:
             L.append(f"\tssl_certificate_key {s['SSLCertificateKey']};")
             if s.get("SSLCiphers"):
                 L.append(f"\tssl_ciphers {s['SSLCiphers']};")
+        for cidr in s.get("SetRealIPFrom") or []:                 # nginx.ingress.tmpl:46-49
+            L.append(f"\tset_real_ip_from {cidr};")
+        if s.get("RealIPHeader"):
+            L.append(f"\treal_ip_header {s['RealIPHeader']};")
+        if s.get("RealIPRecursive"):
+            L.append("\treal_ip_recursive on;")
         L.append(f"\tserver_tokens {s['ServerTokens']};")
         L.append(f"\tserver_name {s['Name']};")
         if s["SSL"] and s["SSLRedirect"]:
@@ -907,6 +933,8 @@ def render_ingress(cfg: dict) -> str:
             L.append("\t\tproxy_http_version 1.1;")
             if cfg.get("Keepalive"):
                 L.append('\t\tproxy_set_header Connection "";')
+            for v in loc.get("LocationSnippets") or []:                # nginx.ingress.tmpl:168-171
+                L.append("\t\t" + v)
             L.append(f"\t\tproxy_connect_timeout {loc['ProxyConnectTimeout']};")
             L.append(f"\t\tproxy_read_timeout {loc['ProxyReadTimeout']};")
             L.append(f"\t\tclient_max_body_size {loc['ClientMaxBodySize']};")
@@ -963,6 +991,12 @@ def render_virtual_server(cfg: dict) -> str:
     if s["RedirectToHTTPSBasedOnXForwarderProto"]:
         L += ["    if ($http_x_forwarded_proto = 'http') {", "        return 301 https://$host$request_uri;", "    }"]
     L.append(f'    server_tokens "{s["ServerTokens"]}";')
+    for cidr in s.get("SetRealIPFrom") or []:                      # nginx.virtualserver.tmpl:64-72
+        L.append(f"    set_real_ip_from {cidr};")
+    if s.get("RealIPHeader"):
+        L.append(f"    real_ip_header {s['RealIPHeader']};")
+    if s.get("RealIPRecursive"):
+        L.append("    real_ip_recursive on;")
     for v in s.get("Snippets") or []:
         L.append("    " + v)
     for irl in s["InternalRedirectLocations"]:
@@ -970,6 +1004,8 @@ def render_virtual_server(cfg: dict) -> str:
               "        return 418;", "    }"]
     for loc in s["Locations"]:
         L.append(f"    location {loc['Path']} {{")
+        for v in loc.get("Snippets") or []:                           # nginx.virtualserver.tmpl:87-89
+            L.append("        " + v)
         L.append(f"        proxy_connect_timeout {loc['ProxyConnectTimeout']};")
         L.append(f"        proxy_read_timeout {loc['ProxyReadTimeout']};")
         L.append(f"        client_max_body_size {loc['ClientMaxBodySize']};")

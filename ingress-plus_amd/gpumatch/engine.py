@@ -18,13 +18,16 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GM_LIB") or os.path.join(os.path.dirname(HERE), "libgpumatch.so")
 
 GM_OK = 0
-GM_ABI_VERSION = 6   # include/gpumatch.h
+GM_ABI_VERSION = 7   # include/gpumatch.h
 GM_E_OVERFLOW = -4
 GM_CREATE_COMPILE_ONLY = 0x1
 GM_BATCH_HOST = 0x1
 
 ACT = {0: "PROXY", 1: "REDIRECT", 2: "RETURN", 3: "AUTO_301", 4: "NOT_FOUND", 5: "BAD_REQUEST", 6: "BLOCK",
-       7: "ERRPAGE", 8: "UNSUPPORTED", 9: "NO_LISTENER"}
+       7: "ERRPAGE", 8: "UNSUPPORTED", 9: "NO_LISTENER", 10: "TOO_LARGE"}
+GM_ACT_TOO_LARGE = 10
+GM_REQ_CHUNKED = 0x10
+GM_BUILD_EXPERIMENT, GM_BUILD_TUNING = 0x1, 0x2
 
 STATS_FIELDS = ["gen", "n_servers", "n_locations", "n_upstreams", "n_routes_rules", "n_routes_split", "n_sigs",
                 "n_sig_literals", "n_sig_regex", "n_sig_regex_always", "n_rejected_pcre", "n_rejected_other",
@@ -35,15 +38,22 @@ STATS_FIELDS64 = ["table_bytes", "lds_bytes_scan", "last_candidates", "last_pair
 STATS_FIELDS_MS = ["last_ms_route", "last_ms_scan", "last_ms_verify", "last_ms_tail"]
 STATS_FIELDS_WAF = ["n_waf_keys", "bloom_pk", "bloom_fp_ppm", "last_ctx_pass", "last_jobs", "n_peers",
                     "n_upstreams_deferred", "decoders", "n_alw_groups", "n_alw_states", "n_alw_slices",
-                    "n_alw_single", "n_rsl_slices", "n_rk_prefilter", "n_rsl_reversed", "n_rsl_pref"]
+                    "n_alw_single", "n_rsl_slices", "n_rk_prefilter", "n_rsl_reversed", "n_rsl_pref",
+                    "n_realip", "build_flags"]
 GM_CREATE_PROFILE = 0x2
 GM_CREATE_SERIAL = 0x4
+
+
+def GM_CREATE_SCRATCH_SHIFT(k: int) -> int:
+    """Test hook: the internal WAF buffers at 2^-k of their default capacity (include/gpumatch.h)."""
+    return (k & 0xFF) << 8
 
 
 class GmStats(ctypes.Structure):
     _fields_ = ([(f, ctypes.c_uint32) for f in STATS_FIELDS] + [(f, ctypes.c_uint64) for f in STATS_FIELDS64] +
                 [(f, ctypes.c_float) for f in STATS_FIELDS_MS] +
-                [(f, ctypes.c_uint32) for f in STATS_FIELDS_WAF])
+                [(f, ctypes.c_uint32) for f in STATS_FIELDS_WAF] +
+                [("scratch_scale", ctypes.c_float), ("reserved_stats", ctypes.c_uint32 * 5)])
 
 
 class GmBatch(ctypes.Structure):
@@ -55,7 +65,7 @@ EXPORTS = ["gm_create", "gm_destroy", "gm_abi_version", "gm_load_generation", "g
            "gm_counters", "gm_counters_reset", "gm_comm_unique_id", "gm_comm_init", "gm_counters_allreduce",
            "gm_stats", "gm_last_error", "gm_normalize_uris", "gm_counters_global", "gm_parse_requests",
            "gm_peers_init", "gm_select_peers", "gm_release_peers", "gm_peer_address", "gm_upstream_uris",
-           "gm_update_upstream", "gm_peers_migrate"]
+           "gm_update_upstream", "gm_peers_migrate", "gm_rejects"]
 
 # gm_peer_state (include/gpumatch.h)
 PEER_STATE_DTYPE = np.dtype([("conns", "<u4"), ("current_weight", "<i4"), ("flags", "<u4"), ("reserved", "<u4")])
@@ -107,6 +117,7 @@ def lib():
                                       ctypes.c_void_p]
         L.gm_upstream_uris.argtypes = [ctypes.c_void_p, ctypes.POINTER(GmBatch), ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.gm_rejects.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
         L.gm_last_error.restype = ctypes.c_char_p
         L.gm_last_error.argtypes = [ctypes.c_void_p]
         _lib = L
@@ -122,10 +133,11 @@ class GmError(RuntimeError):
 class Engine:
     """One context per HIP device (one process per GPU)."""
 
-    def __init__(self, device: int = 0, compile_only: bool = False, profile: bool = False, serial: bool = False):
+    def __init__(self, device: int = 0, compile_only: bool = False, profile: bool = False, serial: bool = False,
+                 scratch_shift: int = 0):
         L = lib()
         fl = (GM_CREATE_COMPILE_ONLY if compile_only else 0) | (GM_CREATE_PROFILE if profile else 0) | \
-             (GM_CREATE_SERIAL if serial else 0)
+             (GM_CREATE_SERIAL if serial else 0) | GM_CREATE_SCRATCH_SHIFT(scratch_shift)
         self.h = L.gm_create(device, fl)
         if not self.h:
             raise GmError(-1, L.gm_last_error(None).decode())
@@ -153,7 +165,18 @@ class Engine:
     def stats(self) -> dict:
         s = GmStats()
         self._chk(lib().gm_stats(self.h, ctypes.byref(s)))
-        return {f: getattr(s, f) for f in STATS_FIELDS + STATS_FIELDS64 + STATS_FIELDS_MS + STATS_FIELDS_WAF}
+        d = {f: getattr(s, f) for f in STATS_FIELDS + STATS_FIELDS64 + STATS_FIELDS_MS + STATS_FIELDS_WAF}
+        d["scratch_scale"] = s.scratch_scale
+        return d
+
+    def rejects(self) -> list:
+        """gm_rejects: the live generation's rejected constructs ("context: directive ...")."""
+        n = lib().gm_rejects(self.h, None, 0)
+        if n < 0:
+            self._chk(n)
+        buf = ctypes.create_string_buffer(n + 1)
+        lib().gm_rejects(self.h, buf, n + 1)
+        return [x for x in buf.value.decode().split("\n") if x]
 
     def match_ptr(self, reqs_ptr, arena_ptr, arena_len, n, out_ptr, hits_ptr, hit_cap, stream=0, host=False,
                   arena_len_dev=None):

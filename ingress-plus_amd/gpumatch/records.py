@@ -27,7 +27,7 @@ assert REQ_DTYPE.itemsize == 64
 LEN_FIELD = {"uri": "uri_len", "args": "args_len", "hdrs": "hdr_len", "body": "body_len",
              "host": "host_len", "method": "method_len", "ruri": "ruri_len", "raddr": "raddr_len"}
 
-REQ_HTTPS, REQ_HTTP2, REQ_HTTP10, REQ_INVALID = 0x01, 0x02, 0x04, 0x08
+REQ_HTTPS, REQ_HTTP2, REQ_HTTP10, REQ_INVALID, REQ_CHUNKED = 0x01, 0x02, 0x04, 0x08, 0x10
 
 VERDICT_DTYPE = np.dtype([
     ("gen", "<u4"), ("server_id", "<u4"), ("location_id", "<u4"), ("upstream_id", "<u4"),
@@ -147,7 +147,8 @@ def field_bytes(reqs, arena, i: int, name: str) -> bytes:
 
 def from_dicts(items: list[dict]):
     """Build a batch from explicit requests (KAT fixtures).  Keys: host, method, uri, args,
-    headers (list of (name, value)), body, https, http2, port, rid (bytes16/hex), raddr, ruri."""
+    headers (list of (name, value)), body, https, http2, chunked, port, rid (bytes16/hex), raddr,
+    ruri, remote_port."""
     n = len(items)
     cols = {f: [] for f in FIELDS}
     ports, flags, rids, rports = [], [], [], []
@@ -167,7 +168,7 @@ def from_dicts(items: list[dict]):
         https = bool(it.get("https", False))
         ports.append(int(it.get("port", 443 if https else 80)))
         fl = (REQ_HTTPS if https else 0) | (REQ_HTTP2 if it.get("http2") else 0) | \
-             (REQ_HTTP10 if it.get("http10") else 0)
+             (REQ_HTTP10 if it.get("http10") else 0) | (REQ_CHUNKED if it.get("chunked") else 0)
         flags.append(fl)
         rid = it.get("rid", bytes(16))
         if isinstance(rid, str):

@@ -168,13 +168,30 @@ typedef struct {
     int waf_mode;
     int pcre_only;            /* regex location the engine rejects (orc_pcre_only) */
     int nested;               /* contains location / if / rewrite: deferred (GM_ACT_UNSUPPORTED) */
+    int unknown;              /* a directive outside the neutral set (default-deny): deferred */
+    char *cmbs;               /* client_max_body_size written here, NULL: inherited */
+    int64_t body_max;         /* the limit in effect (-1: none), set once the server is known */
     pcre *relaxed;            /* its superset pattern (orc_relax), NULL = none */
 } loc_t;
 
 typedef struct { char *var; int op; char *val; pcre *re; int code; char *text; int is_return_only; int unsupported; } sif_t;
 
+/* ngx_http_realip_module settings (set_real_ip_from / real_ip_header / real_ip_recursive) */
+typedef struct { uint8_t fam; uint8_t addr[16], mask[16]; } ocidr_t;
+typedef struct {
+    int nfrom; char **from;    /* NULL (nfrom 0) = unset */
+    char *header;              /* NULL = unset */
+    int recursive;             /* -1 unset */
+} orip_t;
+
 typedef struct {
     int id; int nports; int ports[16]; int ssl[16]; int def[16];
+    char *cmbs;               /* server-level client_max_body_size, NULL inherited */
+    int64_t body_max;         /* limit in effect for a request with no location (-1 none) */
+    orip_t rip;
+    /* realip in effect: type 0 none, 1 X-Real-IP, 2 X-Forwarded-For, 3 proxy_protocol, 4 other
+     * header (hdr lowercase), 5 unknowable (a set_real_ip_from that is no address) */
+    int rtype, rrec; char hdr[128]; int ncidr; ocidr_t *cidr;
     int pd_mask;              /* server-level wallarm_parser_disable */
     int nnames; char **names; int *nlen; pcre **nre;
     int nifs; sif_t *ifs;
@@ -216,6 +233,7 @@ typedef struct orc_ctx {
     split_t *spl; int nspl;
     char **ups; int nups;
     int http_waf;
+    char *http_cmbs; orip_t http_rip; int http_unknown;
     sig_t *sig; int nsig;
     int decoders;             /* the signature set's "@decoders" (DEC bits) */
     /* CPU-baseline engine (orc_set_prefilter): a regex runs on a zone only if its required factor
@@ -337,10 +355,247 @@ char *orc_relax(const char *p) {
 
 static int cmp_str(const void *a, const void *b) { return strcmp(*(char *const *)a, *(char *const *)b); }
 
+/* ------------------------------------------------------------------ default-deny
+ * The engine's contract (gm_compile.cpp neutral_directive), restated: the directives known to
+ * leave a request's verdict alone.  Any other directive in a server or location (snippets) makes
+ * the requests reaching it GM_ACT_UNSUPPORTED; at http level it defers every server's requests
+ * after their server rewrite phase. */
+static int orc_neutral(const char *n, int ctx /* 0 http, 1 server, 2 location */) {
+    static const char *pre[] = {"proxy_", "grpc_", "ssl_", "gzip", "http2_", "open_file_cache", "sub_filter",
+                                "keepalive_", "wallarm_", NULL};
+    static const char *any[] = {
+        "add_header", "add_trailer", "access_log", "error_log", "log_not_found", "log_subrequest",
+        "default_type", "charset", "charset_types", "source_charset", "override_charset", "expires", "etag",
+        "send_timeout", "client_body_timeout", "client_body_buffer_size", "client_body_temp_path",
+        "client_header_timeout", "sendfile", "sendfile_max_chunk", "tcp_nodelay", "tcp_nopush",
+        "server_tokens", "status_zone", "chunked_transfer_encoding", "output_buffers", "postpone_output",
+        "lingering_close", "lingering_time", "lingering_timeout", "reset_timedout_connection", "resolver",
+        "resolver_timeout", "auth_jwt_key_file", "auth_jwt_leeway", "port_in_redirect",
+        "server_name_in_redirect", "absolute_redirect", "msie_padding", "msie_refresh", NULL};
+    static const char *http[] = {
+        "log_format", "server_names_hash_max_size", "server_names_hash_bucket_size", "variables_hash_max_size",
+        "variables_hash_bucket_size", "types_hash_max_size", "types_hash_bucket_size", "map_hash_max_size",
+        "map_hash_bucket_size", "limit_req_zone", "limit_conn_zone", "proxy_cache_path", "geo", "match",
+        "js_include", "js_import", "keyval_zone", "types", NULL};
+    for (int i = 0; pre[i]; i++) if (!strncmp(n, pre[i], strlen(pre[i]))) return 1;
+    for (int i = 0; any[i]; i++) if (!strcmp(n, any[i])) return 1;
+    if (ctx == 2) return !strcmp(n, "health_check");
+    if (ctx == 0) for (int i = 0; http[i]; i++) if (!strcmp(n, http[i])) return 1;
+    return 0;
+}
+
+/* client_max_body_size (ngx_parse_offset): digits + optional k/m/g; 0 = unlimited (-1 here);
+ * -2 = not a size */
+static int64_t orc_size(const char *v) {
+    int n = (int)strlen(v);
+    if (n == 0) return -2;
+    int64_t scale = 1;
+    char u = v[n - 1];
+    if (u == 'k' || u == 'K') { scale = 1024; n--; }
+    else if (u == 'm' || u == 'M') { scale = 1 << 20; n--; }
+    else if (u == 'g' || u == 'G') { scale = 1 << 30; n--; }
+    if (n == 0) return -2;
+    int64_t x = 0;
+    for (int i = 0; i < n; i++) {
+        if (!isdigit((unsigned char)v[i])) return -2;
+        if (x < ((int64_t)1 << 50)) x = x * 10 + (v[i] - '0');
+    }
+    if (x >= ((int64_t)1 << 50)) return -1;
+    x *= scale;
+    return x == 0 ? -1 : x;
+}
+
+/* ------------------------------------------------------------------ addresses (nginx 1.17.3)
+ * ngx_inet_addr, ngx_inet6_addr, ngx_parse_addr[_port], ngx_ptocidr, ngx_cidr_match,
+ * ngx_inet6_ntop -- restated from nginx's behaviour for the realip module. */
+static int o_inet4(const char *t, int n, uint8_t *out) {
+    uint32_t a = 0, oct = 0; int dots = 0;
+    for (const char *p = t; p < t + n; p++) {
+        if (*p >= '0' && *p <= '9') { oct = oct * 10 + (uint32_t)(*p - '0'); if (oct > 255) return 0; }
+        else if (*p == '.') { a = (a << 8) + oct; oct = 0; dots++; }
+        else return 0;
+    }
+    if (dots != 3) return 0;
+    a = (a << 8) + oct;
+    if (a == 0xFFFFFFFFu) return 0;        /* INADDR_NONE */
+    out[0] = a >> 24; out[1] = a >> 16; out[2] = a >> 8; out[3] = a;
+    return 1;
+}
+static int o_inet6(const char *p, int len, uint8_t *addr) {
+    if (len == 0) return 0;
+    uint8_t *zero = NULL, *a0 = addr;
+    const char *digit = NULL; int len4 = 0, nibbles = 0, n = 8; unsigned word = 0;
+    if (p[0] == ':') { p++; len--; }
+    for (; len; len--) {
+        char c = *p++;
+        if (c == ':') {
+            if (nibbles) {
+                digit = p; len4 = len;
+                *addr++ = (uint8_t)(word >> 8); *addr++ = (uint8_t)word;
+                if (--n) { nibbles = 0; word = 0; continue; }
+            } else if (zero == NULL) { digit = p; len4 = len; zero = addr; continue; }
+            return 0;
+        }
+        if (c == '.' && nibbles) {
+            uint8_t v4[4];
+            if (n < 2 || digit == NULL || !o_inet4(digit, len4 - 1, v4)) return 0;
+            *addr++ = v4[0]; *addr++ = v4[1];
+            word = (unsigned)v4[2] << 8 | v4[3];
+            n--;
+            break;
+        }
+        if (++nibbles > 4) return 0;
+        if (c >= '0' && c <= '9') { word = word * 16 + (unsigned)(c - '0'); continue; }
+        c |= 0x20;
+        if (c >= 'a' && c <= 'f') { word = word * 16 + (unsigned)(c - 'a') + 10; continue; }
+        return 0;
+    }
+    if (nibbles == 0 && zero == NULL) return 0;
+    *addr++ = (uint8_t)(word >> 8); *addr++ = (uint8_t)word;
+    if (--n) {
+        if (zero) {
+            n *= 2;
+            uint8_t *s = addr - 1, *d = s + n;
+            while (s >= zero) *d-- = *s--;
+            memset(zero, 0, (size_t)n);
+            return 1;
+        }
+    } else if (zero == NULL) return 1;
+    (void)a0;
+    return 0;
+}
+typedef struct { int fam; uint8_t b[16]; int port; } oaddr_t;
+static int o_parse_addr(const char *t, int n, oaddr_t *a) {
+    a->port = 0;
+    if (o_inet4(t, n, a->b)) { a->fam = 4; return 1; }
+    if (o_inet6(t, n, a->b)) { a->fam = 6; return 1; }
+    return 0;
+}
+static int o_parse_addr_port(const char *text, int len, oaddr_t *a) {
+    if (o_parse_addr(text, len, a)) return 1;
+    const char *last = text + len, *p;
+    if (len && text[0] == '[') {
+        p = memchr(text, ']', (size_t)len);
+        if (p == NULL || p == last - 1 || *++p != ':') return 0;
+        text++; len -= 2;
+    } else {
+        p = memchr(text, ':', (size_t)len);
+        if (p == NULL) return 0;
+    }
+    p++;
+    int plen = (int)(last - p);
+    if (plen <= 0 || plen > 9) return 0;
+    long port = 0;
+    for (int i = 0; i < plen; i++) { if (!isdigit((unsigned char)p[i])) return 0; port = port * 10 + (p[i] - '0'); }
+    if (port < 1 || port > 65535) return 0;
+    len -= plen + 1;
+    if (!o_parse_addr(text, len, a)) return 0;
+    a->port = (int)port;
+    return 1;
+}
+static int o_ptocidr(const char *t, ocidr_t *c) {
+    const char *sl = strchr(t, '/');
+    int alen = sl ? (int)(sl - t) : (int)strlen(t);
+    oaddr_t a;
+    memset(c, 0, sizeof *c);
+    if (!o_parse_addr(t, alen, &a)) return 0;
+    int nb = a.fam == 4 ? 4 : 16, bits = nb * 8;
+    if (sl) {
+        const char *q = sl + 1;
+        if (!*q) return 0;
+        bits = 0;
+        for (; *q; q++) { if (!isdigit((unsigned char)*q)) return 0; bits = bits * 10 + (*q - '0'); if (bits > 1000) return 0; }
+        if (bits > nb * 8) return 0;
+    }
+    c->fam = (uint8_t)a.fam;
+    for (int i = 0; i < nb; i++) {
+        int k = bits - 8 * i;
+        c->mask[i] = k >= 8 ? 0xFF : k <= 0 ? 0 : (uint8_t)(0xFF << (8 - k));
+        c->addr[i] = a.b[i] & c->mask[i];
+    }
+    return 1;
+}
+static int o_cidr_match(const srv_t *S, const oaddr_t *a) {
+    int fam = a->fam; const uint8_t *b = a->b;
+    static const uint8_t mapped[12] = {0,0,0,0,0,0,0,0,0,0,0xFF,0xFF};
+    if (fam == 6 && !memcmp(b, mapped, 12)) { fam = 4; b += 12; }
+    for (int i = 0; i < S->ncidr; i++) {
+        const ocidr_t *c = &S->cidr[i];
+        if (c->fam != fam) continue;
+        int ok = 1;
+        for (int k = 0; k < (fam == 4 ? 4 : 16) && ok; k++) ok = (b[k] & c->mask[k]) == c->addr[k];
+        if (ok) return 1;
+    }
+    return 0;
+}
+static int o_ntop(const oaddr_t *a, char *out) {
+    if (a->fam == 4) return sprintf(out, "%u.%u.%u.%u", a->b[0], a->b[1], a->b[2], a->b[3]);
+    const uint8_t *p = a->b;
+    int zero = -1, last = -1, max = 1, n = 0;
+    for (int i = 0; i < 16; i += 2) {
+        if (p[i] || p[i + 1]) { if (max < n) { zero = last; max = n; } n = 0; continue; }
+        if (n++ == 0) last = i;
+    }
+    if (max < n) { zero = last; max = n; }
+    char *d = out;
+    n = 16;
+    if (zero == 0) {
+        if ((max == 5 && p[10] == 0xff && p[11] == 0xff) || max == 6 || (max == 7 && p[14] != 0 && p[15] != 1)) n = 12;
+        *d++ = ':';
+    }
+    for (int i = 0; i < n; i += 2) {
+        if (i == zero) { *d++ = ':'; i += (max - 1) * 2; continue; }
+        d += sprintf(d, "%x", p[i] * 256 + p[i + 1]);
+        if (i < 14) *d++ = ':';
+    }
+    if (n == 12) d += sprintf(d, "%u.%u.%u.%u", p[12], p[13], p[14], p[15]);
+    *d = 0;
+    return (int)(d - out);
+}
+/* test export: ngx_parse_addr_port + ngx_sock_ntop of a text -> "<text> <port>", -1 not an address */
+int orc_inet(const char *t, int n, char *out, int cap) {
+    oaddr_t a;
+    if (!o_parse_addr_port(t, n, &a)) return -1;
+    char x[64];
+    o_ntop(&a, x);
+    return snprintf(out, (size_t)cap, "%s %d", x, a.port);
+}
+
+/* ngx_http_get_forwarded_addr_internal, recursive as in nginx: 0 declined, 1 ok, 2 done */
+static int o_fwd_internal(const srv_t *S, oaddr_t *addr, const char *xff, int xfflen) {
+    if (!o_cidr_match(S, addr)) return 0;
+    if (xfflen <= 0) return 0;     /* nginx reads the byte before an empty value: never an address */
+    const char *p;
+    for (p = xff + xfflen - 1; p > xff; p--, xfflen--) if (*p != ' ' && *p != ',') break;
+    for (; p > xff; p--) if (*p == ' ' || *p == ',') { p++; break; }
+    oaddr_t pa;
+    if (!o_parse_addr_port(p, xfflen - (int)(p - xff), &pa)) return 0;
+    *addr = pa;
+    if (S->rrec && p > xff) {
+        int rc = o_fwd_internal(S, addr, xff, (int)(p - 1 - xff));
+        return rc == 0 ? 2 : rc;
+    }
+    return 1;
+}
+
 /* ------------------------------------------------------------------ build from directives */
 typedef struct { orc_ctx *c; dir_t **confd; int nconfd; } build_t;
 
 static void add_server(build_t *B, dir_t *s, int http_waf);
+
+/* set_real_ip_from / real_ip_header / real_ip_recursive into R; 0 if d is none of them */
+static int orc_realip_dir(orip_t *R, dir_t *d) {
+    const char *n = d->args[0];
+    if (d->nargs != 2) return 0;
+    if (!strcmp(n, "set_real_ip_from")) {
+        R->from = realloc(R->from, sizeof(char *) * (R->nfrom + 1));
+        R->from[R->nfrom++] = strdup(d->args[1]);
+        return 1;
+    }
+    if (!strcmp(n, "real_ip_header")) { R->header = strdup(d->args[1]); return 1; }
+    if (!strcmp(n, "real_ip_recursive")) { R->recursive = !strcmp(d->args[1], "on"); return 1; }
+    return 0;
+}
 
 static void walk_http(build_t *B, dir_t *h) {
     orc_ctx *c = B->c;
@@ -350,6 +605,12 @@ static void walk_http(build_t *B, dir_t *h) {
         const char *n = d->args[0];
         if (!strcmp(n, "include") && d->nargs == 2 && strstr(d->args[1], "conf.d/")) {
             for (int k = 0; k < B->nconfd; k++) walk_http(B, B->confd[k]);
+        } else if (!strcmp(n, "include") && d->nargs == 2 &&
+                   (!strcmp(d->args[1], "/etc/nginx/mime.types") || !strcmp(d->args[1], "mime.types") ||
+                    !strcmp(d->args[1], "/etc/nginx/config-version.conf"))) {
+        } else if (!strcmp(n, "client_max_body_size") && d->nargs == 2) {
+            c->http_cmbs = strdup(d->args[1]);
+        } else if (orc_realip_dir(&c->http_rip, d)) {
         } else if (!strcmp(n, "wallarm_mode") && d->nargs == 2) {
             c->http_waf = waf_mode_of(d->args[1]);
         } else if (!strcmp(n, "upstream") && d->nargs == 2 && d->block) {
@@ -411,6 +672,9 @@ static void walk_http(build_t *B, dir_t *h) {
             c->spl = realloc(c->spl, sizeof(split_t) * (c->nspl + 1)); c->spl[c->nspl++] = s;
         } else if (!strcmp(n, "server") && d->block) {
             add_server(B, d, c->http_waf);
+        } else if (!(!strcmp(n, "map") || !strcmp(n, "split_clients") || !strcmp(n, "upstream")) &&
+                   !orc_neutral(n, 0)) {
+            c->http_unknown = 1;
         }
     }
 }
@@ -462,6 +726,14 @@ static void add_location(build_t *B, srv_t *S, dir_t *d, int srv_waf) {
             L.pd_mask |= dec_bit(k->args[1]); L.has_pd = 1;
         } else if (!strcmp(k->args[0], "location") || !strcmp(k->args[0], "if") || !strcmp(k->args[0], "rewrite")) {
             L.nested = 1;   /* nested location / if / rewrite: outside the restated subset */
+        } else if (!strcmp(k->args[0], "client_max_body_size") && k->nargs == 2) {
+            L.cmbs = strdup(k->args[1]);
+        } else if (!strcmp(k->args[0], "error_page") && k->nargs >= 3 &&
+                   !strncmp(k->args[k->nargs - 1], "@grpcerror", 10)) {
+            /* gRPC error pages: a named location answering the same status */
+        } else if (!strcmp(k->args[0], "auth_jwt") && k->nargs == 2 && !strcmp(k->args[1], "off")) {
+        } else if (!orc_neutral(k->args[0], 2)) {
+            L.unknown = 1;
         }
     }
     if (L.has_proxy && L.plen && L.path[L.plen - 1] == '/' && (L.kind == LK_PREFIX || L.kind == LK_EXACT ||
@@ -475,6 +747,7 @@ static void add_server(build_t *B, dir_t *s, int http_waf) {
     orc_ctx *c = B->c;
     srv_t S; memset(&S, 0, sizeof S);
     S.id = c->nsrv; S.waf_mode = http_waf;
+    S.rip.recursive = -1;
     for (int i = 0; i < s->nkids; i++) {
         dir_t *d = &s->kids[i];
         if (d->nargs == 2 && !strcmp(d->args[0], "wallarm_mode")) S.waf_mode = waf_mode_of(d->args[1]);
@@ -527,13 +800,20 @@ static void add_server(build_t *B, dir_t *s, int http_waf) {
                 else if (!strcmp(op, "!~")) { f.op = 4; f.re = re_compile(f.val, 0); }
                 else if (!strcmp(op, "!~*")) { f.op = 4; f.re = re_compile(f.val, 1); }
             }
-            int has_ret = 0;
+            int has_ret = 0, other = 0;
             for (int k = 0; k < d->nkids; k++) {
                 dir_t *r = &d->kids[k];
                 if (r->nargs >= 2 && !strcmp(r->args[0], "return")) {
                     has_ret = 1;
                     if (isdigit((unsigned char)r->args[1][0])) f.code = atoi(r->args[1]); else f.code = 302;
+                } else if (!(r->nargs >= 2 && !strcmp(r->args[0], "set") && !strcmp(r->args[1], "$hsts_header_val"))) {
+                    other = 1;
                 }
+            }
+            if (other) {   /* an `if` doing more than return / the HSTS header value: deferred here */
+                memset(&f, 0, sizeof f); f.unsupported = 1;
+                S.ifs = realloc(S.ifs, sizeof(sif_t) * (S.nifs + 1)); S.ifs[S.nifs++] = f;
+                continue;
             }
             if (!has_ret) continue;   /* e.g. HSTS `if` only sets a header variable */
             S.ifs = realloc(S.ifs, sizeof(sif_t) * (S.nifs + 1)); S.ifs[S.nifs++] = f;
@@ -548,6 +828,18 @@ static void add_server(build_t *B, dir_t *s, int http_waf) {
             S.ifs = realloc(S.ifs, sizeof(sif_t) * (S.nifs + 1)); S.ifs[S.nifs++] = f;
         } else if (!strcmp(n, "location") && d->block) {
             add_location(B, &S, d, S.waf_mode);
+        } else if (!strcmp(n, "client_max_body_size") && d->nargs == 2) {
+            S.cmbs = strdup(d->args[1]);
+        } else if (orc_realip_dir(&S.rip, d)) {
+        } else if ((!strcmp(n, "set") && d->nargs >= 2 && !strcmp(d->args[1], "$hsts_header_val")) ||
+                   (!strcmp(n, "error_page") && d->nargs >= 3 && !strncmp(d->args[d->nargs - 1], "@grpcerror", 10)) ||
+                   (!strcmp(n, "auth_jwt") && d->nargs == 2 && !strcmp(d->args[1], "off")) ||
+                   !strcmp(n, "server_name") || !strcmp(n, "listen") || orc_neutral(n, 1)) {
+        } else {
+            /* any other directive (server snippets): deferred at its place in the server's
+             * rewrite-phase order */
+            sif_t f; memset(&f, 0, sizeof f); f.unsupported = 1;
+            S.ifs = realloc(S.ifs, sizeof(sif_t) * (S.nifs + 1)); S.ifs[S.nifs++] = f;
         }
     }
     c->srv[S.id] = S;
@@ -980,6 +1272,49 @@ orc_ctx *orc_create(const void *blob, size_t len, uint32_t gen) {
         char **hit = bsearch(&key, c->ups, c->nups, sizeof(char *), cmp_str);
         L->upstream_id = hit ? (int)(hit - c->ups) : -1;
     }
+    /* limits and realip in effect per server / location (nginx's merge of http -> server ->
+     * location settings) */
+    for (int si = 0; si < c->nsrv; si++) {
+        srv_t *S = &c->srv[si];
+        const char *sv_size = S->cmbs ? S->cmbs : c->http_cmbs ? c->http_cmbs : "1m";
+        int64_t x = orc_size(sv_size);
+        S->body_max = x == -2 ? -1 : x;
+        if (x == -2) {   /* not a size: the whole server defers */
+            S->ifs = realloc(S->ifs, sizeof(sif_t) * (S->nifs + 1));
+            memmove(S->ifs + 1, S->ifs, sizeof(sif_t) * S->nifs);
+            memset(&S->ifs[0], 0, sizeof(sif_t)); S->ifs[0].unsupported = 1; S->nifs++;
+        }
+        for (int k = 0; k < S->nlocs; k++) {
+            loc_t *L = &c->loc[S->locs[k]];
+            int64_t y = orc_size(L->cmbs ? L->cmbs : sv_size);
+            if (y == -2) { L->unknown = 1; y = -1; }
+            L->body_max = (L->nested || L->pcre_only) ? -1 : y;
+        }
+        if (c->http_unknown) {
+            S->ifs = realloc(S->ifs, sizeof(sif_t) * (S->nifs + 1));
+            memset(&S->ifs[S->nifs], 0, sizeof(sif_t)); S->ifs[S->nifs].unsupported = 1; S->nifs++;
+        }
+        const orip_t *a = &S->rip, *h = &c->http_rip;
+        const orip_t *fr = a->nfrom ? a : h;
+        if (fr->nfrom) {
+            const char *hd = a->header ? a->header : h->header ? h->header : "X-Real-IP";
+            S->rrec = a->recursive >= 0 ? a->recursive : h->recursive >= 0 ? h->recursive : 0;
+            if (!strcmp(hd, "X-Real-IP")) S->rtype = 1;
+            else if (!strcmp(hd, "X-Forwarded-For")) S->rtype = 2;
+            else if (!strcmp(hd, "proxy_protocol")) S->rtype = 3;
+            else {
+                S->rtype = 4;
+                snprintf(S->hdr, sizeof S->hdr, "%s", hd);
+                for (char *q = S->hdr; *q; q++) *q = (char)lc((unsigned char)*q);
+            }
+            S->cidr = calloc((size_t)fr->nfrom, sizeof(ocidr_t));
+            for (int k = 0; k < fr->nfrom; k++) {
+                if (!strncmp(fr->from[k], "unix:", 5)) continue;
+                if (!o_ptocidr(fr->from[k], &S->cidr[S->ncidr])) { S->rtype = 5; continue; }
+                S->ncidr++;
+            }
+        }
+    }
     if (sigt && load_sigs(c, sigt, sign) < 0) return NULL;
     build_ac(c);
     return c;
@@ -995,6 +1330,9 @@ int orc_info(orc_ctx *c, uint32_t *out4) {
 typedef struct {
     const gm_req *r; const uint8_t *a;
     sv uri, args, hdrs, body, host, method, ruri, raddr;
+    const srv_t *S;        /* the server (its realip settings), NULL before it is known */
+    int rip;               /* 0 not evaluated, 1 unchanged, 2 replaced, 3 unknown to the engine */
+    char ra[64]; int ra_len; oaddr_t raddr2;
 } rq_t;
 
 static void rq_init(rq_t *q, const gm_req *r, const uint8_t *arena) {
@@ -1008,6 +1346,50 @@ static void rq_init(rq_t *q, const gm_req *r, const uint8_t *arena) {
     q->method = (sv){p, r->method_len}; p += r->method_len;
     q->ruri = (sv){p, r->ruri_len}; p += r->ruri_len;
     q->raddr = (sv){p, r->raddr_len};
+    q->S = NULL; q->rip = 0;
+}
+
+static int hdr_next(sv h, int *pos, sv *name, sv *val);
+
+/* ngx_http_realip_handler for the request's server (post-read phase): q->rip */
+static void orc_realip(rq_t *q) {
+    const srv_t *S = q->S;
+    q->rip = 1;
+    if (!S || !S->rtype) return;
+    if (S->rtype == 5) { q->rip = 3; return; }
+    oaddr_t a;
+    memset(&a, 0, sizeof a);
+    if (!(q->raddr.n > 0 && q->raddr.n < 46 && o_parse_addr(q->raddr.p, q->raddr.n, &a))) a.fam = 0;
+    if (S->rtype == 3) {   /* proxy_protocol: the address is in the PROXY header, not the record */
+        if (a.fam && o_cidr_match(S, &a)) q->rip = 3;
+        return;
+    }
+    if (!a.fam) return;
+    int rc = 0;
+    int pos = 0; sv hn, vv;
+    if (S->rtype == 2) {
+        /* every X-Forwarded-For line, last first (ngx_http_get_forwarded_addr over the array) */
+        sv vals[256]; int nv = 0;
+        while (hdr_next(q->hdrs, &pos, &hn, &vv))
+            if (hn.n == 15 && !strncasecmp(hn.p, "x-forwarded-for", 15) && nv < 256) vals[nv++] = vv;
+        int found = 0;
+        for (int i = nv - 1; i >= 0; i--) {
+            rc = o_fwd_internal(S, &a, vals[i].p, vals[i].n);
+            if (!S->rrec) break;
+            if (rc == 0 && found) { rc = 2; break; }
+            if (rc != 1) break;
+            found = 1;
+        }
+    } else {
+        const char *want = S->rtype == 1 ? "x-real-ip" : S->hdr;
+        int wl = (int)strlen(want);
+        while (hdr_next(q->hdrs, &pos, &hn, &vv))
+            if (hn.n == wl && !strncasecmp(hn.p, want, (size_t)wl)) { rc = o_fwd_internal(S, &a, vv.p, vv.n); break; }
+    }
+    if (rc == 0) return;
+    q->raddr2 = a;
+    q->ra_len = o_ntop(&a, q->ra);
+    q->rip = 2;
 }
 
 /* scratch string arena, per thread: chunked so earlier views stay valid until reset */
@@ -1076,7 +1458,7 @@ static uint32_t murmur2(const uint8_t *data, size_t len) {
 }
 uint32_t orc_murmur2(const uint8_t *d, size_t n) { return murmur2(d, n); }
 
-typedef struct { orc_ctx *c; rq_t *q; scratch_t *sc; int depth; int *last_param; int *last_part; } ev_t;
+typedef struct { orc_ctx *c; rq_t *q; scratch_t *sc; int depth; int *last_param; int *last_part; int unknown; } ev_t;
 
 static sv eval_complex(ev_t *E, const char *tpl);
 
@@ -1091,8 +1473,14 @@ static sv get_var(ev_t *E, const char *name, int nlen) {
     if (!strcmp(nm, "args") || !strcmp(nm, "query_string")) return q->args;
     if (!strcmp(nm, "uri") || !strcmp(nm, "document_uri")) return q->uri;
     if (!strcmp(nm, "request_body")) return (sv){"", 0};
-    if (!strcmp(nm, "remote_addr")) return q->raddr;
-    if (!strcmp(nm, "remote_port")) { char t[8]; int n = snprintf(t, 8, "%u", r->remote_port); return sc_put(E->sc, t, n); }
+    if (!strcmp(nm, "remote_addr") || !strcmp(nm, "remote_port")) {
+        if (!q->rip) orc_realip(q);
+        if (q->rip == 3) { E->unknown = 1; return (sv){"", 0}; }
+        if (nm[7] == 'a') return q->rip == 2 ? (sv){q->ra, q->ra_len} : q->raddr;
+        unsigned port = q->rip == 2 ? (unsigned)q->raddr2.port : r->remote_port;
+        if (q->rip == 2 && port == 0) return (sv){"", 0};   /* no port in the header's address */
+        char t[8]; int n = snprintf(t, 8, "%u", port); return sc_put(E->sc, t, n);
+    }
     if (!strcmp(nm, "server_port")) { char t[8]; int n = snprintf(t, 8, "%u", r->port); return sc_put(E->sc, t, n); }
     if (!strcmp(nm, "request_uri")) {
         if (q->ruri.n) return q->ruri;
@@ -1589,6 +1977,7 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
     }
     if (bad || (port_ssl && !(r->flags & GM_REQ_HTTPS))) { v->action = GM_ACT_BAD_REQUEST; v->status = 400; return; }
     srv_t *S = &c->srv[sidx];
+    q.S = S;
     ev_t E = {c, &q, sc, 0, NULL, NULL};
     for (int i = 0; i < S->nifs; i++) {
         sif_t *f = &S->ifs[i];
@@ -1598,6 +1987,7 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
         else {
             const char *vn = f->var; sv val = {"", 0};
             if (vn[0] == '$') val = get_var(&E, vn + 1, (int)strlen(vn + 1));
+            if (E.unknown) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
             if (f->op == 0) hit = val.n && !(val.n == 1 && val.p[0] == '0');
             else if (f->op == 1) hit = sv_eq(val, f->val);
             else if (f->op == 2) hit = !sv_eq(val, f->val);
@@ -1608,19 +1998,32 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
             v->status = (uint32_t)f->code; return;
         }
     }
+    /* client_max_body_size: a Content-Length body against the location found, before its rewrite
+     * phase (ngx_http_core_find_config_phase); a chunked one when the proxying location reads it */
+    const int chunked = (r->flags & GM_REQ_CHUNKED) != 0;
+#define TOO_LARGE(lim) (!chunked && (lim) >= 0 && (int64_t)r->body_len > (lim))
     int a301 = 0;
     int lid = find_location(c, S, q.uri, &a301);
-    if (lid < 0) { v->action = GM_ACT_NOT_FOUND; v->status = 404; return; }
+    if (lid < 0) {
+        if (TOO_LARGE(S->body_max)) { v->action = GM_ACT_TOO_LARGE; v->status = 413; return; }
+        v->action = GM_ACT_NOT_FOUND; v->status = 404; return;
+    }
     v->location_id = (uint32_t)lid;
-    if (a301) { v->action = GM_ACT_AUTO_301; v->status = 301; return; }
     loc_t *L = &c->loc[lid];
-    if (L->pcre_only || L->nested) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
+    if (TOO_LARGE(L->body_max)) { v->action = GM_ACT_TOO_LARGE; v->status = 413; return; }
+#undef TOO_LARGE
+    if (a301) { v->action = GM_ACT_AUTO_301; v->status = 301; return; }
+    if (L->pcre_only || L->nested || L->unknown) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
     loc_t *F = L;   /* location that runs the content phase */
     if (L->has_return && L->ret_code == 418 && L->err418) {
         int pidx = -2, part = -2;
         E.last_param = &pidx; E.last_part = &part;
         sv target = eval_complex(&E, L->err418);
         E.last_param = NULL; E.last_part = NULL;
+        if (E.unknown) {   /* a condition / split source the engine cannot know: deferred */
+            v->route_kind = part != -2 ? GM_ROUTE_SPLIT : GM_ROUTE_RULES;
+            v->action = GM_ACT_UNSUPPORTED; v->status = 0; return;
+        }
         if (part != -2) { v->route_kind = GM_ROUTE_SPLIT; v->split_bucket = part < 0 ? 0xFF : (uint8_t)part; }
         else if (pidx != -2) { v->route_kind = GM_ROUTE_RULES; v->match_idx = pidx < 0 ? 0xFF : (uint8_t)pidx; }
         if (target.n && target.p[0] == '@') {
@@ -1646,6 +2049,9 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
         v->status = (uint32_t)F->ret_code; return;
     }
     if (!F->has_proxy) { v->action = GM_ACT_NOT_FOUND; v->status = 404; return; }
+    if (chunked && F->body_max >= 0 && (int64_t)r->body_len > F->body_max) {
+        v->action = GM_ACT_TOO_LARGE; v->status = 413; return;
+    }
     v->action = GM_ACT_PROXY; v->status = 0;
     v->upstream_id = F->upstream_id < 0 ? GM_NONE : (uint32_t)F->upstream_id;
     v->waf_mode = (uint16_t)F->waf_mode;
@@ -1843,6 +2249,7 @@ typedef struct {
     const uint8_t *args; int args_len;
     const uint8_t *uhost; int uhost_len;     /* absolute-form host */
     int body_start;                          /* offset of the first body byte */
+    int chunked;                             /* Transfer-Encoding: chunked */
 } orc_rl_t;
 
 static int orc_rl_parse(const uint8_t *b, int n, orc_rl_t *r) {
@@ -1987,6 +2394,7 @@ static int orc_parse_one(const uint8_t *b, int n, orc_rl_t *R, obuf_t *uri, obuf
     if (R->uhost) { *host = R->uhost; *host_len = R->uhost_len; }   /* the absolute URI's host wins */
     if (cl_bad) return 400;
     if (te_kind == 3) return 501;
+    R->chunked = te_kind == 1;
     if (te_kind == 1) {
         for (;;) {
             /* chunk-size line: hex digits, then CRLF / LF, or an extension (';', SP, HT ...) up
@@ -2055,6 +2463,7 @@ int64_t orc_parse_requests(const uint8_t *wire, const gm_wire_msg *msgs, uint32_
             r->pad0[1] = (uint8_t)(st & 0xFF); r->pad0[2] = (uint8_t)(st >> 8);
         } else {
             if (R.minor == 0) r->flags |= GM_REQ_HTTP10;
+            if (R.chunked) r->flags |= GM_REQ_CHUNKED;
             seg[0] = uri.p; len[0] = uri.n;
             seg[1] = R.args; len[1] = (size_t)R.args_len;
             seg[2] = hdrs.p; len[2] = hdrs.n;
@@ -2130,7 +2539,7 @@ static int orc_lc(oups_t *U, gm_peer_state *st) {
 
 /* -1: round robin, -2: defer; st conns are the batch-start snapshot for random two */
 static int orc_stateless(orc_ctx *c, oups_t *U, const gm_req *r, const uint8_t *arena, gm_peer_state *st,
-                         const uint32_t *snap_conns, scratch_t *sc) {
+                         const uint32_t *snap_conns, scratch_t *sc, uint32_t server) {
     int n = U->npeers;
     if (U->method == OM_RANDOM) {
         for (uint32_t tries = 0;;) {
@@ -2153,10 +2562,15 @@ static int orc_stateless(orc_ctx *c, oups_t *U, const gm_req *r, const uint8_t *
     }
     if (n == 1) return -1;
     rq_t q; rq_init(&q, r, arena);
+    if (server < (uint32_t)c->nsrv) q.S = &c->srv[server];
     if (U->method == OM_IP_HASH) {
         uint8_t b[16] = {0}; int alen = 3;
         char t[64];
-        if (q.raddr.n < (int)sizeof t) {
+        orc_realip(&q);   /* ip_hash hashes the address the realip module set */
+        if (q.rip == 3) return -2;
+        if (q.rip == 2) {
+            memcpy(b, q.raddr2.b, 16); alen = q.raddr2.fam == 4 ? 3 : 16;
+        } else if (q.raddr.n < (int)sizeof t) {
             memcpy(t, q.raddr.p, q.raddr.n); t[q.raddr.n] = 0;
             uint8_t a6[16];
             if (inet_pton(AF_INET, t, b) == 1) alen = 3;
@@ -2173,6 +2587,7 @@ static int orc_stateless(orc_ctx *c, oups_t *U, const gm_req *r, const uint8_t *
     }
     ev_t E = {c, &q, sc, 0, NULL, NULL};
     sv key = eval_complex(&E, U->key);
+    if (E.unknown) return -2;
     if (key.n == 0) return -1;
     if (U->method == OM_CHASH) {
         uint32_t h = orc_crc32(key.p, key.n);
@@ -2222,7 +2637,7 @@ int orc_select_peers(orc_ctx *c, const gm_req *reqs, const uint8_t *arena, const
             p = orc_lc(U, st);
             if (p >= 0) st[U->first_peer + p].conns++;   /* least_conn sees its own picks at once */
         } else {
-            p = U->method == OM_RR ? -1 : orc_stateless(c, U, &reqs[i], arena, st, snap, &sc);
+            p = U->method == OM_RR ? -1 : orc_stateless(c, U, &reqs[i], arena, st, snap, &sc, v[i].server_id);
             if (p == -2) { out[i] = GM_PEER_DEFER; continue; }
             /* the engine's round-robin fallback holds at most 1024 peers (SEQ_PEERS_MAX) */
             if (p == -1 && U->npeers > 1024) { out[i] = GM_PEER_DEFER; continue; }

@@ -201,13 +201,15 @@ def main():
         "vsrs": [vsr_coffee([ups("coffee", "coffee-svc")], {"path": "/coffee", "upstream": "coffee"})],
         "endpoints": {"default/tea-svc:80": ["10.0.0.20:80"], "default/coffee-svc:80": ["10.0.0.30:80"]},
         "params": {"ServerTokens": "off", "Keepalive": 16, "ServerSnippets": ["# server snippet"],
-                   "ProxyProtocol": True, "RedirectToHTTPS": True},
+                   "ProxyProtocol": True, "RedirectToHTTPS": True,
+                   "SetRealIPFrom": ["0.0.0.0/0"], "RealIPHeader": "X-Real-IP", "RealIPRecursive": True},   # :230-232
         "expected": {
             "Upstreams": [["vs_default_cafe_tea", "10.0.0.20:80"],
                           ["vs_default_cafe_vsr_default_coffee_coffee", "10.0.0.30:80"]],
             "SplitClients": [], "Maps": [],
             "Server": {"ServerName": "cafe.example.com", "ProxyProtocol": True,
                        "RedirectToHTTPSBasedOnXForwarderProto": True, "ServerTokens": "off",
+                       "SetRealIPFrom": ["0.0.0.0/0"], "RealIPHeader": "X-Real-IP", "RealIPRecursive": True,   # :260-262
                        "Snippets": ["# server snippet"], "InternalRedirectLocations": [],
                        "Locations": [["/tea", "http://vs_default_cafe_tea"],
                                      ["/coffee", "http://vs_default_cafe_vsr_default_coffee_coffee"]]},

@@ -194,25 +194,17 @@ def test_normalize_after_overflow_syncs_clean(torch_dev):
 # a batch that overflows an internal WAF buffer must complete on the device.  The
 # scan's candidate regions and the context filter's survivor regions are finished by
 # k_waf_direct; an overflowing pair or job list is replaced by the dedupe set (k_hits_scatter /
-# k_waf_regex read it).  GM_SCRATCH_SCALE (read at gm_create) shrinks the default capacities so
+# k_waf_regex read it).  GM_CREATE_SCRATCH_SHIFT (a gm_create flag) shrinks the default capacities so
 # that every continuation runs on a batch the oracle checks in seconds.
 OV_PAIRS, OV_CAND, OV_SURV, OV_JOBS = 1, 4, 8, 128
 
 
-def _engine_scaled(scale):
-    import os
-    old = os.environ.get("GM_SCRATCH_SCALE")
-    os.environ["GM_SCRATCH_SCALE"] = str(scale)
-    try:
-        return engine.Engine(0)
-    finally:
-        if old is None:
-            del os.environ["GM_SCRATCH_SCALE"]
-        else:
-            os.environ["GM_SCRATCH_SCALE"] = old
+def _engine_scaled(shift):
+    e = engine.Engine(0, scratch_shift=shift)   # GM_CREATE_SCRATCH_SHIFT: buffers at 2^-shift
+    return e
 
 
-@pytest.mark.parametrize("scale,want", [(0.002, OV_CAND | OV_SURV), (0.0002, OV_CAND | OV_SURV | OV_PAIRS)])
+@pytest.mark.parametrize("scale,want", [(9, OV_CAND | OV_SURV), (12, OV_CAND | OV_SURV | OV_PAIRS)])
 def test_internal_overflow_completes_on_device(torch_dev, scale, want):
     """The stress variant (many candidates, real matches) on a fresh stream with shrunken internal
     buffers: the first call returns GM_OK, the overflow bits show which continuations ran, and
@@ -234,7 +226,7 @@ def test_job_list_overflow_runs_jobs_from_set(torch_dev):
     ss = workloads.c4_job_sigset()
     reqs, arena = records.gen_c4(8_000, ss, seed=records.SEED_BASE + 91, plant_rate=0.5, pool_mb=4)
     b = workloads.c4_blob(ss)
-    e = _engine_scaled(0.0002)
+    e = _engine_scaled(12)
     e.load(b, 6)
     got, gh = e.match_host(reqs, arena)
     st = e.stats()
