@@ -35,7 +35,7 @@ def check_build(st, args):
     if st["build_flags"] and not args.allow_nondefault_build:
         raise SystemExit(f"bench.py: the loaded libgpumatch.so is a non-default build (build_flags "
                          f"{st['build_flags']:#x}); rebuild it with `make` or pass --allow-nondefault-build")
-    if st.get("scratch_scale", 1.0) != 1.0:
+    if st.get("scratch_scale", 1.0) != 1.0 or st.get("set_shift", 0):
         raise SystemExit(f"bench.py: scratch capacities are scaled ({st['scratch_scale']}): not the default context")
 
 

@@ -43,6 +43,8 @@ extern "C" {
 #define GM_E_NOMEM      -6
 #define GM_E_COMM       -7   /* RCCL error                                             */
 #define GM_E_NODEVICE   -8   /* compute call on a compile-only context                 */
+#define GM_E_STALE      -9   /* gm_update_upstream: the live generation changed under it
+                                (a load or another update published first); nothing published */
 
 /* ---------------------------------------------------------------- gm_create flags */
 #define GM_CREATE_COMPILE_ONLY  0x1u  /* no HIP device: compile + stats only (host tests) */
@@ -54,6 +56,9 @@ extern "C" {
  * capacity, k = 1..31 (bits 8..15), so the overflow continuations run on batches small enough for
  * the oracle; reported in gm_stats_t.scratch_scale */
 #define GM_CREATE_SCRATCH_SHIFT(k) (((uint32_t)(k) & 0xFFu) << 8)
+/* test hook: the WAF dedupe set at 2^-k of its default capacity too (bits 16..23), so a batch
+ * overflows it (OV_SET) and gm_sync's re-run with the set doubled is exercised */
+#define GM_CREATE_SET_SHIFT(k) (((uint32_t)(k) & 0xFFu) << 16)
 
 /* ---------------------------------------------------------------- packed request record
  * One 64-byte header per request; payload bytes live in one byte arena.  The payload of a
@@ -214,7 +219,10 @@ typedef struct gm_stats_t {
     uint32_t build_flags;
     /* the internal WAF capacity scale in effect (GM_CREATE_SCRATCH_SHIFT test hook; 1.0 normally) */
     float    scratch_scale;
-    uint32_t reserved_stats[5];
+    /* batches gm_sync re-ran because the WAF dedupe set overflowed (cumulative, this ctx) */
+    uint32_t n_set_reruns;
+    uint32_t set_shift;          /* GM_CREATE_SET_SHIFT in effect (0 normally) */
+    uint32_t reserved_stats[3];
 } gm_stats_t;
 
 /* gm_stats_t.build_flags: measurement / test variants compiled into the library.  bench.py refuses
@@ -267,7 +275,10 @@ int         gm_sync(gm_ctx *ctx, void *stream);
 /* Per-location and per-signature hit counters of this device, u64, cumulative since the
  * generation was loaded (or gm_counters_reset): [0, n_locations) locations,
  * [n_locations, n_locations + n_sigs) signatures (gm_stats_t.n_counters entries).  The analogue
- * of the reference's monotonic Prometheus counters (internal/metrics/collectors/manager.go:27-59). */
+ * of the reference's monotonic Prometheus counters (internal/metrics/collectors/manager.go:27-59).
+ * A batch's hits are committed once, when it completes whole: a batch gm_sync reports void
+ * (GM_E_OVERFLOW) adds nothing, so its retry counts each request once; a batch whose WAF dedupe
+ * set overflowed is re-run inside gm_sync (gm_stats_t.n_set_reruns) and counted on that run. */
 int         gm_counters(gm_ctx *ctx, uint64_t *out, size_t n);
 int         gm_counters_reset(gm_ctx *ctx);
 
@@ -276,7 +287,9 @@ int         gm_comm_unique_id(void *out_128_bytes);
 int         gm_comm_init(gm_ctx *ctx, const void *nccl_unique_id, int nranks, int rank);
 /* Sum of every rank's cumulative counters (RCCL all-reduce over xGMI, enqueued on `stream`),
  * OUT OF PLACE: the local counters are untouched, so any number of calls give the true job
- * totals.  gm_counters_global() reads the result of the last call. */
+ * totals.  gm_counters_global() reads the result of the last call.  Collective: every rank calls
+ * it.  The ranks first agree on (gen, n_counters) with one 4-word MAX reduction (synchronous on
+ * `stream`); if any rank differs, every rank returns GM_E_COMM and no sum is issued. */
 int         gm_counters_allreduce(gm_ctx *ctx, void *stream);
 int         gm_counters_global(gm_ctx *ctx, uint64_t *out, size_t n);
 
@@ -382,7 +395,12 @@ int         gm_release_peers(gm_ctx *ctx, const uint32_t *peer_ids, uint32_t n, 
  * either table stay valid for gm_select_peers (same upstream ids).  Counters carry over.  The
  * peer table is renumbered (gm_stats_t.n_peers, gm_peer_address): carry every balancer state
  * array over with gm_peers_migrate before its next gm_select_peers.  GM_E_INVAL: no upstream of
- * that name (the previous tables stay live). */
+ * that name (the previous tables stay live).  GM_E_STALE: a gm_load_generation or another
+ * gm_update_upstream published between this call's read of the live tables and its publish -- the
+ * newer tables stay, nothing is overwritten (the reference refuses a Plus update whose
+ * configVersion no longer matches, verifyConfigVersion, manager.go:258); re-issue the update.
+ * Peer order: the kept servers in their previous relative order, then the added ones in the order
+ * given (the Plus API appends a POSTed server); that order is parity-unpinned against a live Plus. */
 int         gm_update_upstream(gm_ctx *ctx, const char *upstream, const char *const *servers, uint32_t n);
 /* new_state[j] = old_state[i] where peer j of the live table is the server of the same upstream
  * and address as peer i of the table before the last gm_update_upstream (NGINX Plus keeps a kept

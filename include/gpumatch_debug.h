@@ -42,6 +42,15 @@ int64_t gm_debug_waf_prefilter(struct gm_ctx *ctx, const uint8_t *A, size_t len,
 int64_t gm_debug_waf_prefilter2(struct gm_ctx *ctx, const uint8_t *A, size_t len, uint64_t *out, size_t cap);
 /* The realip address rules on the host (gm_inet.hpp, the code the device runs): `text` parsed as
  * ngx_parse_addr_port -> "<ngx_sock_ntop text> <port>" into out; -1 if it is not an address. */
+/* gm_counters_allreduce's generation agreement: the 4 words a rank contributes to the MAX
+ * reduction (gen, n_counters and their complements to 0xFFFFFFFF), and the verdict on the reduced
+ * words (GM_OK: every rank had the same gen and n_counters; GM_E_COMM otherwise). */
+void gm_debug_agree_pack(uint64_t gen, uint64_t n_counters, uint64_t *words4);
+int  gm_debug_agree_check(const uint64_t *max_words4);
+/* Tests: fn(arg) runs inside every later gm_update_upstream between its read of the live tables and
+ * its publish, with no lock held (a gm_load_generation there must make the update fail GM_E_STALE).
+ * fn = NULL clears it. */
+void gm_debug_update_hook(void (*fn)(void *), void *arg);
 int gm_debug_inet(const uint8_t *text, size_t n, char *out, size_t cap);
 #ifdef __cplusplus
 }

@@ -2225,18 +2225,28 @@ CompileResult update_upstream(const CompileResult &live, const std::string &name
             if (D.method == UM_DEFER) R.stats.n_upstreams_deferred++;
             continue;
         }
-        // the updated upstream: its servers in the given order, a kept address keeps its state
+        // the updated upstream in NGINX Plus's order after UpdateHTTPServers (the API client deletes
+        // the servers not listed and POSTs the new ones, each appended to the upstream's peer list):
+        // the kept servers in their previous relative order, then the added ones in the order given.
+        // A kept address keeps its state (gm_peers_migrate).  (The order of a live Plus upstream is
+        // parity-unpinned: no reference fixture covers it; the tests check this rule.)
         const UpstreamMeta &M = live.ups_meta[u];
-        std::vector<bool> used(O.n_peers, false);
-        for (const std::string &a : addrs) {
-            uint32_t from = GM_NONE;
-            for (uint32_t j = 0; j < O.n_peers; j++)
-                if (!used[j] && live.peer_addrs[O.first_peer + j] == a) { used[j] = true; from = O.first_peer + j; break; }
+        std::vector<bool> taken(addrs.size(), false);
+        std::vector<std::string> order;
+        auto put = [&](const std::string &a, uint32_t from) {
             peer_init.push_back(0u);   // Plus API servers: none `down`
             R.peer_addrs.push_back(a);
             R.peer_ups.push_back(u);
             R.peer_map.push_back(from);
+            order.push_back(a);
+        };
+        for (uint32_t j = 0; j < O.n_peers; j++) {
+            const std::string &old_a = live.peer_addrs[O.first_peer + j];
+            for (size_t i = 0; i < addrs.size(); i++)
+                if (!taken[i] && addrs[i] == old_a) { taken[i] = true; put(old_a, O.first_peer + j); break; }
         }
+        for (size_t i = 0; i < addrs.size(); i++)
+            if (!taken[i]) put(addrs[i], GM_NONE);
         D.n_peers = (uint32_t)addrs.size();
         D.method = M.has_block ? M.method : UM_DEFER;
         bool defer = !M.has_block || M.defer_fixed;
@@ -2245,8 +2255,8 @@ CompileResult update_upstream(const CompileResult &live, const std::string &name
         D.n_points = 0;
         if (D.method == UM_CHASH && !defer) {
             std::set<std::string> seen;
-            for (const std::string &a : addrs) if (!seen.insert(a).second) defer = true;
-            if (!defer) chash_ring(addrs, points);
+            for (const std::string &a : order) if (!seen.insert(a).second) defer = true;
+            if (!defer) chash_ring(order, points);
             D.n_points = (uint32_t)points.size() - D.first_point;
         }
         if (defer) { D.method = UM_DEFER; R.stats.n_upstreams_deferred++; }

@@ -22,6 +22,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <shared_mutex>
 #include <string>
@@ -1342,15 +1343,29 @@ struct Scratch {
     uint4 *d_rqu = nullptr; size_t cap_rqu = 0;          // and its $uri's first 32 bytes (+ a pad block)
     int32_t *d_rqb = nullptr; size_t cap_rqb = 0;        // and its longest prefix match (the tail pass)
     unsigned long long *d_rqm = nullptr; size_t cap_rqm = 0;   // and its prefiltered-slice mask
+    unsigned long long *d_bctr = nullptr; size_t cap_bctr = 0; // this batch's counters (k_ctr_commit)
+    unsigned long long *d_agree = nullptr, *h_agree = nullptr;  // gm_counters_allreduce's agreement words
+    // the last gm_match_batch's arguments: gm_sync re-runs a batch whose dedupe set overflowed
+    // (OV_SET) with the set doubled, until it fits -- only the caller's hit_cap voids a batch
+    struct Replay {
+        bool valid = false;
+        const void *gen = nullptr; uint64_t seq = 0;
+        const gm_req *reqs = nullptr; const uint8_t *A = nullptr; uint64_t alen = 0; uint32_t n = 0;
+        gm_verdict *out = nullptr; uint32_t *hits = nullptr; size_t hit_cap = 0; const uint64_t *dlen = nullptr;
+        // GM_BATCH_HOST: the staged device copies and the caller's host buffers
+        gm_verdict *h_out = nullptr; uint32_t *h_hits = nullptr; size_t h_hit_cap = 0;
+    } replay;
     ~Scratch() {
         for (void *p : {(void *)d_status, (void *)d_blk2rec, (void *)d_cand, (void *)d_surv, (void *)d_pairs,
                         (void *)d_jobs, (void *)d_set, (void *)d_cnt, (void *)d_start, (void *)d_ccnt,
                         (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp, (void *)d_wscr, (void *)d_wsum,
                         (void *)d_pk, (void *)d_pseg, (void *)d_pprog, (void *)d_ppat, (void *)d_ptemp,
                         (void *)d_usize, (void *)d_utemp, (void *)d_sreqs, (void *)d_sarena, (void *)d_sblk,
-                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm, (void *)d_rqu})
+                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm, (void *)d_rqu, (void *)d_bctr})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
+        if (h_agree) (void)hipHostFree(h_agree);
+        if (d_agree) (void)hipFree(d_agree);
         for (auto &e : ev) if (e) (void)hipEventDestroy(e);
         for (auto &e : ev_route) if (e) (void)hipEventDestroy(e);
         if (ev_fork) (void)hipEventDestroy(ev_fork);
@@ -1365,8 +1380,11 @@ struct gm_ctx {
     uint32_t flags = 0;
     int cu_count = 256;
     double cap_scale = 1.0;                   // GM_CREATE_SCRATCH_SHIFT (test hook): internal WAF capacities
+    uint32_t set_shift = 0;                   // GM_CREATE_SET_SHIFT (test hook): the dedupe set
+    std::atomic<uint32_t> n_set_reruns{0};    // gm_sync re-runs of OV_SET batches
     std::shared_mutex gen_mu;                 // shared: enqueueing batches; exclusive: the swap
     Generation *gen = nullptr;
+    uint64_t publish_seq = 0;                 // bumped under gen_mu (exclusive) by every publish
     std::mutex scr_mu;                        // the stream -> scratch map only
     std::map<hipStream_t, std::unique_ptr<Scratch>> scratch;
     ncclComm_t comm = nullptr;
@@ -1380,6 +1398,10 @@ struct gm_ctx {
 // gm_last_error() is thread-local (include/gpumatch.h): concurrent callers on one ctx never see
 // each other's messages
 static thread_local std::string t_err;
+// gm_debug_update_hook: a test callback run by gm_update_upstream between reading the live tables
+// and publishing (no lock held), e.g. a gm_load_generation racing the update
+static void (*g_update_hook)(void *) = nullptr;
+static void *g_update_hook_arg = nullptr;
 
 static int fail(gm_ctx *, int code, const std::string &m) {
     t_err = m;
@@ -1441,6 +1463,21 @@ static int mark_done(gm_ctx *c, Scratch *S) {
     S->done_rec = true;
     return GM_OK;
 }
+// Scope guard of a call that enqueues work: done() records ev_done; an early (error) return drains
+// the stream and its side stream instead, so nothing enqueued before the error is left in flight
+// uncovered by an event (RCU retirement and counter reads wait only on ev_done).
+struct DoneGuard {
+    Scratch *S;
+    bool armed = true;
+    explicit DoneGuard(Scratch *s) : S(s) {}
+    int done(gm_ctx *c) { armed = false; return mark_done(c, S); }
+    ~DoneGuard() {
+        if (armed && S) {
+            (void)hipStreamSynchronize(S->side);
+            (void)hipStreamSynchronize(S->stream);
+        }
+    }
+};
 
 // Wait until every call enqueued so far through this ctx has completed: the completion event of
 // each stream's last call (RCU retirement of a swapped-out generation, counter reads).  Only this
@@ -1473,6 +1510,7 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
     c->dev = hip_device;
     c->flags = flags;
     if (const uint32_t k = (flags >> 8) & 0xFFu) c->cap_scale = k < 32 ? 1.0 / (double)(1ull << k) : 1.0;
+    if (const uint32_t k = (flags >> 16) & 0xFFu) c->set_shift = k < 24 ? k : 0;
     if (!(flags & GM_CREATE_COMPILE_ONLY)) {
         if (hipSetDevice(hip_device) != hipSuccess) { t_err = "hipSetDevice failed"; delete c; return nullptr; }
         // the WAF scan's Bloom filter is dynamic LDS beyond the 64 KiB default
@@ -1534,7 +1572,10 @@ const char *gm_last_error(gm_ctx *) { return t_err.c_str(); }
 // enqueueing before the lock was granted, and its completion event is waited for before the old
 // memory is freed.  `same_counters`: the new tables keep the live generation's counter space
 // (gm_update_upstream: same locations and signatures), the counters move over unreset.
-static int publish(gm_ctx *c, CompileResult &R, uint32_t gen, bool same_counters) {
+// `expect_seq` (same_counters only): the publish_seq the tables were derived under -- a load or
+// another update published since fails GM_E_STALE instead of being overwritten (the reference's
+// Plus update refuses a configVersion mismatch, verifyConfigVersion, manager.go:258).
+static int publish(gm_ctx *c, CompileResult &R, uint32_t gen, bool same_counters, uint64_t expect_seq = 0) {
     if (R.stats.n_sigs >= (1u << 21) || R.stats.n_sig_regex >= (1u << 21))
         return fail(c, GM_E_INVAL, "more than 2^21 signatures");
     std::unique_ptr<Generation> g(new Generation());
@@ -1571,13 +1612,17 @@ static int publish(gm_ctx *c, CompileResult &R, uint32_t gen, bool same_counters
     {
         std::unique_lock<std::shared_mutex> lk(c->gen_mu);
         old = c->gen;
-        if (same_counters && old) {
+        if (same_counters) {
+            if (c->publish_seq != expect_seq || !old)
+                return fail(c, GM_E_STALE, "the live generation changed during the upstream update (a load or "
+                                           "another update published first); nothing published");
             if (old->n_counters != g->n_counters) return fail(c, GM_E_INVAL, "counter space changed");
             g->d_counters = old->d_counters; g->d_counters_sum = old->d_counters_sum;
             old->d_counters = old->d_counters_sum = nullptr;
             g->peer_map_old_n = old->stats.n_peers;
         }
         c->gen = g.release();
+        c->publish_seq++;
     }
     if (old && !(c->flags & GM_CREATE_COMPILE_ONLY)) {
         const int e = wait_done(c);
@@ -1603,6 +1648,7 @@ int gm_update_upstream(gm_ctx *c, const char *upstream, const char *const *serve
     }
     CompileResult live;
     uint32_t gen;
+    uint64_t seq;
     {
         std::shared_lock<std::shared_mutex> lk(c->gen_mu);
         const Generation *g = c->gen;
@@ -1611,13 +1657,13 @@ int gm_update_upstream(gm_ctx *c, const char *upstream, const char *const *serve
         live.peer_addrs = g->peer_addrs; live.peer_ups = g->peer_ups; live.ups_meta = g->ups_meta;
         live.rejects = g->rejects;
         gen = g->stats.gen;
+        seq = c->publish_seq;
     }
     CompileResult R = update_upstream(live, upstream, addrs);
     if (!R.ok) return fail(c, R.code, R.err);
     R.rejects = live.rejects;
-    // (two concurrent updates: the second publishes over the first's tables -- the Manager calls
-    // UpdateServersInPlus one upstream at a time, configurator.go:442,467,489)
-    return publish(c, R, gen, true);
+    if (g_update_hook) g_update_hook(g_update_hook_arg);   // tests: a load between the read and the publish
+    return publish(c, R, gen, true, seq);
 }
 
 // The measurement / tuning variants compiled in (gm_stats_t.build_flags): a bench line can show it
@@ -1643,6 +1689,8 @@ int gm_stats(gm_ctx *c, gm_stats_t *out) {
     *out = c->gen->stats;
     out->build_flags = kBuildFlags;
     out->scratch_scale = (float)c->cap_scale;
+    out->n_set_reruns = c->n_set_reruns.load();
+    out->set_shift = c->set_shift;
     std::lock_guard<std::mutex> l2(c->last_mu);
     out->last_candidates = c->last_candidates;
     out->last_pairs = c->last_pairs;
@@ -1714,10 +1762,20 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     S->ev_used = 0;
     S->route_side = false;
     HIPCHK(c, hipMemsetAsync(S->d_status, 0, BATCH_STATUS_WORDS * 4, s));
+    // the batch's counters accumulate apart and are committed by k_ctr_commit at the end
+    const size_t nctr = std::max<size_t>(g->n_counters, 1);
+    if (int e0 = grow(c, s, S->d_bctr, S->cap_bctr, nctr)) return e0;
+    HIPCHK(c, hipMemsetAsync(S->d_bctr, 0, nctr * 8, s));
+    auto commit = [&]() -> int {
+        k_ctr_commit<<<std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)((nctr + 255) / 256), (uint32_t)c->cu_count)), 256, 0, s>>>(
+            S->d_bctr, g->d_counters, (uint32_t)g->n_counters, S->d_status);
+        HIPCHK(c, hipGetLastError());
+        return GM_OK;
+    };
     if (mark(0)) return GM_E_HIP;
     const uint32_t route_blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
                                                                            (uint32_t)c->cu_count * GM_EXP_GRIDMUL));
-    unsigned long long *ctr = g->d_counters;
+    unsigned long long *ctr = S->d_bctr;
     // prefiltered regex locations: k_route defers their step to k_rloc (a tile of requests per
     // workgroup, gm_rloc.inc) and a second k_route pass over the deferred list finishes them
     RlocQ q{};
@@ -1777,6 +1835,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
             const int e4 = launch_rloc(s, route_blocks);
             if (e4) return e4;
         }
+        if (int e5 = commit()) return e5;
         return mark(1) ? GM_E_HIP : GM_OK;
     }
     int e;
@@ -1797,6 +1856,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     // overflow): sized from the unscaled list capacities
     size_t set_need = 1;
     while (set_need < 2 * (pcap0 + jcap0)) set_need <<= 1;
+    set_need = std::max<size_t>(set_need >> c->set_shift, 1024);
     size_t scan_tmp = 0;
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
     if ((e = grow(c, s, S->d_blk2rec, S->cap_blk, nblk))) return e;
@@ -1947,6 +2007,8 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
                                            S->d_sblk, snblk, slen, S->d_status);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemsetAsync(S->d_status + 2, 0, 4, s));   // the job list restarts (pairs continue)
+        k_status_pass<<<1, 64, 0, s>>>(S->d_status);   // the continuations restart too
+        HIPCHK(c, hipGetLastError());
         Dedup dd2 = dd;
         dd2.jepoch = S->epoch + 1;
         const uint8_t *SA = S->d_sarena;
@@ -1979,6 +2041,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     k_hits_finalize<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8)), 256, 0, s>>>(
         S->d_start, n, out, hit_ids, hit_cap, S->d_status);
     HIPCHK(c, hipGetLastError());
+    if ((e = commit())) return e;
     if (mark(4)) return GM_E_HIP;
     return GM_OK;
 }
@@ -1993,14 +2056,23 @@ int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     const Generation *g = c->gen;
     if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
+    S->replay.valid = false;
     if (in->n == 0) { HIPCHK(c, hipMemsetAsync(S->d_status, 0, BATCH_STATUS_WORDS * 4, s)); S->ev_pending = false; return GM_OK; }
     if (((uintptr_t)in->arena & 15) || ((uintptr_t)in->reqs & 15) || ((uintptr_t)out & 15))
         return fail(c, GM_E_INVAL, "reqs / arena / out must be 16-byte aligned");
     if (hit_cap > 0xFFFFFFFFull) hit_cap = 0xFFFFFFFFull;   // hit offsets are u32
+    DoneGuard G(S);
+    Scratch::Replay &rp = S->replay;
+    rp.gen = g; rp.seq = c->publish_seq; rp.n = in->n; rp.alen = in->arena_len;
+    rp.h_out = nullptr; rp.h_hits = nullptr; rp.h_hit_cap = 0;
     if (!(in->flags & GM_BATCH_HOST)) {
         const int e = run_batch(c, S, g, in->reqs, in->arena, in->arena_len, in->n, out, hit_ids, hit_ids ? hit_cap : 0,
                                 in->arena_len_dev);
-        return e ? e : mark_done(c, S);
+        if (e) return e;
+        rp.reqs = in->reqs; rp.A = in->arena; rp.out = out; rp.hits = hit_ids; rp.hit_cap = hit_ids ? hit_cap : 0;
+        rp.dlen = in->arena_len_dev;
+        rp.valid = true;
+        return G.done(c);
     }
     // host buffers: stage reqs + arena + verdicts + hits through HBM (PCIe both ways)
     size_t rq = (size_t)in->n * sizeof(gm_req), ar = (in->arena_len + 255) & ~255ull;
@@ -2020,7 +2092,10 @@ int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit
     if (e) return e;
     HIPCHK(c, hipMemcpyAsync(out, dv, vo, hipMemcpyDeviceToHost, s));
     if (hit_ids && hit_cap) HIPCHK(c, hipMemcpyAsync(hit_ids, dh, ho, hipMemcpyDeviceToHost, s));
-    return mark_done(c, S);
+    rp.reqs = dr; rp.A = da; rp.out = dv; rp.hits = dh; rp.hit_cap = hit_ids ? hit_cap : 0; rp.dlen = nullptr;
+    rp.h_out = out; rp.h_hits = hit_ids; rp.h_hit_cap = hit_ids ? hit_cap : 0;
+    rp.valid = true;
+    return G.done(c);
 }
 
 int gm_sync(gm_ctx *c, void *stream) {
@@ -2030,39 +2105,65 @@ int gm_sync(gm_ctx *c, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     Scratch *S = scratch_for(c, s);
     if (!S) return fail(c, GM_E_NOMEM, t_err);
-    HIPCHK(c, hipMemcpyAsync(S->h_status, S->d_status, STATUS_WORDS * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    {
-        std::lock_guard<std::mutex> lk(c->last_mu);
-        memcpy(c->last_status, S->h_status, STATUS_WORDS * 4);
-        c->last_candidates = S->h_status[6];
-        c->last_ctx_pass = S->h_status[7];
-        c->last_jobs = S->h_status[2];
-        c->last_pairs = S->h_status[1];
-        c->last_hits = S->h_status[4];
-        if (S->ev_pending) {
-            for (int k = 0; k < 4; k++) {
-                c->last_ms[k] = 0;
-                if (k + 1 < S->ev_used) (void)hipEventElapsedTime(&c->last_ms[k], S->ev[k], S->ev[k + 1]);
+    uint32_t ov;
+    for (;;) {
+        HIPCHK(c, hipMemcpyAsync(S->h_status, S->d_status, STATUS_WORDS * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        {
+            std::lock_guard<std::mutex> lk(c->last_mu);
+            memcpy(c->last_status, S->h_status, STATUS_WORDS * 4);
+            c->last_candidates = S->h_status[6];
+            c->last_ctx_pass = S->h_status[7];
+            c->last_jobs = S->h_status[2];
+            c->last_pairs = S->h_status[1];
+            c->last_hits = S->h_status[4];
+            if (S->ev_pending) {
+                for (int k = 0; k < 4; k++) {
+                    c->last_ms[k] = 0;
+                    if (k + 1 < S->ev_used) (void)hipEventElapsedTime(&c->last_ms[k], S->ev[k], S->ev[k + 1]);
+                }
+                // stage 0 = the route on the side stream (its own time); stage 1 = the scan
+                if (S->route_side) (void)hipEventElapsedTime(&c->last_ms[0], S->ev_route[0], S->ev_route[1]);
+                S->ev_pending = false;
             }
-            // stage 0 = the route on the side stream (its own time); stage 1 = the scan
-            if (S->route_side) (void)hipEventElapsedTime(&c->last_ms[0], S->ev_route[0], S->ev_route[1]);
-            S->ev_pending = false;
         }
+        ov = S->h_status[3];
+        // the next batch on this stream gets twice the buffer that overflowed (bounded)
+        if ((ov & OV_CAND) && S->cand_mult < 64) S->cand_mult *= 2;
+        if ((ov & OV_SURV) && S->surv_mult < 64) S->surv_mult *= 2;
+        const uint32_t list_before = S->list_mult;
+        if ((ov & (OV_PAIRS | OV_JOBS | OV_SET)) && S->list_mult < 64) S->list_mult *= 2;
+        // the dedupe set overflowed (more unique hits + regex jobs than its sizing, e.g. an attack
+        // burst): the batch is re-run here with the set doubled -- its counters were not committed
+        // (k_ctr_commit) -- until it fits, so the caller sees a whole batch
+        Scratch::Replay &rp = S->replay;
+        if (!(ov & OV_SET) || !rp.valid || S->list_mult == list_before) break;
+        std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+        if (c->gen != rp.gen || c->publish_seq != rp.seq) {
+            rp.valid = false;
+            return fail(c, GM_E_OVERFLOW, "WAF dedupe set full and the generation changed before the batch could be "
+                                          "re-run: retry it");
+        }
+        c->n_set_reruns++;
+        DoneGuard G(S);
+        int e = run_batch(c, S, c->gen, rp.reqs, rp.A, rp.alen, rp.n, rp.out, rp.hits, rp.hit_cap, rp.dlen);
+        if (e) { rp.valid = false; return e; }
+        if (rp.h_out) {
+            HIPCHK(c, hipMemcpyAsync(rp.h_out, rp.out, (size_t)rp.n * sizeof(gm_verdict), hipMemcpyDeviceToHost, s));
+            if (rp.h_hits && rp.h_hit_cap)
+                HIPCHK(c, hipMemcpyAsync(rp.h_hits, rp.hits, rp.h_hit_cap * 4, hipMemcpyDeviceToHost, s));
+        }
+        if ((e = G.done(c))) { rp.valid = false; return e; }
     }
-    const uint32_t ov = S->h_status[3];
-    // the next batch on this stream gets twice the buffer that overflowed (bounded)
-    if ((ov & OV_CAND) && S->cand_mult < 64) S->cand_mult *= 2;
-    if ((ov & OV_SURV) && S->surv_mult < 64) S->surv_mult *= 2;
-    if ((ov & (OV_PAIRS | OV_JOBS | OV_SET)) && S->list_mult < 64) S->list_mult *= 2;
+    S->replay.valid = false;
     if (S->h_status[PARSE_STATUS_WORD + 3]) return fail(c, GM_E_OVERFLOW, "gm_parse_requests: arena capacity exceeded");
     if (S->h_status[UPURI_STATUS_WORD]) return fail(c, GM_E_OVERFLOW, "gm_upstream_uris: output capacity exceeded");
-    if (ov & OV_HITS) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded");
+    if (ov & OV_HITS) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded (the batch's counters were not committed)");
     // candidate / survivor / pair / job overflows were completed on the device (k_waf_direct, the
     // set-based scatter and regex runs): the batch is whole, the buffers grow for speed
-    if (ov & OV_SET) return fail(c, GM_E_OVERFLOW, "WAF dedupe set full (> 6 unique hits + regex jobs per request); "
-                                                   "it is doubled for the stream's next batch: retry it");
-    if (ov & 64u) return fail(c, GM_E_OVERFLOW, "decoded-view arena capacity exceeded");
+    if (ov & OV_SET) return fail(c, GM_E_OVERFLOW, "WAF dedupe set full at its largest size (64x: > ~380 unique hits + "
+                                                   "regex jobs per request); the batch's counters were not committed");
+    if (ov & OV_DEC) return fail(c, GM_E_OVERFLOW, "decoded-view arena capacity exceeded");
     return GM_OK;
 }
 
@@ -2118,20 +2219,51 @@ int gm_comm_init(gm_ctx *c, const void *uid, int nranks, int rank) {
     return GM_OK;
 }
 
+// The ranks' agreement on the counter space before the sum: every rank contributes
+// {gen, n, 0xFFFFFFFF - gen, 0xFFFFFFFF - n} to one MAX reduction, which yields the largest and
+// (by complement) the smallest gen and n over the ranks; they agree iff the two are equal.  All
+// ranks see the same reduced words, so all take the same branch: on a disagreement none issues
+// the sum (mismatched element counts would hang or corrupt the collective).
+static void agree_pack(uint64_t gen, uint64_t n, unsigned long long w[4]) {
+    w[0] = gen & 0xFFFFFFFFu; w[1] = n & 0xFFFFFFFFu;
+    w[2] = 0xFFFFFFFFull - w[0]; w[3] = 0xFFFFFFFFull - w[1];
+}
+static bool agree_check(const unsigned long long m[4]) {
+    return m[0] == 0xFFFFFFFFull - m[2] && m[1] == 0xFFFFFFFFull - m[3];
+}
+
 // Out of place: the cumulative local counters stay this device's own; their sum over the ranks
 // goes to the generation's reduced buffer (gm_counters_global).  Any number of calls give the
 // true totals (an in-place reduction of cumulative counters would add them up again each time).
+// First the ranks agree on (gen, n_counters) -- GM_E_COMM when one rank runs another generation.
 int gm_counters_allreduce(gm_ctx *c, void *stream) {
     if (!c || !c->comm) return fail(c, GM_E_COMM, "gm_comm_init not called");
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     if (!c->gen || !c->gen->d_counters) return fail(c, GM_E_NOGEN, "no counters");
     HIPCHK(c, hipSetDevice(c->dev));
-    Scratch *S = scratch_for(c, (hipStream_t)stream);
+    hipStream_t s = (hipStream_t)stream;
+    Scratch *S = scratch_for(c, s);
     if (!S) return fail(c, GM_E_NOMEM, t_err);
-    ncclResult_t r = ncclAllReduce(c->gen->d_counters, c->gen->d_counters_sum, std::max<size_t>(c->gen->n_counters, 1),
-                                   ncclUint64, ncclSum, c->comm, (hipStream_t)stream);
+    DoneGuard G(S);
+    if (!S->d_agree) {
+        HIPCHK(c, hipMalloc((void **)&S->d_agree, 4 * 8));
+        HIPCHK(c, hipHostMalloc((void **)&S->h_agree, 4 * 8, hipHostMallocDefault));
+    }
+    agree_pack(c->gen->stats.gen, c->gen->n_counters, S->h_agree);
+    HIPCHK(c, hipMemcpyAsync(S->d_agree, S->h_agree, 4 * 8, hipMemcpyHostToDevice, s));
+    ncclResult_t r = ncclAllReduce(S->d_agree, S->d_agree, 4, ncclUint64, ncclMax, c->comm, s);
+    if (r != ncclSuccess) return fail(c, GM_E_COMM, std::string("ncclAllReduce (agreement): ") + ncclGetErrorString(r));
+    HIPCHK(c, hipMemcpyAsync(S->h_agree, S->d_agree, 4 * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (!agree_check(S->h_agree))
+        return fail(c, GM_E_COMM, "ranks disagree on the generation or its counter space (gen " +
+                                      std::to_string(0xFFFFFFFFull - S->h_agree[2]) + ".." + std::to_string(S->h_agree[0]) +
+                                      ", counters " + std::to_string(0xFFFFFFFFull - S->h_agree[3]) + ".." +
+                                      std::to_string(S->h_agree[1]) + "): no reduction issued");
+    r = ncclAllReduce(c->gen->d_counters, c->gen->d_counters_sum, std::max<size_t>(c->gen->n_counters, 1),
+                      ncclUint64, ncclSum, c->comm, s);
     if (r != ncclSuccess) return fail(c, GM_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-    return mark_done(c, S);
+    return G.done(c);
 }
 
 }  // extern "C"
@@ -2145,6 +2277,22 @@ extern "C" int gm_debug_waf_keys(gm_ctx *c, uint32_t *out, size_t cap) {
     for (uint32_t i = 0; i < h.n_lit_buckets_cap; i++)
         if (b[i].count) { if (k < cap) out[k] = b[i].key; k++; }
     return (int)k;
+}
+
+// gm_counters_allreduce's agreement protocol, exposed for the world-size-2 gloo test
+extern "C" void gm_debug_agree_pack(uint64_t gen, uint64_t n, uint64_t *w4) {
+    unsigned long long w[4];
+    agree_pack(gen, n, w);
+    for (int k = 0; k < 4; k++) w4[k] = w[k];
+}
+extern "C" int gm_debug_agree_check(const uint64_t *max4) {
+    const unsigned long long m[4] = {max4[0], max4[1], max4[2], max4[3]};
+    return agree_check(m) ? GM_OK : GM_E_COMM;
+}
+
+extern "C" void gm_debug_update_hook(void (*fn)(void *), void *arg) {
+    g_update_hook = fn;
+    g_update_hook_arg = arg;
 }
 
 extern "C" int gm_debug_inet(const uint8_t *text, size_t n, char *out, size_t cap) {
@@ -2439,9 +2587,10 @@ extern "C" int gm_peers_init(gm_ctx *c, gm_peer_state *state, uint32_t n_peers, 
     if (!state) return fail(c, GM_E_INVAL, "null state");
     Scratch *S = scratch_for(c, (hipStream_t)stream);
     if (!S) return fail(c, GM_E_NOMEM, t_err);
+    DoneGuard G(S);
     k_peers_init<<<std::min<uint32_t>((n_peers + 255) / 256, 1024), 256, 0, (hipStream_t)stream>>>(g->tab, state);
     HIPCHK(c, hipGetLastError());
-    return mark_done(c, S);
+    return G.done(c);
 }
 
 // NGINX Plus keeps a kept server's runtime state across an API update: new_state[j] = the state
@@ -2472,10 +2621,11 @@ extern "C" int gm_peers_migrate(gm_ctx *c, const gm_peer_state *old_state, uint3
     if ((const void *)old_state == (const void *)new_state) return fail(c, GM_E_INVAL, "migrate in place");
     Scratch *S = scratch_for(c, (hipStream_t)stream);
     if (!S) return fail(c, GM_E_NOMEM, t_err);
+    DoneGuard G(S);
     k_peers_migrate<<<std::min<uint32_t>((new_n + 255) / 256, 1024), 256, 0, (hipStream_t)stream>>>(
         old_state, g->d_peer_map, g->tab.peer_init, new_n, new_state);
     HIPCHK(c, hipGetLastError());
-    return mark_done(c, S);
+    return G.done(c);
 }
 
 extern "C" int gm_select_peers(gm_ctx *c, const gm_batch *in, const gm_verdict *verdicts, gm_peer_state *state,
@@ -2490,6 +2640,7 @@ extern "C" int gm_select_peers(gm_ctx *c, const gm_batch *in, const gm_verdict *
     hipStream_t s = (hipStream_t)stream;
     Scratch *S = scratch_for(c, s);
     if (!S) return fail(c, GM_E_NOMEM, t_err);
+    DoneGuard G(S);
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     const Generation *g = c->gen;
     if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
@@ -2529,7 +2680,7 @@ extern "C" int gm_select_peers(gm_ctx *c, const gm_batch *in, const gm_verdict *
             peer_out, n, state, t.n_peers, 1);
         HIPCHK(c, hipGetLastError());
     }
-    return mark_done(c, S);
+    return G.done(c);
 }
 
 extern "C" int gm_release_peers(gm_ctx *c, const uint32_t *peer_ids, uint32_t n, gm_peer_state *state,
@@ -2545,10 +2696,11 @@ extern "C" int gm_release_peers(gm_ctx *c, const uint32_t *peer_ids, uint32_t n,
     if (!peer_ids || !state) return fail(c, GM_E_INVAL, "null argument");
     Scratch *S = scratch_for(c, (hipStream_t)stream);
     if (!S) return fail(c, GM_E_NOMEM, t_err);
+    DoneGuard G(S);
     k_peer_count<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 4095) / 4096, (uint32_t)c->cu_count * 2)), 256, 0,
                    (hipStream_t)stream>>>(peer_ids, n, state, n_peers, -1);
     HIPCHK(c, hipGetLastError());
-    return mark_done(c, S);
+    return G.done(c);
 }
 
 extern "C" int gm_peer_address(gm_ctx *c, uint32_t peer, char *buf, size_t cap, uint32_t *upstream_id) {
@@ -2581,6 +2733,7 @@ extern "C" int gm_upstream_uris(gm_ctx *c, const gm_batch *in, const gm_verdict 
     hipStream_t s = (hipStream_t)stream;
     Scratch *S = scratch_for(c, s);
     if (!S) return fail(c, GM_E_NOMEM, t_err);
+    DoneGuard G(S);
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     const Generation *g = c->gen;
     if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
@@ -2598,5 +2751,5 @@ extern "C" int gm_upstream_uris(gm_ctx *c, const gm_batch *in, const gm_verdict 
     k_upuri_emit<<<blocks, 256, 0, s>>>(in->reqs, in->arena, verdicts, n, g->tab, out_off, out, out_cap, out_len,
                                         S->d_status + UPURI_STATUS_WORD);
     HIPCHK(c, hipGetLastError());
-    return mark_done(c, S);
+    return G.done(c);
 }

@@ -20,6 +20,8 @@ LIB_PATH = os.environ.get("GM_LIB") or os.path.join(os.path.dirname(HERE), "libg
 GM_OK = 0
 GM_ABI_VERSION = 7   # include/gpumatch.h
 GM_E_OVERFLOW = -4
+GM_E_STALE = -9
+GM_E_COMM = -7
 GM_CREATE_COMPILE_ONLY = 0x1
 GM_BATCH_HOST = 0x1
 
@@ -44,6 +46,10 @@ GM_CREATE_PROFILE = 0x2
 GM_CREATE_SERIAL = 0x4
 
 
+def GM_CREATE_SET_SHIFT(k: int) -> int:
+    return (k & 0xFF) << 16
+
+
 def GM_CREATE_SCRATCH_SHIFT(k: int) -> int:
     """Test hook: the internal WAF buffers at 2^-k of their default capacity (include/gpumatch.h)."""
     return (k & 0xFF) << 8
@@ -53,7 +59,8 @@ class GmStats(ctypes.Structure):
     _fields_ = ([(f, ctypes.c_uint32) for f in STATS_FIELDS] + [(f, ctypes.c_uint64) for f in STATS_FIELDS64] +
                 [(f, ctypes.c_float) for f in STATS_FIELDS_MS] +
                 [(f, ctypes.c_uint32) for f in STATS_FIELDS_WAF] +
-                [("scratch_scale", ctypes.c_float), ("reserved_stats", ctypes.c_uint32 * 5)])
+                [("scratch_scale", ctypes.c_float), ("n_set_reruns", ctypes.c_uint32),
+                 ("set_shift", ctypes.c_uint32), ("reserved_stats", ctypes.c_uint32 * 3)])
 
 
 class GmBatch(ctypes.Structure):
@@ -134,10 +141,11 @@ class Engine:
     """One context per HIP device (one process per GPU)."""
 
     def __init__(self, device: int = 0, compile_only: bool = False, profile: bool = False, serial: bool = False,
-                 scratch_shift: int = 0):
+                 scratch_shift: int = 0, set_shift: int = 0):
         L = lib()
         fl = (GM_CREATE_COMPILE_ONLY if compile_only else 0) | (GM_CREATE_PROFILE if profile else 0) | \
-             (GM_CREATE_SERIAL if serial else 0) | GM_CREATE_SCRATCH_SHIFT(scratch_shift)
+             (GM_CREATE_SERIAL if serial else 0) | GM_CREATE_SCRATCH_SHIFT(scratch_shift) | \
+             GM_CREATE_SET_SHIFT(set_shift)
         self.h = L.gm_create(device, fl)
         if not self.h:
             raise GmError(-1, L.gm_last_error(None).decode())
@@ -167,6 +175,8 @@ class Engine:
         self._chk(lib().gm_stats(self.h, ctypes.byref(s)))
         d = {f: getattr(s, f) for f in STATS_FIELDS + STATS_FIELDS64 + STATS_FIELDS_MS + STATS_FIELDS_WAF}
         d["scratch_scale"] = s.scratch_scale
+        d["n_set_reruns"] = s.n_set_reruns
+        d["set_shift"] = s.set_shift
         return d
 
     def rejects(self) -> list:

@@ -46,6 +46,21 @@ def server_addrs(u: int) -> list:
     return [_addr(u, j) for j in range(UPSTREAMS[u][1])]
 
 
+def plus_order(old: list, new: list) -> list:
+    """The server order of an upstream after an NGINX Plus API update from `old` to `new`
+    (Manager.UpdateServersInPlus, manager.go:257-284 -> UpdateHTTPServers: the servers not listed
+    are deleted, the new ones added, each appended to the peer list): the kept servers in their
+    previous relative order, then the added ones in the order given -- gm_update_upstream's rule
+    (parity-unpinned against a live Plus: no reference fixture covers the order)."""
+    left = list(new)
+    kept = []
+    for a in old:
+        if a in left:
+            left.remove(a)
+            kept.append(a)
+    return kept + left
+
+
 def conf_text(method: str | None = None, servers: dict | None = None, upstreams=None) -> str:
     """``method``: one LBMethod for every upstream (e.g. the default "random two least_conn").
     ``servers``: {upstream index: [address, ...]} -- the server list an NGINX Plus API update

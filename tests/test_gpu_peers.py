@@ -157,7 +157,7 @@ def test_plus_endpoint_update_and_migration(torch_dev):
         old_state = g.state_np()
         old_n = g.n_peers
         g.e.update_upstream(peers.upstream_name(u), sv)
-        servers[u] = sv
+        servers[u] = peers.plus_order(servers.get(u, peers.server_addrs(u)), sv)
         st = g.e.stats()
         assert st["gen"] == 1   # configVersion unchanged by a Plus API update
         new_n = st["n_peers"]

@@ -190,6 +190,78 @@ def test_normalize_after_overflow_syncs_clean(torch_dev):
     assert [out[16 * i:16 * i + int(ol[i])] for i in range(len(paths))] == [b"/a/c", b"/x/y", b"/A/"]
 
 
+# ---------------------------------------------------------------- counters: whole batches only
+# a batch's location and rule hits accumulate in per-batch scratch and are committed
+# by k_ctr_commit only when the batch is whole -- a void batch (hit_cap too small) adds nothing, so
+# the caller's retry counts each request once (internal/metrics/collectors/manager.go:27-59).
+def _one_batch_counters(e, got, gh):
+    st = e.stats()
+    nl = st["n_locations"]
+    loc = got["location_id"][got["location_id"] != 0xFFFFFFFF]
+    return np.concatenate([np.bincount(loc, minlength=nl),
+                           np.bincount(gh, minlength=st["n_sigs"])]).astype(np.uint64)
+
+
+def test_void_batch_commits_no_counters(torch_dev):
+    ss = workloads.c4_sigset(400, 100)
+    reqs, arena = records.gen_c4(20_000, ss, plant_rate=0.3, pool_mb=4)
+    b = workloads.c4_blob(ss, "monitoring")
+    e = engine.Engine(0)
+    e.load(b, 3)
+    for _ in range(2):   # the overflowing call, twice: nothing committed
+        with pytest.raises(engine.GmError) as ei:
+            e.match_host(reqs, arena, hit_cap=10)
+        assert ei.value.code == engine.GM_E_OVERFLOW
+        assert not e.counters().any()
+    got, gh = e.match_host(reqs, arena)   # the retry with room: one batch's counts
+    assert len(gh) > 10
+    assert np.array_equal(e.counters(), _one_batch_counters(e, got, gh))
+    exp, eh = Oracle(b, 3).match(reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "retry after a void batch")
+
+
+@pytest.mark.parametrize("host", [True, False])
+def test_set_overflow_reruns_whole_batch(torch_dev, host):
+    """a dedupe-set overflow (OV_SET: more unique hits + regex jobs than the set holds --
+    an attack burst) no longer voids the batch.  With the set shrunk (GM_CREATE_SET_SHIFT) the first
+    run overflows it; gm_sync re-runs the batch with the set doubled until it fits and returns GM_OK:
+    verdicts and hits equal the oracle's, and the counters hold exactly one batch."""
+    torch, dev = torch_dev
+    ss, b = workloads.c4_stress_generation()
+    reqs, arena = records.gen_c4(6_000, ss, seed=workloads.C4_STRESS_POOL_SEED + 9, plant_rate=0.3, stress=True)
+    probe = engine.Engine(0)
+    probe.load(b, 5)
+    probe.match_host(reqs, arena)
+    st = probe.stats()
+    keys = st["last_pairs"] + st["last_jobs"]
+    probe.close()
+    assert keys > 2048, keys
+    # the default set for 6000 requests holds 2^19 slots; shrink it below the keys but within
+    # reach of the re-runs' doubling (x64 at most)
+    shift = 1
+    while (1 << 19) >> (shift + 1) >= keys // 2 and shift < 12:
+        shift += 1
+    e = engine.Engine(0, set_shift=shift)
+    e.load(b, 5)
+    if host:
+        got, gh = e.match_host(reqs, arena)   # no GmError
+    else:
+        d_reqs, d_arena = _to_dev(torch, dev, reqs, arena)
+        n = len(reqs)
+        d_out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+        d_hits = torch.zeros(8 * n + 1024, dtype=torch.int32, device=dev)
+        e.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), len(arena), n, d_out.data_ptr(), d_hits.data_ptr(),
+                    d_hits.numel(), 0)
+        e.sync(0)
+        got = d_out.cpu().numpy().view(records.VERDICT_DTYPE)
+        gh = d_hits[:e.stats()["last_hits"]].cpu().numpy().view(np.uint32)
+    st = e.stats()
+    assert st["n_set_reruns"] >= 1 and st["set_shift"] == shift, st
+    exp, eh = Oracle(b, 5).match(reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, f"set overflow re-run (shift {shift})")
+    assert np.array_equal(e.counters(), _one_batch_counters(e, got, gh))
+
+
 # ---------------------------------------------------------------- internal overflow completes
 # VERDICT r2: a batch that overflows an internal WAF buffer must complete on the device.  The
 # scan's candidate regions and the context filter's survivor regions are finished by

@@ -177,3 +177,52 @@ def test_two_rank_gloo_c5_stream_matches_single_process(tmp_path):
     for step in (1, 2):
         assert np.array_equal(np.load(tmp_path / f"c5_counters_{step}.npy"), step * one)
     assert one.sum() > C5_STREAM // 10   # about half the stream is plain http: redirected before a location
+
+
+# ---------------------------------------------------------------- generation agreement
+# gm_counters_allreduce first reduces {gen, n_counters, 0xFFFFFFFF - gen, 0xFFFFFFFF - n} with
+# MAX over the ranks and issues the counter sum only if the largest and smallest agree
+# (libgpumatch's agreement words, gm_debug_agree_pack / gm_debug_agree_check; gloo is the
+# transport here, RCCL on the GPU).  Ranks on different generations must all return GM_E_COMM
+# without issuing the sum -- never hang in a collective of mismatched size.
+def _agree_rank(rank, world, port, out_dir, gens):
+    import ctypes
+    from gpumatch import engine
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    L = engine.lib()
+    L.gm_debug_agree_pack.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+    L.gm_debug_agree_check.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+    results = []
+    for gen, blob in gens[rank]:
+        e = engine.Engine(compile_only=True)
+        e.load(blob, gen)
+        st = e.stats()
+        w = (ctypes.c_uint64 * 4)()
+        L.gm_debug_agree_pack(st["gen"], st["n_counters"], w)
+        t = torch.tensor(list(w), dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        m = (ctypes.c_uint64 * 4)(*[int(x) for x in t.tolist()])
+        rc = L.gm_debug_agree_check(m)
+        if rc == 0:   # agreed: the counter sum has the same length on every rank
+            c = torch.ones(st["n_counters"], dtype=torch.int64)
+            dist.all_reduce(c, op=dist.ReduceOp.SUM)
+            results.append((rc, int(c[0])))
+        else:
+            results.append((rc, -1))
+        e.close()
+    np.save(os.path.join(out_dir, f"agree_{rank}.npy"), np.array(results, dtype=np.int64))
+    dist.destroy_process_group()
+
+
+def test_two_rank_generation_agreement(tmp_path):
+    from gpumatch import engine
+    a = workloads.c4_blob(workloads.c4_sigset(400, 100), "monitoring")
+    b = workloads.c4_blob(workloads.c4_sigset(300, 50), "monitoring")   # another counter space
+    gens = {0: [(1, a), (2, a), (3, a), (4, a)],
+            1: [(1, a), (3, a), (3, b), (4, a)]}
+    mp.spawn(_agree_rank, args=(2, _free_port(), str(tmp_path), gens), nprocs=2, join=True)
+    r0, r1 = np.load(tmp_path / "agree_0.npy"), np.load(tmp_path / "agree_1.npy")
+    assert np.array_equal(r0, r1)   # every rank takes the same branch
+    assert r0[:, 0].tolist() == [0, engine.GM_E_COMM, engine.GM_E_COMM, 0]
+    assert r0[0, 1] == 2 and r0[3, 1] == 2

@@ -313,7 +313,7 @@ def test_oracle_state_accounting(pblob):
 # Configurator.UpdateEndpoints* push servers through Manager.UpdateServersInPlus with no reload
 # (configurator.go:442,467,489; manager.go:257-284): gm_update_upstream patches the live tables'
 # upstream section.  Its peer tables must equal a fresh compile of the config a reload with the
-# new server lines would have rendered.
+# new server lines would have rendered, in NGINX Plus's order (peers.plus_order: kept servers first).
 def _addresses(e):
     st = e.stats()
     return [e.peer_address(p) for p in range(st["n_peers"])]
@@ -331,11 +331,17 @@ def test_update_upstream_equals_fresh_compile(pblob, u, servers):
     e.load(pblob, 4)
     e.update_upstream(peers.upstream_name(u), servers)
     f = engine.Engine(compile_only=True)
-    f.load(peers.peers_blob(servers={u: servers}), 4)
+    f.load(peers.peers_blob(servers={u: peers.plus_order(peers.server_addrs(u), servers)}), 4)
     se, sf = e.stats(), f.stats()
     for k in ("gen", "n_peers", "n_upstreams", "n_upstreams_deferred", "n_counters", "n_locations"):
         assert se[k] == sf[k], k
     assert _addresses(e) == _addresses(f)
+
+
+def test_plus_order():
+    assert peers.plus_order(["a", "b", "c"], ["d", "c", "a"]) == ["a", "c", "d"]
+    assert peers.plus_order(["a", "b"], ["b", "b", "e"]) == ["b", "b", "e"]
+    assert peers.plus_order(["a"], []) == []
 
 
 def test_update_upstream_unknown_name(pblob):
@@ -345,3 +351,37 @@ def test_update_upstream_unknown_name(pblob):
     with pytest.raises(engine.GmError):
         e.update_upstream("no-such-upstream", ["10.0.0.1:80"])
     assert e.stats()["n_peers"] == n0   # the live tables stay
+
+
+def test_update_upstream_racing_a_load_is_refused(pblob):
+    """a gm_load_generation that publishes between gm_update_upstream's read of the live
+    tables and its publish must not be undone -- the update fails GM_E_STALE (the reference's
+    verifyConfigVersion refusal, manager.go:258) and the loaded generation stays live."""
+    import ctypes
+    e = engine.Engine(compile_only=True)
+    e.load(pblob, 4)
+    other = peers.peers_blob(servers={1: ["10.55.0.1:80", "10.55.0.2:80"]})
+    L = engine.lib()
+    calls = []
+
+    @ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+    def hook(_arg):
+        if not calls:
+            calls.append(1)
+            e.load(other, 5)
+    L.gm_debug_update_hook.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    L.gm_debug_update_hook(ctypes.cast(hook, ctypes.c_void_p), None)
+    try:
+        with pytest.raises(engine.GmError) as ei:
+            e.update_upstream(peers.upstream_name(9), ["10.9.9.9:80"])
+        assert ei.value.code == engine.GM_E_STALE
+        f = engine.Engine(compile_only=True)
+        f.load(other, 5)
+        assert e.stats()["gen"] == 5
+        assert _addresses(e) == _addresses(f)   # the reload's tables, not the stale update's
+        # re-issued against the new generation, the update goes through
+        e.update_upstream(peers.upstream_name(9), ["10.9.9.9:80"])
+        assert e.stats()["gen"] == 5
+        assert [a for a, _ in _addresses(e)].count("10.9.9.9:80") == 1
+    finally:
+        L.gm_debug_update_hook(None, None)
