@@ -782,7 +782,7 @@ struct Compiler {
     int rules_route(const Server &S, const std::string &var) {
         const MapIR &m = M.maps.at(var);
         std::vector<std::string> chains;
-        if (!var_list(m.src, chains) || chains.size() > 8) return -1;
+        if (!var_list(m.src, chains) || chains.size() > RULES_CHAINS_MAX) return -1;
         DRules r{};
         r.first_chain = (uint32_t)chain_heads.size();
         r.n_chains = (uint32_t)chains.size();
@@ -810,6 +810,26 @@ struct Compiler {
         }
         int64_t dt = m.has_default ? target(S, m.def) : (int64_t)GM_NONE;
         if (dt == -2) return -1;
+        if (chains.size() > RULES_TABLE_MAX) {
+            // too many chains for a 2^n truth table: the map's params as conditions over the
+            // chains' '0'/'1' string, evaluated on the device in ngx_http_map_find's order (the
+            // exact keys, then the regexes in config order); DRules.pad[0] = the first
+            r.table_off = GM_NONE;
+            r.pad[0] = (uint32_t)conds.size();
+            std::vector<DCond> pc;
+            for (size_t k = 0; k < m.params.size(); k++) {
+                DCond c{};
+                if (m.params[k].rx) {
+                    const int d = regex(m.params[k].key, m.params[k].rxi);
+                    if (d < 0) return -1;
+                    c.is_regex = 1; c.dfa = (uint32_t)d;
+                } else {
+                    c.key_off = put_bytes(m.params[k].key); c.key_len = (uint32_t)m.params[k].key.size();
+                }
+                pc.push_back(c);
+            }
+            conds.insert(conds.end(), pc.begin(), pc.end());
+        } else {
         // truth table over the chains' 0/1 outcomes (ngx_http_map_find: hash, then regexes)
         r.table_off = (uint32_t)rtab.size();
         for (uint32_t b = 0; b < (1u << chains.size()); b++) {
@@ -821,6 +841,7 @@ struct Compiler {
             for (size_t k = 0; k < m.params.size() && res < 0; k++)
                 if (m.params[k].rx && !s.empty() && dfa_search(rx[k], (const uint8_t *)s.data(), s.size())) res = (int)k;
             rtab.push_back(res < 0 ? 0xFF : (uint8_t)res);
+        }
         }
         for (auto h : heads) chain_heads.push_back(h);
         r.first_target = (uint32_t)rtargets.size();
@@ -1621,7 +1642,10 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                     if (M.splits.count(vv[0])) { route = C.split_route(S, vv[0]); kind = LK_IRL_SPLIT; }
                     else if (M.maps.count(vv[0])) { route = C.rules_route(S, vv[0]); kind = LK_IRL_RULES; }
                 }
-                if (route < 0) { dl.kind = LK_UNSUPPORTED; st.n_rejected_other++; }
+                if (route < 0) {
+                    dl.kind = LK_UNSUPPORTED; st.n_rejected_other++;
+                    R.rejects.push_back("location " + L.path + ": error_page 418 = " + L.err418 + " (map / split not modelled)");
+                }
                 else { dl.kind = kind; dl.route = (uint32_t)route; }
                 if (kind == LK_IRL_SPLIT && route >= 0) st.n_routes_split++;
                 if (kind == LK_IRL_RULES && route >= 0) st.n_routes_rules++;

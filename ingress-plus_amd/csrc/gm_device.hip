@@ -848,7 +848,23 @@ __device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, co
         }
         if (nd == NEXT_1) bits |= 1u << ch;
     }
-    return t.rtab[R.table_off + bits];
+    if (R.table_off != GM_NONE) return t.rtab[R.table_off + bits];
+    // more chains than a truth table holds: ngx_http_map_find over the '0'/'1' string -- the
+    // exact keys first, then the regexes in config order
+    uint8_t sb[RULES_CHAINS_MAX];
+    for (uint32_t ch = 0; ch < R.n_chains; ch++) sb[ch] = (bits >> ch) & 1u ? '1' : '0';
+    Val sv;
+    sv.clear();
+    sv.add(sb, R.n_chains);
+    for (uint32_t k = 0; k < R.n_targets; k++) {
+        const DCond cd = t.conds[R.pad[0] + k];
+        if (!cd.is_regex && val_eq(sv, t.bytes + cd.key_off, cd.key_len, false)) return (int)k;
+    }
+    for (uint32_t k = 0; k < R.n_targets; k++) {
+        const DCond cd = t.conds[R.pad[0] + k];
+        if (cd.is_regex && dfa_run_val(t, cd.dfa, sv)) return (int)k;
+    }
+    return 0xFF;
 }
 
 // split_clients: murmur2 of the source -> part index (0xFF none, 0xFFFFFFFF unsupported value)

@@ -175,6 +175,9 @@ struct DCond {
     int32_t  next_true, next_false;
     uint32_t pad;
 };
+// a rules map of <= RULES_TABLE_MAX chains is a 2^n truth table; up to RULES_CHAINS_MAX its
+// params are conditions over the chains' '0'/'1' string (table_off = GM_NONE, pad[0]: first DCond)
+constexpr uint32_t RULES_TABLE_MAX = 8, RULES_CHAINS_MAX = 32;
 struct DRules {
     uint32_t first_chain, n_chains;  // chain head node ids in DChainHead[]
     uint32_t table_off;              // 2^n_chains entries (uint8 result index, 0xFF = default)

@@ -144,6 +144,32 @@ def test_realip_random_parity(eng, header, rec):
     assert (v["match_idx"] != 0xFF).sum() > 500
 
 
+def test_rules_route_many_chains(eng):
+    """A VirtualServer rules route with more (match, condition) chains than a truth table holds
+    (RULES_TABLE_MAX = 8): 9 matches x 2 conditions = 18 chains, the final map evaluated on the
+    device as ngx_http_map_find does (exact keys, then regexes in order) over the chains' string."""
+    rng = np.random.Generator(np.random.PCG64(17))
+    addrs = ["192.168.0.7", "10.1.0.1", "172.16.5.5", "2001:db8::7"]
+    matches = []
+    for k in range(9):
+        matches.append({"values": [addrs[k % 4] if k < 8 else "~^1", "~^(%d|%d)" % (k, k + 1)],
+                        "upstream": f"u{k + 1}"})
+    ups = [{"name": f"u{k}", "service": f"svc{k}", "port": 80} for k in range(10)]
+    vs = {"metadata": {"name": "m", "namespace": "default"},
+          "spec": {"host": "m.example.com", "upstreams": ups,
+                   "routes": [{"path": "/", "rules": {"conditions": [{"variable": "$remote_addr"},
+                                                                     {"header": "X-Pick"}],
+                                                      "matches": matches, "defaultUpstream": "u0"}}]}}
+    b = SC._vs_blob(vs)
+    items = _rand_requests(20_000, "m.example.com", 29)
+    for it in items:
+        it["headers"] = it["headers"] + [("X-Pick", str(int(rng.integers(0, 12))))]
+    v = _both(eng, b, items)
+    st = eng.stats()
+    assert st["n_routes_rules"] == 1 and st["n_rejected_other"] == 0, eng.rejects()
+    assert len(set(v["match_idx"].tolist())) >= 6
+
+
 def _peer_pair(e, b, items, gen=4):
     import torch
     dev = torch.device("cuda", 0)
