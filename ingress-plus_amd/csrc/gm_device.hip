@@ -102,6 +102,9 @@ __device__ void realip_eval(Ctx &c, const GTab &t);
 // rip: the server's realip settings -- evaluated here, at the top of the out-of-line step that
 // needs the request's variables, where little else is live (called from deep inside the variable
 // lookup, the call chain raised the route kernel's register allocation past its occupancy target)
+// RIP = false: the caller's kernel was instantiated for a generation without realip (k_route's
+// RIP template parameter), so realip_eval -- a register-heavy step -- is not in its call graph
+template <bool RIP = true>
 __device__ __forceinline__ void ctx_init(Ctx &c, const uint8_t *A, const Rec &r, const GTab *t = nullptr,
                                          uint32_t rip = GM_NONE) {
     c.A = A; c.r = r;
@@ -110,7 +113,7 @@ __device__ __forceinline__ void ctx_init(Ctx &c, const uint8_t *A, const Rec &r,
     c.body = o; o += r.body_len; c.host = o; o += r.host_len; c.method = o; o += r.method_len;
     c.ruri = o; o += r.ruri_len; c.raddr = o;
     c.rip = rip; c.rip_state = RIPS_SAME;
-    if (rip != GM_NONE) realip_eval(c, *t);
+    if (RIP && rip != GM_NONE) realip_eval(c, *t);
 }
 
 // exact per-byte flags (bit 7 of each byte) of the zero bytes of x
@@ -328,10 +331,10 @@ __device__ void get_var(Ctx &c, const GTab &t, uint32_t src_id, Val &v) {
 // in place, so this rare step does not raise the route kernel's register allocation)
 // out-of-line leaves: each keeps its own small register frame, so the call chain under
 // realip_eval stays under the route kernel's occupancy target
-__device__ __noinline__ bool d_parse_addr_port(const uint8_t *p, uint32_t n, InetAddr &a) { return ngx_parse_addr_port(p, n, a); }
-__device__ __noinline__ uint32_t d_parse_addr(const uint8_t *p, uint32_t n, uint8_t *b) { return ngx_parse_addr(p, n, b); }
-__device__ __noinline__ uint32_t d_addr_text(const InetAddr &a, uint8_t *out) { return ngx_addr_text(a, out); }
-__device__ __noinline__ bool rip_trusted(const GTab &t, const DRealIp *R, const InetAddr &a) {
+__device__ __forceinline__ bool d_parse_addr_port(const uint8_t *p, uint32_t n, InetAddr &a) { return ngx_parse_addr_port(p, n, a); }
+__device__ __forceinline__ uint32_t d_parse_addr(const uint8_t *p, uint32_t n, uint8_t *b) { return ngx_parse_addr(p, n, b); }
+__device__ __forceinline__ uint32_t d_addr_text(const InetAddr &a, uint8_t *out) { return ngx_addr_text(a, out); }
+__device__ __forceinline__ bool rip_trusted(const GTab &t, const DRealIp *R, const InetAddr &a) {
     if (!a.fam) return false;
     for (uint32_t k = 0; k < R->n_cidr; k++) {
         const DCidr *c = t.cidrs + R->first_cidr + k;
@@ -360,6 +363,47 @@ __device__ __forceinline__ int rip_forwarded(const GTab &t, const DRealIp *R, co
         return RIP_OK;
     }
 }
+// the k-th (0-based) header line named `want`: its value span; false if none
+__device__ __forceinline__ bool hdr_nth(const Ctx &c, const uint8_t *want, uint32_t wl, uint32_t k, uint64_t &vs, uint32_t &vl) {
+    HdrIt it{c.hdrs, c.hdrs + c.r.hdr_len};
+    uint64_t ns; uint32_t nl;
+    uint32_t seen = 0;
+    while (hdr_next(c.A, it, ns, nl, vs, vl))
+        if (hdr_name_ci(c.A, ns, nl, want, wl) && seen++ == k) return true;
+    return false;
+}
+__device__ __forceinline__ uint32_t hdr_count(const Ctx &c, const uint8_t *want, uint32_t wl) {
+    HdrIt it{c.hdrs, c.hdrs + c.r.hdr_len};
+    uint64_t ns, vs; uint32_t nl, vl;
+    uint32_t nh = 0;
+    while (hdr_next(c.A, it, ns, nl, vs, vl)) nh += hdr_name_ci(c.A, ns, nl, want, wl);
+    return nh;
+}
+// every X-Forwarded-For line, the last first (nginx's headers_in.x_forwarded_for array)
+__device__ __forceinline__ int rip_xfwd(Ctx &c, const GTab &t, const DRealIp *R) {
+    const uint8_t *want = (const uint8_t *)"x-forwarded-for";
+    const uint32_t nh = hdr_count(c, want, 15);
+    int rc = RIP_DECLINED;
+    bool found = false;
+    for (uint32_t k = nh; k-- > 0;) {
+        uint64_t vs; uint32_t vl;
+        hdr_nth(c, want, 15, k, vs, vl);
+        rc = rip_forwarded(t, R, c.A + vs, vl, c.ra, c.ra_tmp);
+        if (!R->recursive) break;
+        if (rc == RIP_DECLINED && found) { rc = RIP_DONE; break; }
+        if (rc != RIP_OK) break;
+        found = true;
+    }
+    return rc;
+}
+// X-Real-IP or a named header: its first line
+__device__ __forceinline__ int rip_one_header(Ctx &c, const GTab &t, const DRealIp *R) {
+    const bool xr = R->type == RIP_XREALIP;
+    uint64_t vs; uint32_t vl;
+    if (!hdr_nth(c, xr ? (const uint8_t *)"x-real-ip" : t.bytes + R->hdr_off, xr ? 9u : R->hdr_len, 0, vs, vl))
+        return RIP_DECLINED;
+    return rip_forwarded(t, R, c.A + vs, vl, c.ra, c.ra_tmp);
+}
 __device__ __noinline__ void realip_eval(Ctx &c, const GTab &t) {
     const DRealIp *R = t.realip + c.rip;
     const uint8_t *A = c.A;
@@ -373,31 +417,7 @@ __device__ __noinline__ void realip_eval(Ctx &c, const GTab &t) {
         if (rip_trusted(t, R, a)) c.rip_state = RIPS_UNKNOWN;
         return;
     }
-    int rc = RIP_DECLINED;
-    HdrIt it{c.hdrs, c.hdrs + c.r.hdr_len};
-    uint64_t ns, vs; uint32_t nl, vl;
-    if (type == RIP_XFWD) {
-        // every X-Forwarded-For line, the last first (nginx's headers_in.x_forwarded_for array)
-        uint32_t nh = 0;
-        while (hdr_next(A, it, ns, nl, vs, vl)) nh += hdr_name_ci(A, ns, nl, (const uint8_t *)"x-forwarded-for", 15);
-        bool found = false;
-        for (uint32_t k = nh; k-- > 0;) {
-            HdrIt j{c.hdrs, c.hdrs + c.r.hdr_len};
-            uint32_t seen = 0;
-            while (hdr_next(A, j, ns, nl, vs, vl))
-                if (hdr_name_ci(A, ns, nl, (const uint8_t *)"x-forwarded-for", 15) && seen++ == k) break;
-            rc = rip_forwarded(t, R, A + vs, vl, a, c.ra_tmp);
-            if (!R->recursive) break;
-            if (rc == RIP_DECLINED && found) { rc = RIP_DONE; break; }
-            if (rc != RIP_OK) break;
-            found = true;
-        }
-    } else {
-        const uint8_t *want = type == RIP_XREALIP ? (const uint8_t *)"x-real-ip" : t.bytes + R->hdr_off;
-        const uint32_t wl = type == RIP_XREALIP ? 9u : R->hdr_len;
-        while (hdr_next(A, it, ns, nl, vs, vl))
-            if (hdr_name_ci(A, ns, nl, want, wl)) { rc = rip_forwarded(t, R, A + vs, vl, a, c.ra_tmp); break; }
-    }
+    const int rc = type == RIP_XFWD ? rip_xfwd(c, t, R) : rip_one_header(c, t, R);
     if (rc == RIP_DECLINED) return;
     c.ra_len = d_addr_text(a, c.ra_txt);
     c.rip_state = RIPS_NEW;
@@ -790,12 +810,13 @@ __device__ __noinline__ uint32_t host_wildcards(const uint8_t *h, int hl, const 
 // lane-private arrays only exist on these paths (scratch), never on the host/URI fast path.
 // server rewrite `if` on a request variable: 1 hit, 0 miss
 // (-1: the variable's value is unknown to the engine -- the request defers)
+template <bool RIP>
 __device__ __noinline__ int server_if_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t if_idx,
                                              uint32_t rip) {
     const Rec r = load_rec(rp);
     const DServerIf f = t.server_ifs[if_idx];
     Ctx c;
-    ctx_init(c, A, r, &t, rip);
+    ctx_init<RIP>(c, A, r, &t, rip);
     Val v;
     get_var(c, t, f.src, v);
     if (v.unknown) return -1;
@@ -808,12 +829,13 @@ __device__ __noinline__ int server_if_generic(const uint8_t *A, const gm_req *rp
 
 // rules route (compiled map chains) -> result index (0xFF default; -1 a condition read a value the
 // engine cannot know)
+template <bool RIP>
 __device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t rules_idx,
                                           uint32_t rip) {
     const Rec r = load_rec(rp);
     const DRules R = t.rules[rules_idx];
     Ctx c;
-    ctx_init(c, A, r, &t, rip);
+    ctx_init<RIP>(c, A, r, &t, rip);
     Val v;
     // header / cookie / argument values are looked up once per request, not once per condition
     // that reads them (every match of a rules route repeats the route's conditions); variables
@@ -868,12 +890,13 @@ __device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, co
 }
 
 // split_clients: murmur2 of the source -> part index (0xFF none, 0xFFFFFFFF unsupported value)
+template <bool RIP>
 __device__ __noinline__ uint32_t split_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t split_idx,
                                                uint32_t rip) {
     const Rec r = load_rec(rp);
     const DSplit Sp = t.splits[split_idx];
     Ctx c;
-    ctx_init(c, A, r, &t, rip);
+    ctx_init<RIP>(c, A, r, &t, rip);
     Val v;
     get_var(c, t, Sp.src, v);
     if (v.unknown) return 0xFFFFFFFFu;
@@ -910,12 +933,14 @@ constexpr uint32_t RLOC_STATUS_WORD = 16;   // batch status word: requests defer
 // (URI <= RLOC_URI_CAP, n_rloc <= RLOC_BM_BITS) sets *pend and returns; >= -1 -- k_rloc's answer
 // (the location index, -1 none).  *sid_out: the server chosen (valid whenever *pend is set).
 constexpr int32_t RK_INLINE = -3, RK_DEFER = -2;
+template <bool RIP>
 __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
                           RouteOut &o, uint32_t blen, uint32_t rflags);
 // client_max_body_size exceeded: 413, nothing proxied, no WAF phase
 __device__ __forceinline__ void too_large(RouteOut &o) {
     o.action = GM_ACT_TOO_LARGE; o.status = 413; o.ups = GM_NONE; o.waf = GM_WAF_OFF;
 }
+template <bool RIP>
 __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const RoutePre &pre,
                           const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb, int32_t rk_in = RK_INLINE,
                           bool *pend = nullptr) {
@@ -963,7 +988,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
         else if (f.op == SIF_FLAGS) hit = (f.tt >> (r.flags & 3)) & 1u;
         else if (f.op == 0xFF) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; return; }
         else {
-            const int g = server_if_generic(A, rp, *t.self, S.first_if + i, S.realip);
+            const int g = server_if_generic<RIP>(A, rp, *t.self, S.first_if + i, S.realip);
             if (g < 0) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; return; }
             hit = g != 0;
         }
@@ -1054,7 +1079,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
             if (loc < 0) loc = best;
         }
     }
-    route_loc(A, rp, t, h, loc, o, r.body_len, r.flags);
+    route_loc<RIP>(A, rp, t, h, loc, o, r.body_len, r.flags);
 }
 
 // The rest of route_one once the location is known (loc < 0: none): location kinds, rules and
@@ -1064,6 +1089,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
 // server's limit when none) before that location's rewrite phase (ngx_http_core_find_config_phase);
 // a chunked body only when it is read -- by the proxying location, the final one after an
 // internal redirect (the chunked body filter)
+template <bool RIP>
 __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
                           RouteOut &o, uint32_t blen, uint32_t rflags) {
     const bool chunked = rflags & GM_REQ_CHUNKED;
@@ -1077,14 +1103,14 @@ __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, co
     uint32_t fin = (uint32_t)loc;
     if (L.kind == LK_IRL_RULES) {
         const DRules R = t.rules[L.route];
-        const int idx = rules_generic(A, rp, *t.self, L.route, h.servers[o.server].realip);
+        const int idx = rules_generic<RIP>(A, rp, *t.self, L.route, h.servers[o.server].realip);
         o.kind = GM_ROUTE_RULES;
         if (idx < 0) { o.action = GM_ACT_UNSUPPORTED; return; }
         o.match = (uint8_t)idx;
         fin = idx == 0xFF ? R.default_target : t.rtargets[R.first_target + idx];
     } else if (L.kind == LK_IRL_SPLIT) {
         o.kind = GM_ROUTE_SPLIT;
-        const uint32_t k = split_generic(A, rp, *t.self, L.route, h.servers[o.server].realip);
+        const uint32_t k = split_generic<RIP>(A, rp, *t.self, L.route, h.servers[o.server].realip);
         if (k == 0xFFFFFFFFu) { o.action = GM_ACT_UNSUPPORTED; return; }
         fin = GM_NONE;
         if (k != 0xFFu) { o.bucket = (uint8_t)k; fin = t.parts[t.splits[L.route].first_part + k].target; }
@@ -1136,7 +1162,9 @@ inline uint32_t route_lds(const GTab &t, bool beside) { return route_hot16(t) + 
 // u: its $uri's first 32 bytes (two uint4; the slices' first two 16-byte steps read them instead
 // of an arena line each)
 struct RlocQ { uint2 *list; uint32_t *count; int32_t *loc; uint4 *st; int32_t *best; uint4 *u; };
-template <int WPE, bool RK = false, bool TAIL = false>
+// RIP: the generation configures realip (gm_stats_t.n_realip): only then is the realip step in the
+// kernel's call graph (its registers would raise every instantiation's allocation)
+template <int WPE, bool RK = false, bool TAIL = false, bool RIP = false>
 __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_route(const gm_req *__restrict__ reqs, uint32_t n,
                                                        const uint8_t *__restrict__ A, uint64_t arena_len,
                                                        GTab tg, gm_verdict *__restrict__ out,
@@ -1195,11 +1223,11 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
             o.server = e.y; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0; o.action = GM_ACT_NO_LISTENER;
             o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF; o.pend_best = -1;
             const uint32_t *rw = reinterpret_cast<const uint32_t *>(reqs + i);   // body_len, flags
-            route_loc(A, reqs + i, t, h, loc, o, rw[5], rw[9] & 0xFF);
+            route_loc<RIP>(A, reqs + i, t, h, loc, o, rw[5], rw[9] & 0xFF);
         } else {
             r = load_rec(reqs + i);
             route_prefetch(A, arena_len, r, pre);
-            route_one(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
+            route_one<RIP>(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
                       RK && q.list ? RK_DEFER : RK_INLINE, &pend);
         }
         if (RK && !TAIL) {   // deferred to k_rloc: appended, one atomic per wave
@@ -1556,7 +1584,10 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
         }
         // the route's hot tables + location histogram (route_lds)
         const void *routes[] = {(const void *)k_route<3, true, true>, (const void *)k_route<3, true>,
-                                (const void *)k_route<3>, (const void *)k_route<GM_ROUTE_WPE, true>, (const void *)k_route<GM_ROUTE_WPE>};
+                                (const void *)k_route<3>, (const void *)k_route<GM_ROUTE_WPE, true>, (const void *)k_route<GM_ROUTE_WPE>,
+                                (const void *)k_route<3, true, true, true>, (const void *)k_route<3, true, false, true>,
+                                (const void *)k_route<3, false, false, true>, (const void *)k_route<GM_ROUTE_WPE, true, false, true>,
+                                (const void *)k_route<GM_ROUTE_WPE, false, false, true>};
         for (const void *f : routes)
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)(ROUTE_STAGE_BYTES + 4 * LDS_HIST_ALONE)) != hipSuccess) {
@@ -1770,6 +1801,13 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     const GTab &t = g->tab;
     const bool waf = t.n_sigs > 0 && (t.n_lits > 0 || t.n_sig_regex > 0);
     const uint32_t nblk = (uint32_t)((alen >> BLK_SHIFT) + 1);
+    // the route instantiation with the realip step only for a generation that configures realip
+    const bool rip_gen = g->stats.n_realip > 0;
+#define GM_ROUTE_LAUNCH(W, RKV, TAILV, GRID, LDS, STRM, ...)                                               \
+    do {                                                                                                   \
+        if (rip_gen) k_route<W, RKV, TAILV, true><<<GRID, ROUTE_BLOCK, LDS, STRM>>>(__VA_ARGS__);          \
+        else k_route<W, RKV, TAILV, false><<<GRID, ROUTE_BLOCK, LDS, STRM>>>(__VA_ARGS__);                 \
+    } while (0)
     const bool prof = c->flags & GM_CREATE_PROFILE;
     auto mark = [&](int k) -> int {
         if (prof) { HIPCHK(c, hipEventRecord(S->ev[k], s)); S->ev_used = k + 1; S->ev_pending = true; }
@@ -1838,14 +1876,14 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         }
         if (t.n_rk_prefilter)
             k_rloc<<<(uint32_t)c->cu_count * 4, RLOC_BLOCK, 0, rs>>>(reqs, A, alen, t, q.list, q.count, q.loc, dlen);
-        k_route<3, true, true><<<tail_blocks, ROUTE_BLOCK, route_lds(t, false), rs>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk,
-                                                                    nullptr, 0, dlen, route_hist_n(t, false), q);
+        GM_ROUTE_LAUNCH(3, true, true, tail_blocks, route_lds(t, false), rs, reqs, n, A, alen, t, out, ctr, nullptr, nblk,
+                        nullptr, 0, dlen, route_hist_n(t, false), q);
         HIPCHK(c, hipGetLastError());
         return GM_OK;
     };
     if (!waf) {
-        if (rk) k_route<3, true><<<route_blocks, ROUTE_BLOCK, route_lds(t, false), s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), q);
-        else k_route<3><<<route_blocks, ROUTE_BLOCK, route_lds(t, false), s>>>(reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false));
+        if (rk) GM_ROUTE_LAUNCH(3, true, false, route_blocks, route_lds(t, false), s, reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), q);
+        else GM_ROUTE_LAUNCH(3, false, false, route_blocks, route_lds(t, false), s, reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), RlocQ{});
         HIPCHK(c, hipGetLastError());
         if (rk) {
             const int e4 = launch_rloc(s, route_blocks);
@@ -1935,9 +1973,9 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         // raised issue priority beside the scan: the route's short latency-bound waves finish
         // early instead of stretching past the scan
         if (rk)
-            k_route<GM_ROUTE_WPE, true><<<nb, ROUTE_BLOCK, route_lds(t, !serial), rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial), q);
+            GM_ROUTE_LAUNCH(GM_ROUTE_WPE, true, false, nb, route_lds(t, !serial), rs, reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial), q);
         else
-            k_route<GM_ROUTE_WPE><<<nb, ROUTE_BLOCK, route_lds(t, !serial), rs>>>(reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial));
+            GM_ROUTE_LAUNCH(GM_ROUTE_WPE, false, false, nb, route_lds(t, !serial), rs, reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial), RlocQ{});
         HIPCHK(c, hipGetLastError());
         int e3;
         if (rk && (e3 = launch_rloc(rs, nb))) return e3;

@@ -12,7 +12,7 @@ fi
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in "$@"; do
     if [ "$v" = main ]; then lib=""; else lib="$GRAFT_REPO_ROOT/exp/$v/libgpumatch.so"; fi
-    GM_LIB=$lib timeout -k 10 300 python -u bench.py --no-cpu --stress-requests 0 ${BENCH_ARGS} > gpurun_out/ab_${TAG}_${v}_$r.log 2>&1
+    GM_LIB=$lib timeout -k 10 300 python -u bench.py --no-cpu --stress-requests 0 --allow-nondefault-build ${BENCH_ARGS} > gpurun_out/ab_${TAG}_${v}_$r.log 2>&1
     rc=$?
     [ $rc -eq 0 ] || { tail -5 gpurun_out/ab_${TAG}_${v}_$r.log; exit $rc; }
     python3 - "$v" "gpurun_out/ab_${TAG}_${v}_$r.log" <<'PY'
