@@ -102,9 +102,6 @@ __device__ void realip_eval(Ctx &c, const GTab &t);
 // rip: the server's realip settings -- evaluated here, at the top of the out-of-line step that
 // needs the request's variables, where little else is live (called from deep inside the variable
 // lookup, the call chain raised the route kernel's register allocation past its occupancy target)
-// RIP = false: the caller's kernel was instantiated for a generation without realip (k_route's
-// RIP template parameter), so realip_eval -- a register-heavy step -- is not in its call graph
-template <bool RIP = true>
 __device__ __forceinline__ void ctx_init(Ctx &c, const uint8_t *A, const Rec &r, const GTab *t = nullptr,
                                          uint32_t rip = GM_NONE) {
     c.A = A; c.r = r;
@@ -113,7 +110,7 @@ __device__ __forceinline__ void ctx_init(Ctx &c, const uint8_t *A, const Rec &r,
     c.body = o; o += r.body_len; c.host = o; o += r.host_len; c.method = o; o += r.method_len;
     c.ruri = o; o += r.ruri_len; c.raddr = o;
     c.rip = rip; c.rip_state = RIPS_SAME;
-    if (RIP && rip != GM_NONE) realip_eval(c, *t);
+    if (rip != GM_NONE) realip_eval(c, *t);
 }
 
 // exact per-byte flags (bit 7 of each byte) of the zero bytes of x
@@ -331,10 +328,13 @@ __device__ void get_var(Ctx &c, const GTab &t, uint32_t src_id, Val &v) {
 // in place, so this rare step does not raise the route kernel's register allocation)
 // out-of-line leaves: each keeps its own small register frame, so the call chain under
 // realip_eval stays under the route kernel's occupancy target
-__device__ __forceinline__ bool d_parse_addr_port(const uint8_t *p, uint32_t n, InetAddr &a) { return ngx_parse_addr_port(p, n, a); }
-__device__ __forceinline__ uint32_t d_parse_addr(const uint8_t *p, uint32_t n, uint8_t *b) { return ngx_parse_addr(p, n, b); }
-__device__ __forceinline__ uint32_t d_addr_text(const InetAddr &a, uint8_t *out) { return ngx_addr_text(a, out); }
-__device__ __forceinline__ bool rip_trusted(const GTab &t, const DRealIp *R, const InetAddr &a) {
+// (out of line: realip_eval's own frame stays small -- a leaf holding all of them needs ~100
+// VGPRs, which sets the route kernel's allocation above its target beside the scan)
+#define GM_RIP_INL __noinline__
+__device__ GM_RIP_INL bool d_parse_addr_port(const uint8_t *p, uint32_t n, InetAddr &a) { return ngx_parse_addr_port(p, n, a); }
+__device__ GM_RIP_INL uint32_t d_parse_addr(const uint8_t *p, uint32_t n, uint8_t *b) { return ngx_parse_addr(p, n, b); }
+__device__ GM_RIP_INL uint32_t d_addr_text(const InetAddr &a, uint8_t *out) { return ngx_addr_text(a, out); }
+__device__ GM_RIP_INL bool rip_trusted(const GTab &t, const DRealIp *R, const InetAddr &a) {
     if (!a.fam) return false;
     for (uint32_t k = 0; k < R->n_cidr; k++) {
         const DCidr *c = t.cidrs + R->first_cidr + k;
@@ -346,7 +346,7 @@ __device__ __forceinline__ bool rip_trusted(const GTab &t, const DRealIp *R, con
 // ngx_http_get_forwarded_addr_internal over one header value, its recursion as a loop:
 // 0 declined (a unchanged), 1 ok, 2 done (a = the last address taken); na: scratch
 constexpr int RIP_DECLINED = 0, RIP_OK = 1, RIP_DONE = 2;
-__device__ __forceinline__ int rip_forwarded(const GTab &t, const DRealIp *R, const uint8_t *x, uint32_t len, InetAddr &a,
+__device__ GM_RIP_INL int rip_forwarded(const GTab &t, const DRealIp *R, const uint8_t *x, uint32_t len, InetAddr &a,
                                           InetAddr &na) {
     for (int depth = 0;; depth++) {
         if (!rip_trusted(t, R, a) || len == 0) return depth ? RIP_DONE : RIP_DECLINED;
@@ -364,7 +364,7 @@ __device__ __forceinline__ int rip_forwarded(const GTab &t, const DRealIp *R, co
     }
 }
 // the k-th (0-based) header line named `want`: its value span; false if none
-__device__ __forceinline__ bool hdr_nth(const Ctx &c, const uint8_t *want, uint32_t wl, uint32_t k, uint64_t &vs, uint32_t &vl) {
+__device__ GM_RIP_INL bool hdr_nth(const Ctx &c, const uint8_t *want, uint32_t wl, uint32_t k, uint64_t &vs, uint32_t &vl) {
     HdrIt it{c.hdrs, c.hdrs + c.r.hdr_len};
     uint64_t ns; uint32_t nl;
     uint32_t seen = 0;
@@ -372,7 +372,7 @@ __device__ __forceinline__ bool hdr_nth(const Ctx &c, const uint8_t *want, uint3
         if (hdr_name_ci(c.A, ns, nl, want, wl) && seen++ == k) return true;
     return false;
 }
-__device__ __forceinline__ uint32_t hdr_count(const Ctx &c, const uint8_t *want, uint32_t wl) {
+__device__ GM_RIP_INL uint32_t hdr_count(const Ctx &c, const uint8_t *want, uint32_t wl) {
     HdrIt it{c.hdrs, c.hdrs + c.r.hdr_len};
     uint64_t ns, vs; uint32_t nl, vl;
     uint32_t nh = 0;
@@ -380,7 +380,7 @@ __device__ __forceinline__ uint32_t hdr_count(const Ctx &c, const uint8_t *want,
     return nh;
 }
 // every X-Forwarded-For line, the last first (nginx's headers_in.x_forwarded_for array)
-__device__ __forceinline__ int rip_xfwd(Ctx &c, const GTab &t, const DRealIp *R) {
+__device__ GM_RIP_INL int rip_xfwd(Ctx &c, const GTab &t, const DRealIp *R) {
     const uint8_t *want = (const uint8_t *)"x-forwarded-for";
     const uint32_t nh = hdr_count(c, want, 15);
     int rc = RIP_DECLINED;
@@ -397,7 +397,7 @@ __device__ __forceinline__ int rip_xfwd(Ctx &c, const GTab &t, const DRealIp *R)
     return rc;
 }
 // X-Real-IP or a named header: its first line
-__device__ __forceinline__ int rip_one_header(Ctx &c, const GTab &t, const DRealIp *R) {
+__device__ GM_RIP_INL int rip_one_header(Ctx &c, const GTab &t, const DRealIp *R) {
     const bool xr = R->type == RIP_XREALIP;
     uint64_t vs; uint32_t vl;
     if (!hdr_nth(c, xr ? (const uint8_t *)"x-real-ip" : t.bytes + R->hdr_off, xr ? 9u : R->hdr_len, 0, vs, vl))
@@ -810,13 +810,12 @@ __device__ __noinline__ uint32_t host_wildcards(const uint8_t *h, int hl, const 
 // lane-private arrays only exist on these paths (scratch), never on the host/URI fast path.
 // server rewrite `if` on a request variable: 1 hit, 0 miss
 // (-1: the variable's value is unknown to the engine -- the request defers)
-template <bool RIP>
 __device__ __noinline__ int server_if_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t if_idx,
                                              uint32_t rip) {
     const Rec r = load_rec(rp);
     const DServerIf f = t.server_ifs[if_idx];
     Ctx c;
-    ctx_init<RIP>(c, A, r, &t, rip);
+    ctx_init(c, A, r, &t, rip);
     Val v;
     get_var(c, t, f.src, v);
     if (v.unknown) return -1;
@@ -829,13 +828,12 @@ __device__ __noinline__ int server_if_generic(const uint8_t *A, const gm_req *rp
 
 // rules route (compiled map chains) -> result index (0xFF default; -1 a condition read a value the
 // engine cannot know)
-template <bool RIP>
 __device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t rules_idx,
                                           uint32_t rip) {
     const Rec r = load_rec(rp);
     const DRules R = t.rules[rules_idx];
     Ctx c;
-    ctx_init<RIP>(c, A, r, &t, rip);
+    ctx_init(c, A, r, &t, rip);
     Val v;
     // header / cookie / argument values are looked up once per request, not once per condition
     // that reads them (every match of a rules route repeats the route's conditions); variables
@@ -890,13 +888,12 @@ __device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, co
 }
 
 // split_clients: murmur2 of the source -> part index (0xFF none, 0xFFFFFFFF unsupported value)
-template <bool RIP>
 __device__ __noinline__ uint32_t split_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t split_idx,
                                                uint32_t rip) {
     const Rec r = load_rec(rp);
     const DSplit Sp = t.splits[split_idx];
     Ctx c;
-    ctx_init<RIP>(c, A, r, &t, rip);
+    ctx_init(c, A, r, &t, rip);
     Val v;
     get_var(c, t, Sp.src, v);
     if (v.unknown) return 0xFFFFFFFFu;
@@ -933,14 +930,16 @@ constexpr uint32_t RLOC_STATUS_WORD = 16;   // batch status word: requests defer
 // (URI <= RLOC_URI_CAP, n_rloc <= RLOC_BM_BITS) sets *pend and returns; >= -1 -- k_rloc's answer
 // (the location index, -1 none).  *sid_out: the server chosen (valid whenever *pend is set).
 constexpr int32_t RK_INLINE = -3, RK_DEFER = -2;
-template <bool RIP>
 __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
-                          RouteOut &o, uint32_t blen, uint32_t rflags);
+                          RouteOut &o);
+// the request's body length and whether it is chunked, re-read from its record where the 413
+// check needs them (kept in registers across the location walk they cost the route spills)
+__device__ __forceinline__ uint32_t req_body_len(const gm_req *rp) { return reinterpret_cast<const uint32_t *>(rp)[5]; }
+__device__ __forceinline__ bool req_chunked(const gm_req *rp) { return reinterpret_cast<const uint32_t *>(rp)[9] & GM_REQ_CHUNKED; }
 // client_max_body_size exceeded: 413, nothing proxied, no WAF phase
 __device__ __forceinline__ void too_large(RouteOut &o) {
     o.action = GM_ACT_TOO_LARGE; o.status = 413; o.ups = GM_NONE; o.waf = GM_WAF_OFF;
 }
-template <bool RIP>
 __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const RoutePre &pre,
                           const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb, int32_t rk_in = RK_INLINE,
                           bool *pend = nullptr) {
@@ -988,7 +987,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
         else if (f.op == SIF_FLAGS) hit = (f.tt >> (r.flags & 3)) & 1u;
         else if (f.op == 0xFF) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; return; }
         else {
-            const int g = server_if_generic<RIP>(A, rp, *t.self, S.first_if + i, S.realip);
+            const int g = server_if_generic(A, rp, *t.self, S.first_if + i, S.realip);
             if (g < 0) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; return; }
             hit = g != 0;
         }
@@ -1061,7 +1060,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
             // (the location found is the redirect's target: its client_max_body_size is checked
             // before the redirect, ngx_http_core_find_config_phase)
             o.loc = (uint32_t)far;
-            if (!(r.flags & GM_REQ_CHUNKED) && r.body_len > h.locs[far].body_max) too_large(o);
+            if (!req_chunked(rp) && req_body_len(rp) > h.locs[far].body_max) too_large(o);
             else { o.action = GM_ACT_AUTO_301; o.status = 301; }
             return;
         }
@@ -1079,7 +1078,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
             if (loc < 0) loc = best;
         }
     }
-    route_loc<RIP>(A, rp, t, h, loc, o, r.body_len, r.flags);
+    route_loc(A, rp, t, h, loc, o);
 }
 
 // The rest of route_one once the location is known (loc < 0: none): location kinds, rules and
@@ -1089,10 +1088,10 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
 // server's limit when none) before that location's rewrite phase (ngx_http_core_find_config_phase);
 // a chunked body only when it is read -- by the proxying location, the final one after an
 // internal redirect (the chunked body filter)
-template <bool RIP>
 __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
-                          RouteOut &o, uint32_t blen, uint32_t rflags) {
-    const bool chunked = rflags & GM_REQ_CHUNKED;
+                          RouteOut &o) {
+    const uint32_t blen = req_body_len(rp);
+    const bool chunked = req_chunked(rp);
     if (loc < 0) {
         if (!chunked && blen > h.servers[o.server].body_max) { too_large(o); return; }
         o.action = GM_ACT_NOT_FOUND; o.status = 404; return;
@@ -1103,14 +1102,14 @@ __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, co
     uint32_t fin = (uint32_t)loc;
     if (L.kind == LK_IRL_RULES) {
         const DRules R = t.rules[L.route];
-        const int idx = rules_generic<RIP>(A, rp, *t.self, L.route, h.servers[o.server].realip);
+        const int idx = rules_generic(A, rp, *t.self, L.route, h.servers[o.server].realip);
         o.kind = GM_ROUTE_RULES;
         if (idx < 0) { o.action = GM_ACT_UNSUPPORTED; return; }
         o.match = (uint8_t)idx;
         fin = idx == 0xFF ? R.default_target : t.rtargets[R.first_target + idx];
     } else if (L.kind == LK_IRL_SPLIT) {
         o.kind = GM_ROUTE_SPLIT;
-        const uint32_t k = split_generic<RIP>(A, rp, *t.self, L.route, h.servers[o.server].realip);
+        const uint32_t k = split_generic(A, rp, *t.self, L.route, h.servers[o.server].realip);
         if (k == 0xFFFFFFFFu) { o.action = GM_ACT_UNSUPPORTED; return; }
         fin = GM_NONE;
         if (k != 0xFFu) { o.bucket = (uint8_t)k; fin = t.parts[t.splits[L.route].first_part + k].target; }
@@ -1162,9 +1161,7 @@ inline uint32_t route_lds(const GTab &t, bool beside) { return route_hot16(t) + 
 // u: its $uri's first 32 bytes (two uint4; the slices' first two 16-byte steps read them instead
 // of an arena line each)
 struct RlocQ { uint2 *list; uint32_t *count; int32_t *loc; uint4 *st; int32_t *best; uint4 *u; };
-// RIP: the generation configures realip (gm_stats_t.n_realip): only then is the realip step in the
-// kernel's call graph (its registers would raise every instantiation's allocation)
-template <int WPE, bool RK = false, bool TAIL = false, bool RIP = false>
+template <int WPE, bool RK = false, bool TAIL = false>
 __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_route(const gm_req *__restrict__ reqs, uint32_t n,
                                                        const uint8_t *__restrict__ A, uint64_t arena_len,
                                                        GTab tg, gm_verdict *__restrict__ out,
@@ -1222,12 +1219,11 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
             if (loc < 0) loc = q.best[x];
             o.server = e.y; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0; o.action = GM_ACT_NO_LISTENER;
             o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF; o.pend_best = -1;
-            const uint32_t *rw = reinterpret_cast<const uint32_t *>(reqs + i);   // body_len, flags
-            route_loc<RIP>(A, reqs + i, t, h, loc, o, rw[5], rw[9] & 0xFF);
+            route_loc(A, reqs + i, t, h, loc, o);
         } else {
             r = load_rec(reqs + i);
             route_prefetch(A, arena_len, r, pre);
-            route_one<RIP>(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
+            route_one(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
                       RK && q.list ? RK_DEFER : RK_INLINE, &pend);
         }
         if (RK && !TAIL) {   // deferred to k_rloc: appended, one atomic per wave
@@ -1584,10 +1580,7 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
         }
         // the route's hot tables + location histogram (route_lds)
         const void *routes[] = {(const void *)k_route<3, true, true>, (const void *)k_route<3, true>,
-                                (const void *)k_route<3>, (const void *)k_route<GM_ROUTE_WPE, true>, (const void *)k_route<GM_ROUTE_WPE>,
-                                (const void *)k_route<3, true, true, true>, (const void *)k_route<3, true, false, true>,
-                                (const void *)k_route<3, false, false, true>, (const void *)k_route<GM_ROUTE_WPE, true, false, true>,
-                                (const void *)k_route<GM_ROUTE_WPE, false, false, true>};
+                                (const void *)k_route<3>, (const void *)k_route<GM_ROUTE_WPE, true>, (const void *)k_route<GM_ROUTE_WPE>};
         for (const void *f : routes)
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)(ROUTE_STAGE_BYTES + 4 * LDS_HIST_ALONE)) != hipSuccess) {
@@ -1721,7 +1714,7 @@ static constexpr uint32_t kBuildFlags =
     defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_SCAN_NOBRANCH) || defined(GM_SCAN_VMASK)
     GM_BUILD_EXPERIMENT |
 #endif
-#if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != 32 || \
+#if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 4 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != 32 || \
     GM_ROUTE_BPC != 2 || GM_ROUTE_PRIO != 0 || GM_ROUTE_WPE != GM_ROUTE_WPE_SHIPPED || GM_EXP_GRIDMUL != 8 || \
     GM_EXP_WPE != 3 || GM_RLOC_CTX != 1 || GM_RLOC_PREF != 0 || GM_ALW_SLICE_GROUPS != 8 || GM_WIRE_WPE != 8 || \
     GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1
@@ -1801,13 +1794,8 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     const GTab &t = g->tab;
     const bool waf = t.n_sigs > 0 && (t.n_lits > 0 || t.n_sig_regex > 0);
     const uint32_t nblk = (uint32_t)((alen >> BLK_SHIFT) + 1);
-    // the route instantiation with the realip step only for a generation that configures realip
-    const bool rip_gen = g->stats.n_realip > 0;
-#define GM_ROUTE_LAUNCH(W, RKV, TAILV, GRID, LDS, STRM, ...)                                               \
-    do {                                                                                                   \
-        if (rip_gen) k_route<W, RKV, TAILV, true><<<GRID, ROUTE_BLOCK, LDS, STRM>>>(__VA_ARGS__);          \
-        else k_route<W, RKV, TAILV, false><<<GRID, ROUTE_BLOCK, LDS, STRM>>>(__VA_ARGS__);                 \
-    } while (0)
+#define GM_ROUTE_LAUNCH(W, RKV, TAILV, GRID, LDS, STRM, ...) \
+    k_route<W, RKV, TAILV><<<GRID, ROUTE_BLOCK, LDS, STRM>>>(__VA_ARGS__)
     const bool prof = c->flags & GM_CREATE_PROFILE;
     auto mark = [&](int k) -> int {
         if (prof) { HIPCHK(c, hipEventRecord(S->ev[k], s)); S->ev_used = k + 1; S->ev_pending = true; }
