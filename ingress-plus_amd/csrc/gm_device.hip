@@ -1706,28 +1706,15 @@ int gm_update_upstream(gm_ctx *c, const char *upstream, const char *const *serve
     return publish(c, R, gen, true, seq);
 }
 
-// The measurement / tuning variants compiled in (gm_stats_t.build_flags): a bench line can show it
-// came from the product build.  Every GM_EXP_* macro is a measurement (timing) variant; the
-// tuning macros count when they differ from the shipped values.
-static constexpr uint32_t kBuildFlags =
-#if defined(GM_EXP_COUNT) || defined(GM_EXP_CMASK) || defined(GM_EXP_ROUTE_AFTER) || defined(GM_EXP_ROUTE_FIRST) || \
-    defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_SCAN_NOBRANCH) || defined(GM_SCAN_VMASK)
-    GM_BUILD_EXPERIMENT |
-#endif
-#if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 4 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != 32 || \
-    GM_ROUTE_BPC != 2 || GM_ROUTE_PRIO != 0 || GM_ROUTE_WPE != GM_ROUTE_WPE_SHIPPED || GM_EXP_GRIDMUL != 8 || \
-    GM_EXP_WPE != 3 || GM_RLOC_CTX != 1 || GM_RLOC_PREF != 0 || GM_ALW_SLICE_GROUPS != 8 || GM_WIRE_WPE != 8 || \
-    GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1
-    GM_BUILD_TUNING |
-#endif
-    0u;
+static uint32_t build_flags();   // (defined at the end of the file: every tuning macro is set by then)
+
 
 int gm_stats(gm_ctx *c, gm_stats_t *out) {
     if (!c || !out) return fail(c, GM_E_INVAL, "null argument");
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
     *out = c->gen->stats;
-    out->build_flags = kBuildFlags;
+    out->build_flags = build_flags();
     out->scratch_scale = (float)c->cap_scale;
     out->n_set_reruns = c->n_set_reruns.load();
     out->set_shift = c->set_shift;
@@ -2795,3 +2782,20 @@ extern "C" int gm_upstream_uris(gm_ctx *c, const gm_batch *in, const gm_verdict 
     HIPCHK(c, hipGetLastError());
     return G.done(c);
 }
+
+// The measurement / tuning variants compiled in (gm_stats_t.build_flags): a bench line can show it
+// came from the product build.  Every GM_EXP_* macro is a measurement (timing) variant; the
+// tuning macros count when they differ from the shipped values.
+static constexpr uint32_t kBuildFlags =
+#if defined(GM_EXP_COUNT) || defined(GM_EXP_CMASK) || defined(GM_EXP_ROUTE_AFTER) || defined(GM_EXP_ROUTE_FIRST) || \
+    defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_SCAN_NOBRANCH) || defined(GM_SCAN_VMASK)
+    GM_BUILD_EXPERIMENT |
+#endif
+#if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 4 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != 32 || \
+    GM_ROUTE_BPC != 2 || GM_ROUTE_PRIO != 0 || GM_ROUTE_WPE != GM_ROUTE_WPE_SHIPPED || GM_EXP_GRIDMUL != 8 || \
+    GM_EXP_WPE != 3 || GM_RLOC_CTX != 1 || GM_RLOC_PREF != 0 || GM_ALW_SLICE_GROUPS != 8 || GM_WIRE_WPE != 8 || \
+    GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1
+    GM_BUILD_TUNING |
+#endif
+    0u;
+static uint32_t build_flags() { return kBuildFlags; }

@@ -212,3 +212,12 @@ def test_c3_regex_locations_compile(eng):
     assert flagged == [r[2] for r in regs]
     assert s["n_rejected_pcre"] == sum(flagged) > 0
     assert s["n_locations"] == len(regs) + 3
+
+
+def test_in_tree_library_is_the_default_build():
+    """The in-tree libgpumatch.so carries no measurement or tuning macros (gm_stats build_flags = 0):
+    what the tests, smoke() and bench.py load is the shipped pipeline (bench.py refuses otherwise)."""
+    e = engine.Engine(compile_only=True)
+    e.load(workloads.c1_blob(), 1)
+    st = e.stats()
+    assert st["build_flags"] == 0 and st["scratch_scale"] == 1.0 and st["set_shift"] == 0
