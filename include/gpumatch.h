@@ -222,7 +222,9 @@ typedef struct gm_stats_t {
     /* batches gm_sync re-ran because the WAF dedupe set overflowed (cumulative, this ctx) */
     uint32_t n_set_reruns;
     uint32_t set_shift;          /* GM_CREATE_SET_SHIFT in effect (0 normally) */
-    uint32_t reserved_stats[3];
+    /* always-run union members: one per distinct (pattern, nocase) among the always-run regexes */
+    uint32_t n_alw_members;
+    uint32_t reserved_stats[2];
 } gm_stats_t;
 
 /* gm_stats_t.build_flags: measurement / test variants compiled into the library.  bench.py refuses

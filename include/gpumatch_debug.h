@@ -42,6 +42,10 @@ int64_t gm_debug_waf_prefilter(struct gm_ctx *ctx, const uint8_t *A, size_t len,
 int64_t gm_debug_waf_prefilter2(struct gm_ctx *ctx, const uint8_t *A, size_t len, uint64_t *out, size_t cap);
 /* The realip address rules on the host (gm_inet.hpp, the code the device runs): `text` parsed as
  * ngx_parse_addr_port -> "<ngx_sock_ntop text> <port>" into out; -1 if it is not an address. */
+/* Host-side profile of the always-run union DFAs over a batch (host buffers): out[0] transitions,
+ * out[1] transitions taken in a group's start state that stay there, out[2] transitions taken in
+ * the start state, out[3] (group, request, zone) tasks. */
+int gm_debug_alw_profile(gm_ctx *ctx, const gm_req *reqs, const uint8_t *arena, uint32_t n, uint64_t *out4);
 /* gm_counters_allreduce's generation agreement: the 4 words a rank contributes to the MAX
  * reduction (gen, n_counters and their complements to 0xFFFFFFFF), and the verdict on the reduced
  * words (GM_OK: every rank had the same gen and n_counters; GM_E_COMM otherwise). */

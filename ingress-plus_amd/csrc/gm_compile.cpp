@@ -1935,6 +1935,10 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     std::vector<DAlwSlice> alw_slices;
     std::vector<uint8_t> alw_pack;
     std::vector<uint32_t> alw_rule, always_grouped, always_single;
+    // always-run groups: member k's rules are alw_rl[alw_rule[first + k] .. alw_rule[first + k + 1]),
+    // each zones << 24 | rule id -- one member per distinct (pattern, nocase), however many rules
+    // and zone sets share it (the location slices keep one value per member in alw_rule)
+    std::vector<uint32_t> alw_rl;
     auto tab_bytes = [](const MultiDfa &m) {   // the group's rows (gm_tables.hpp DAlwGroup)
         return (size_t)m.n_states * ((size_t)m.n_classes + (m.n_classes & 1) + 4) * 2;
     };
@@ -1956,13 +1960,15 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 for (uint32_t y : cur) cs.push_back(comps[y]);
                 cs.push_back(comps[x]);
                 MultiDfa m;
-                if (build_multi(cs, (int)ALW_BUILD_STATES, m) && tab_bytes(m) <= ALW_GROUP_BYTES) {
+                if (build_multi(cs, (int)ALW_BUILD_STATES, m) && tab_bytes(m) <= ALW_GROUP_BYTES &&
+                    m.n_classes <= ALW_CLASSES_MAX) {
                     cur.push_back(x); cur_m = std::move(m); continue;
                 }
             }
             close();
             MultiDfa m;
-            if (build_multi({comps[x]}, (int)ALW_BUILD_STATES, m) && tab_bytes(m) <= ALW_GROUP_BYTES) {
+            if (build_multi({comps[x]}, (int)ALW_BUILD_STATES, m) && tab_bytes(m) <= ALW_GROUP_BYTES &&
+                m.n_classes <= ALW_CLASSES_MAX) {
                 cur.push_back(x); cur_m = std::move(m);
             } else single.push_back(x);
         }
@@ -1971,7 +1977,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     // slices: consecutive groups, <= ALW_SLICE_GROUPS of them within ALWAYS_LDS_BYTES; member k of
     // group g stores val(g, k) in alw_rule and scans the zones zones(g, k)
     auto pack_slices = [&](const std::vector<std::vector<uint32_t>> &gmem, const std::vector<MultiDfa> &gdfa,
-                           auto val, auto zones, uint32_t server) {
+                           auto val, auto zones, uint32_t server, const std::vector<std::vector<uint32_t>> *mrules = nullptr) {
         auto pad16 = [&]() { alw_pack.resize((alw_pack.size() + 15) & ~size_t(15), 0); };
         for (size_t g0 = 0; g0 < gmem.size();) {
             size_t g1 = g0, bytes = 2048;
@@ -1982,11 +1988,13 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             sl.first_group = (uint32_t)alw.size();
             sl.n_groups = (uint32_t)(g1 - g0);
             sl.server = server;
-            // clsq[b]: byte b's class in groups 0..3 (a byte each); clsq[256 + b]: groups 4..7
+            // clsq[b]: byte b's class in groups 0..3 (a byte each), times 2 -- the class's byte offset
+            // in a row of u16 transitions, added to the row by one byte-select add (add_cls);
+            // clsq[256 + b]: groups 4..7
             std::vector<uint32_t> clsq(512, 0);
             for (size_t j = g0; j < g1; j++)
                 for (int b = 0; b < 256; b++)
-                    clsq[((j - g0) >= 4 ? 256 : 0) + b] |= (uint32_t)gdfa[j].cls[b] << (8 * ((j - g0) & 3));
+                    clsq[((j - g0) >= 4 ? 256 : 0) + b] |= (2u * gdfa[j].cls[b]) << (8 * ((j - g0) & 3));
             const uint8_t *cb = reinterpret_cast<const uint8_t *>(clsq.data());
             alw_pack.insert(alw_pack.end(), cb, cb + 2048);
             for (size_t j = g0; j < g1; j++) {
@@ -2024,12 +2032,18 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 g.n_classes = (uint32_t)Cn; g.n_states = (uint32_t)S;
                 g.first = (uint32_t)alw_rule.size();
                 for (size_t k = 0; k < gmem[j].size(); k++) {
-                    alw_rule.push_back(val(j, k));
+                    if (mrules) {   // the member's rule list (val: its entries, zones << 24 | rule)
+                        alw_rule.push_back((uint32_t)alw_rl.size());
+                        for (uint32_t e : (*mrules)[gmem[j][k]]) alw_rl.push_back(e);
+                    } else {
+                        alw_rule.push_back(val(j, k));
+                    }
                     const uint32_t zk = zones(j, k);
                     for (uint32_t z = 0; z < 4; z++)
                         if (zk & (1u << z)) g.zone_mask[z] |= 1u << k;
                     g.zones |= zk;
                 }
+                if (mrules) alw_rule.push_back((uint32_t)alw_rl.size());   // the last member's end
                 sl.zones |= g.zones;
                 st.n_alw_states += (uint32_t)S;
                 alw.push_back(g);
@@ -2043,23 +2057,43 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     // whose unions stay small; a group holds one zone set.  `always` is reordered: the grouped
     // regexes first (group order), then those left to the per-regex kernel.
     {
+        // members: one per distinct (pattern, nocase) -- the same search DFA -- with every rule
+        // that uses it (its zones the union of theirs); a match of member k in zone z emits the
+        // member's rules that scan z
+        std::map<std::string, uint32_t> ukey;
+        std::vector<uint32_t> urep;                      // member -> its first always index
+        std::vector<std::vector<uint32_t>> uall, mrules;  // member -> always indices / rule entries
+        std::vector<uint32_t> uzones;
+        for (uint32_t x = 0; x < always.size(); x++) {
+            const DSigRegex &sr = sregex[always[x]];
+            const std::string key = always_pat[x] + (sig[sr.rule].nocase ? std::string("\x01i") : std::string("\x01c"));
+            auto it = ukey.find(key);
+            uint32_t m;
+            if (it == ukey.end()) {
+                m = (uint32_t)urep.size();
+                ukey.emplace(key, m);
+                urep.push_back(x); uall.emplace_back(); mrules.emplace_back(); uzones.push_back(0);
+            } else m = it->second;
+            uall[m].push_back(x);
+            mrules[m].push_back((uint32_t)(sr.zones & 15u) << 24 | sr.rule);
+            uzones[m] |= sr.zones & 15u;
+        }
+        st.n_alw_members = (uint32_t)urep.size();
         std::vector<const Dfa *> comps;
-        for (const Dfa &d : always_dfa) comps.push_back(&d);
-        std::vector<uint32_t> ord(always.size());
+        for (uint32_t m = 0; m < urep.size(); m++) comps.push_back(&always_dfa[urep[m]]);
+        std::vector<uint32_t> ord(urep.size());
         for (uint32_t i = 0; i < ord.size(); i++) ord[i] = i;
         std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
-            const uint16_t zx = sregex[always[x]].zones, zy = sregex[always[y]].zones;
-            return zx != zy ? zx < zy : always_pat[x] < always_pat[y];
+            return uzones[x] != uzones[y] ? uzones[x] < uzones[y] : always_pat[urep[x]] < always_pat[urep[y]];
         });
         std::vector<std::vector<uint32_t>> gmem;
         std::vector<MultiDfa> gdfa;
         std::vector<uint32_t> single;
-        form_groups(comps, ord, [&](uint32_t a, uint32_t b) { return sregex[always[a]].zones == sregex[always[b]].zones; },
-                    gmem, gdfa, single);
-        pack_slices(gmem, gdfa, [&](size_t j, size_t k) { return sregex[always[gmem[j][k]]].rule; },
-                    [&](size_t j, size_t k) { return (uint32_t)sregex[always[gmem[j][k]]].zones; }, GM_NONE);
-        for (auto &gm : gmem) for (uint32_t x : gm) always_grouped.push_back(always[x]);
-        for (uint32_t x : single) always_single.push_back(always[x]);
+        form_groups(comps, ord, [&](uint32_t a, uint32_t b) { return uzones[a] == uzones[b]; }, gmem, gdfa, single);
+        pack_slices(gmem, gdfa, [](size_t, size_t) { return 0u; },
+                    [&](size_t j, size_t k) { return uzones[gmem[j][k]]; }, GM_NONE, &mrules);
+        for (auto &gm : gmem) for (uint32_t m : gm) for (uint32_t x : uall[m]) always_grouped.push_back(always[x]);
+        for (uint32_t m : single) for (uint32_t x : uall[m]) always_single.push_back(always[x]);
     }
     const uint32_t n_alw_slices = (uint32_t)alw_slices.size();
     // the regex locations of every rk_on server, in config order (consecutive groups, so the
@@ -2188,6 +2222,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_always = I.put(always);
     h.off_alw = I.put(alw); h.off_alw_slices = I.put(alw_slices); h.off_alw_pack = I.put(alw_pack);
     h.off_alw_rule = I.put(alw_rule);
+    h.off_alw_rl = I.put(alw_rl);
     rsl_pbit.resize((rsl_pbit.size() + 3) & ~size_t(3), 0xFF);
     h.off_rsl_pbit = I.put(rsl_pbit);
     // (before the upstream section: gm_update_upstream copies everything before it unchanged)
@@ -2364,6 +2399,7 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.alw_slices = (const DAlwSlice *)(b + h.off_alw_slices);
     t.alw_pack = b + h.off_alw_pack;
     t.alw_rule = (const uint32_t *)(b + h.off_alw_rule);
+    t.alw_rl = (const uint32_t *)(b + h.off_alw_rl);
     t.rsl_pbit = b + h.off_rsl_pbit;
     t.realip = (const DRealIp *)(b + h.off_realip);
     t.cidrs = (const DCidr *)(b + h.off_cidrs);

@@ -2308,6 +2308,54 @@ extern "C" int gm_debug_waf_keys(gm_ctx *c, uint32_t *out, size_t cap) {
     return (int)k;
 }
 
+// The always-run union DFAs on the host over a batch (host buffers): per (group, request, zone it
+// scans) step counts -- out[0] transitions, out[1] those taken in the start state that stay in
+// it, out[2] those taken in the start state, out[3] (group, request, zone) tasks
+extern "C" int gm_debug_alw_profile(gm_ctx *c, const gm_req *reqs, const uint8_t *arena, uint32_t n, uint64_t *out) {
+    if (!c || !out) return fail(c, GM_E_INVAL, "null argument");
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    const Generation *g = c->gen;
+    if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
+    const uint8_t *img = g->host_image.data();
+    const TabHeader &h = g->hdr;
+    const DAlwSlice *sls = reinterpret_cast<const DAlwSlice *>(img + h.off_alw_slices);
+    const DAlwGroup *grs = reinterpret_cast<const DAlwGroup *>(img + h.off_alw);
+    uint64_t tot = 0, stay = 0, at = 0, tasks = 0;
+    for (uint32_t si = 0; si < h.n_alw_slices; si++) {
+        const DAlwSlice &sl = sls[si];
+        if (sl.server != GM_NONE) continue;
+        const uint8_t *P = img + h.off_alw_pack + sl.off;
+        const uint32_t *clsq = reinterpret_cast<const uint32_t *>(P);
+        for (uint32_t j = 0; j < sl.n_groups; j++) {
+            const DAlwGroup &gr = grs[sl.first_group + j];
+            const uint8_t *G = P + gr.tr_off;
+            for (uint32_t r = 0; r < n; r++) {
+                const gm_req &q = reqs[r];
+                const uint32_t lens[4] = {q.uri_len, q.args_len, q.hdr_len, q.body_len};
+                uint64_t o = q.base;
+                for (uint32_t z = 0; z < 4; z++) {
+                    if ((gr.zones >> z) & 1u) {
+                        tasks++;
+                        uint32_t row = gr.start_row;
+                        for (uint32_t i = 0; i < lens[z] && row; i++) {
+                            const uint32_t b = arena[o + i];
+                            const uint32_t cl = (clsq[(j >= 4 ? 256u : 0u) + b] >> (8 * (j & 3))) & 0xFF;
+                            uint16_t nx;
+                            memcpy(&nx, G + row + cl, 2);   // (clsq holds 2 * class)
+                            tot++;
+                            if (row == gr.start_row) { at++; if (nx == gr.start_row) stay++; }
+                            row = nx;
+                        }
+                    }
+                    o += lens[z];
+                }
+            }
+        }
+    }
+    out[0] = tot; out[1] = stay; out[2] = at; out[3] = tasks;
+    return GM_OK;
+}
+
 // gm_counters_allreduce's agreement protocol, exposed for the world-size-2 gloo test
 extern "C" void gm_debug_agree_pack(uint64_t gen, uint64_t n, uint64_t *w4) {
     unsigned long long w[4];

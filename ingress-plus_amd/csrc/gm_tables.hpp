@@ -299,6 +299,7 @@ __host__ __device__ inline uint32_t peer_draw(uint64_t lo, uint64_t hi, uint32_t
 constexpr uint32_t ALWAYS_LDS_BYTES = 160 * 1024;
 constexpr uint32_t ALW_GROUP_BYTES = 64 * 1024 - 64;   // row byte offsets fit a u16 with the flag bit
 constexpr uint32_t ALW_GROUP_MAX = 32;
+constexpr uint32_t ALW_CLASSES_MAX = 127;   // clsq holds 2 * class in a byte
 #ifndef GM_ALW_SLICE_GROUPS
 #define GM_ALW_SLICE_GROUPS 8
 #endif
@@ -310,7 +311,8 @@ struct DAlwGroup {
     uint32_t start_row;      // byte offset of the start state's row (row 1)
     uint32_t n_classes, n_states;
     uint32_t zone_mask[4];   // members (bit k) that scan zone z
-    uint32_t first;          // member k's rule id: alw_rule[first + k]
+    uint32_t first;          // member k: a location slice's value alw_rule[first + k]; an always-run
+                             // group's rule list alw_rl[alw_rule[first + k] .. alw_rule[first + k + 1])
     uint32_t zones;          // zones some member scans
     uint32_t emit_row;       // byte offset of the first emitting state's row (rows past it emit too)
 };
@@ -363,6 +365,7 @@ struct TabHeader {
     uint32_t n_rk_ents_n, pad_rke; // DRlocEnt entries (k_rloc_pref stages them in LDS)
     uint32_t n_realip, n_cidrs;    // realip configurations and their set_real_ip_from entries
     uint64_t off_realip, off_cidrs;
+    uint64_t off_alw_rl;           // always-run members' rule lists (zones << 24 | rule)
 };
 // The route's hot tables -- ports, the three name tables, servers, server ifs, small-location
 // lists, locations and the name strings -- are laid out first and contiguously in the image;
@@ -390,6 +393,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const DAlwGroup *alw; const DAlwSlice *alw_slices; const uint8_t *alw_pack; const uint32_t *alw_rule;
     const uint8_t *rsl_pbit;
     const DRealIp *realip; const DCidr *cidrs;
+    const uint32_t *alw_rl;
     uint32_t n_always_lds, n_alw_groups, n_alw_slices, n_rsl, n_rk_prefilter;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;

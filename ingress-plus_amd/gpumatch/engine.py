@@ -60,7 +60,8 @@ class GmStats(ctypes.Structure):
                 [(f, ctypes.c_float) for f in STATS_FIELDS_MS] +
                 [(f, ctypes.c_uint32) for f in STATS_FIELDS_WAF] +
                 [("scratch_scale", ctypes.c_float), ("n_set_reruns", ctypes.c_uint32),
-                 ("set_shift", ctypes.c_uint32), ("reserved_stats", ctypes.c_uint32 * 3)])
+                 ("set_shift", ctypes.c_uint32), ("n_alw_members", ctypes.c_uint32),
+                 ("reserved_stats", ctypes.c_uint32 * 2)])
 
 
 class GmBatch(ctypes.Structure):
@@ -177,6 +178,7 @@ class Engine:
         d["scratch_scale"] = s.scratch_scale
         d["n_set_reruns"] = s.n_set_reruns
         d["set_shift"] = s.set_shift
+        d["n_alw_members"] = s.n_alw_members
         return d
 
     def rejects(self) -> list:
