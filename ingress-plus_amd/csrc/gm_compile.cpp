@@ -1125,6 +1125,25 @@ struct KeyModel {
     }
 };
 
+// A prefix-mode regex's anchored DFA after its prefix literal f (k_waf_exact starts the run there:
+// the literal is already verified), as a transition entry (state | accept flags << 14); 0 = run
+// from the start.  Valid only when the arena's bytes take the same path as f's: the literal is
+// matched case-insensitively, so a case-sensitive regex qualifies only if f has no letters.  A
+// state on the way that accepts makes the entry accepting (the run would have stopped there); a
+// '\n' in f keeps the full run (PCRE's "$ before a final newline" looks at the subject's last byte).
+uint16_t prefix_entry(const Dfa &d, const std::string &f, bool nocase) {
+    if (d.n_states == 0 || d.n_states > (int)DFA_TRANS_STATE_MASK) return 0;
+    uint32_t s = 1, fl = d.acc[1] & 3u;
+    for (unsigned char c : f) {
+        if (c == '\n' || (!nocase && ((c | 0x20) >= 'a' && (c | 0x20) <= 'z'))) return 0;
+        if (fl & 1u) break;
+        s = d.trans[(size_t)s * d.n_classes + d.cls[c]];
+        if (s == 0) return 0;
+        fl = d.acc[s] & 3u;
+    }
+    return (uint16_t)(s | (fl << 14));
+}
+
 // The scan probes only even arena offsets (k_waf_scan), so every pattern is keyed on a set of
 // windows that catches an occurrence at either parity:
 //   >= 5 bytes: two ADJACENT windows (o, o + 1), the pair of least summed cost;
@@ -1807,8 +1826,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     // one prefilter pattern -> its key windows (stride-2 scan, see choose_keys)
     std::unordered_map<uint32_t, uint32_t> key_use;
     auto add_lit = [&](const std::string &pat, const std::string &bytes, uint32_t id, uint8_t flags, uint8_t zones,
-                       const std::bitset<256> *follow = nullptr) {
-        const DLit d{id, 0, (uint16_t)bytes.size(), flags, zones, 0, 0};
+                       const std::bitset<256> *follow = nullptr, uint16_t dfa_entry = 0) {
+        const DLit d{id, 0, (uint16_t)bytes.size(), flags, zones, 0, dfa_entry};
         for (auto &k : choose_keys(pat, KM, key_use, follow).keys) {
             LitE e{k.first, d, bytes};
             e.lit.key_off = k.second;
@@ -1837,7 +1856,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 sr.adfa = (uint32_t)C.add_dfa(ri.anchored);
                 for (auto &f : ri.prefix)
                     add_lit(f, f, ridx, (uint8_t)(LIT_NOCASE | LIT_TRIGGER | LIT_PREFIX), (uint8_t)g.zones,
-                            ri.has_prefix_follow ? &ri.prefix_follow : nullptr);
+                            ri.has_prefix_follow ? &ri.prefix_follow : nullptr, prefix_entry(ri.anchored, f, g.nocase));
             } else if (ri.min_factor < 4) {
                 sr.mode = RXM_ALWAYS;
                 always.push_back(ridx);
@@ -1857,6 +1876,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         return a.key != b.key ? a.key < b.key : a.lit.id < b.lit.id;
     });
     std::vector<DLit> dlits;
+    std::vector<DLitChk> dchk;
     std::vector<uint32_t> waf_a(BLOOM_WORDS, 0);   // LDS Bloom image
     // stage-2 context filter: each entry's key window plus the pattern bytes around it
     std::vector<uint32_t> waf_b(BLOOM_WORDS, 0);
@@ -1877,6 +1897,16 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         LitE &e = lits[i];
         e.lit.bytes_off = C.put_bytes(e.bytes);
         dlits.push_back(e.lit);
+        {   // the pattern bytes in the 4 arena bytes either side of the key window, folded
+            const int k = e.lit.key_off, L = (int)e.bytes.size();
+            DLitChk c{0, 0, 0, 0};
+            for (int j = 0; j < 4; j++) {
+                const int ib = k - 4 + j, ia = k + 4 + j;
+                if (ib >= 0 && ib < L) { c.b |= ((uint32_t)(uint8_t)e.bytes[ib] | 0x20u) << (8 * j); c.bmask |= 0xFFu << (8 * j); }
+                if (ia >= 0 && ia < L) { c.a |= ((uint32_t)(uint8_t)e.bytes[ia] | 0x20u) << (8 * j); c.amask |= 0xFFu << (8 * j); }
+            }
+            dchk.push_back(c);
+        }
         if (i == 0 || lits[i - 1].key != e.key) {
             buckets.push_back({e.key, {(uint32_t)i, 0}});
             keys.push_back(e.key);
@@ -2223,6 +2253,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_alw = I.put(alw); h.off_alw_slices = I.put(alw_slices); h.off_alw_pack = I.put(alw_pack);
     h.off_alw_rule = I.put(alw_rule);
     h.off_alw_rl = I.put(alw_rl);
+    h.off_lit_chk = I.put(dchk);
     rsl_pbit.resize((rsl_pbit.size() + 3) & ~size_t(3), 0xFF);
     h.off_rsl_pbit = I.put(rsl_pbit);
     // (before the upstream section: gm_update_upstream copies everything before it unchanged)
@@ -2400,6 +2431,7 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.alw_pack = b + h.off_alw_pack;
     t.alw_rule = (const uint32_t *)(b + h.off_alw_rule);
     t.alw_rl = (const uint32_t *)(b + h.off_alw_rl);
+    t.lit_chk = (const DLitChk *)(b + h.off_lit_chk);
     t.rsl_pbit = b + h.off_rsl_pbit;
     t.realip = (const DRealIp *)(b + h.off_realip);
     t.cidrs = (const DCidr *)(b + h.off_cidrs);

@@ -1890,8 +1890,14 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
     if ((e = grow(c, s, S->d_blk2rec, S->cap_blk, nblk))) return e;
     if ((e = grow(c, s, S->d_cand, S->cap_cand, std::max<size_t>(ccap, scaled((size_t)W * 4096, 4 * W))))) return e;
-    // scan-wave counts, ctx-block counts, scan-wave resume chunks, ctx-region resume records
-    if ((e = grow(c, s, S->d_ccnt, S->cap_ccnt, 3 * (size_t)W + scan_blocks))) return e;
+    // scan-wave counts, ctx-block counts, scan-wave resume chunks, ctx-region resume records,
+    // then k_waf_exact's per-workgroup profiling partials (4 words each)
+#ifndef GM_EXACT_BPC
+#define GM_EXACT_BPC 6
+#endif
+    const uint32_t exact_blocks = (uint32_t)c->cu_count * GM_EXACT_BPC;
+    if ((e = grow(c, s, S->d_ccnt, S->cap_ccnt, 3 * (size_t)W + scan_blocks + 4 * (size_t)exact_blocks))) return e;
+    uint32_t *const xprof = S->d_ccnt + 3 * (size_t)W + scan_blocks;
     if ((e = grow(c, s, S->d_surv, S->cap_surv, std::min<size_t>(scaled((alen / 256 + 65536) * S->surv_mult, scan_blocks),
                                                                  0xFFFFFFFFu)))) return e;
     if ((e = grow(c, s, S->d_pairs, S->cap_pairs, pcap))) return e;
@@ -2001,10 +2007,12 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     HIPCHK(c, hipGetLastError());
     // join: blk2rec, the verdicts and the zeroed counts are complete before the exact check
     if (!serial) HIPCHK(c, hipStreamWaitEvent(s, S->ev_join, 0));
-    constexpr uint32_t EXACT_SUB = 8;
-    k_waf_exact<<<scan_blocks * EXACT_SUB, 256, 0, s>>>(A, alen, reqs, n, S->d_blk2rec, t, S->d_surv, bcap,
-                                                         S->d_ccnt + W, EXACT_SUB, S->d_pairs, (uint32_t)S->cap_pairs,
-                                                         S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, dd, dlen);
+    // persistent exact check: EXACT_BPC workgroups per CU, all resident
+    k_waf_exact<<<exact_blocks, EXACT_BLOCK, 0, s>>>(A, alen, reqs, n, S->d_blk2rec, t, S->d_surv, bcap,
+                                                     S->d_ccnt + W, scan_blocks, S->d_pairs, (uint32_t)S->cap_pairs,
+                                                         S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, dd, dlen, xprof);
+    HIPCHK(c, hipGetLastError());
+    k_exact_prof<<<1, 256, 0, s>>>(xprof, exact_blocks, S->d_status);
     HIPCHK(c, hipGetLastError());
     if ((e = launch_direct(A, alen, reqs, S->d_blk2rec, dd, dlen))) return e;
     if (mark(3)) return GM_E_HIP;
@@ -2050,9 +2058,11 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, S->d_ccnt, W, t, S->d_surv, bcap, S->d_ccnt + W,
                                                     S->d_status, S->d_ccnt + 2 * W + scan_blocks);
         HIPCHK(c, hipGetLastError());
-        k_waf_exact<<<scan_blocks * EXACT_SUB, 256, 0, s>>>(SA, scap, SR, n, S->d_sblk, t, S->d_surv, bcap,
-                                                             S->d_ccnt + W, EXACT_SUB, S->d_pairs, (uint32_t)S->cap_pairs,
-                                                             S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, dd2, slen);
+        k_waf_exact<<<exact_blocks, EXACT_BLOCK, 0, s>>>(SA, scap, SR, n, S->d_sblk, t, S->d_surv, bcap,
+                                                         S->d_ccnt + W, scan_blocks, S->d_pairs, (uint32_t)S->cap_pairs,
+                                                             S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, dd2, slen, xprof);
+        HIPCHK(c, hipGetLastError());
+        k_exact_prof<<<1, 256, 0, s>>>(xprof, exact_blocks, S->d_status);
         HIPCHK(c, hipGetLastError());
         if ((e = launch_direct(SA, scap, SR, S->d_sblk, dd2, slen))) return e;
         if (t.n_sig_regex) {
@@ -2842,7 +2852,7 @@ static constexpr uint32_t kBuildFlags =
 #if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 4 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != 32 || \
     GM_ROUTE_BPC != 2 || GM_ROUTE_PRIO != 0 || GM_ROUTE_WPE != GM_ROUTE_WPE_SHIPPED || GM_EXP_GRIDMUL != 8 || \
     GM_EXP_WPE != 3 || GM_RLOC_CTX != 1 || GM_RLOC_PREF != 0 || GM_ALW_SLICE_GROUPS != 8 || GM_WIRE_WPE != 8 || \
-    GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1
+    GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1 || GM_EXACT_BPC != 6 || !defined(GM_DFA_INL_SHIPPED)
     GM_BUILD_TUNING |
 #endif
     0u;

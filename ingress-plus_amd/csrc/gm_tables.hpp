@@ -229,8 +229,14 @@ struct DLit {
     uint8_t  zones;          // bit0 uri, bit1 args, bit2 hdrs, bit3 body
     int16_t  key_off;        // offset of the 4-byte key window inside the pattern; -1 = the window
                              // starts one byte before the pattern (4-byte patterns, gm_compile.cpp)
-    uint16_t pad;
+    uint16_t dfa_entry;      // LIT_PREFIX: the anchored DFA's state after the whole literal, with
+                             // its accept flags in bits 14-15 (a transition entry), so the run
+                             // starts after the literal; 0 = run from the start state
 };
+// k_waf_exact's first test of a literal at a key hit, before any pattern byte is read: the folded
+// pattern bytes in the 4 arena bytes before (b) and after (a) the key window, each with the mask
+// of the bytes that lie inside the pattern (parallel to the DLit array)
+struct DLitChk { uint32_t b, bmask, a, amask; };
 enum : uint32_t { RXM_TRIGGER = 0, RXM_ALWAYS = 1, RXM_PREFIX = 2 };
 struct DSigRegex {
     uint32_t dfa;            // search DFA (whole zone)
@@ -366,6 +372,7 @@ struct TabHeader {
     uint32_t n_realip, n_cidrs;    // realip configurations and their set_real_ip_from entries
     uint64_t off_realip, off_cidrs;
     uint64_t off_alw_rl;           // always-run members' rule lists (zones << 24 | rule)
+    uint64_t off_lit_chk;          // DLitChk per DLit
 };
 // The route's hot tables -- ports, the three name tables, servers, server ifs, small-location
 // lists, locations and the name strings -- are laid out first and contiguously in the image;
@@ -394,6 +401,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const uint8_t *rsl_pbit;
     const DRealIp *realip; const DCidr *cidrs;
     const uint32_t *alw_rl;
+    const DLitChk *lit_chk;
     uint32_t n_always_lds, n_alw_groups, n_alw_slices, n_rsl, n_rk_prefilter;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
