@@ -1952,6 +1952,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.magic = 0x47544142u; h.version = 1;
     h.n_ports = (uint32_t)ports.size();
     h.n_names_cap = names_mask + 1; h.n_wild_head_cap = head_mask + 1; h.n_wild_tail_cap = tail_mask + 1;
+    h.n_wild = (uint32_t)(head.size() + tail.size());
     h.n_servers = (uint32_t)dservers.size(); h.n_server_ifs = (uint32_t)sifs.size(); h.n_rlocs = (uint32_t)rlocs.size();
     h.n_nodes = (uint32_t)nodes.size(); h.n_edges_cap = ecap; h.n_locs = (uint32_t)dlocs.size();
     h.n_srcs = (uint32_t)C.srcs.size(); h.n_conds = (uint32_t)C.conds.size(); h.n_chain_heads = (uint32_t)C.chain_heads.size();
@@ -2439,6 +2440,7 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.n_rsl = h.n_rsl; t.n_rk_prefilter = h.n_rk_prefilter;
     t.n_ports = h.n_ports;
     t.names_mask = h.n_names_cap - 1; t.wild_head_mask = h.n_wild_head_cap - 1; t.wild_tail_mask = h.n_wild_tail_cap - 1;
+    t.n_wild = h.n_wild;
     t.edges_mask = h.n_edges_cap - 1; t.lit_mask = h.n_lit_buckets_cap - 1;
     t.n_locs = h.n_locs; t.n_sigs = h.n_sigs; t.n_sig_regex = h.n_sig_regex; t.n_always = h.n_always;
     t.n_lits = h.n_lits;

@@ -728,11 +728,15 @@ struct HotTabs {
     const DPort *ports; const DName *names; const DServer *servers; const DServerIf *server_ifs;
     const DSmallLoc *small; const DLoc *locs; const uint8_t *name_bytes;
 };
+// NOV6: an IPv6 literal returns -2 (the caller's slow path): its byte loop indexes hw by a
+// variable, which puts the words in scratch for every request
+template <bool NOV6 = false>
 __device__ __forceinline__ int host_fast(const uint32_t (&hw)[8], uint32_t n, const GTab &t, const HotTabs &h,
                                          uint32_t pi, uint32_t &server) {
     server = GM_NONE;
     int host_len;
-    if ((hw[0] & 0xFF) == '[') {
+    if (NOV6 && (hw[0] & 0xFF) == '[') return -2;
+    if (!NOV6 && (hw[0] & 0xFF) == '[') {
         int dot_pos = (int)n, state = 0;
         bool bad = false;
         host_len = (int)n;
@@ -792,7 +796,8 @@ __device__ __forceinline__ int host_fast(const uint32_t (&hw)[8], uint32_t n, co
 
 // Wildcard names (*.x / .x, then x.*) for a host that missed the exact table; byte-wise over
 // the arena (rare path).
-__device__ __noinline__ uint32_t host_wildcards(const uint8_t *h, int hl, const GTab &t, uint32_t pi) {
+template <bool INL = false>
+__device__ __forceinline__ uint32_t host_wildcards_body(const uint8_t *h, int hl, const GTab &t, uint32_t pi) {
     uint32_t s = GM_NONE;
     uint32_t w = name_probe(t.wild_head, t.wild_head_mask, t.name_bytes, h, 0, (uint32_t)hl, pi);
     if (w != GM_NONE && (w & 0x80000000u)) s = w & 0x7FFFFFFFu;      // ".x" matches x itself
@@ -804,6 +809,9 @@ __device__ __noinline__ uint32_t host_wildcards(const uint8_t *h, int hl, const 
     for (int d = hl - 2; s == GM_NONE && d > 0; d--)
         if (h[d] == '.') s = name_probe(t.wild_tail, t.wild_tail_mask, t.name_bytes, h, 0, (uint32_t)d, pi);
     return s;
+}
+__device__ __noinline__ uint32_t host_wildcards(const uint8_t *h, int hl, const GTab &t, uint32_t pi) {
+    return host_wildcards_body(h, hl, t, pi);
 }
 
 // Generic (variable-reading) steps live in non-inlined functions so that the Ctx / Val
@@ -930,17 +938,31 @@ constexpr uint32_t RLOC_STATUS_WORD = 16;   // batch status word: requests defer
 // (URI <= RLOC_URI_CAP, n_rloc <= RLOC_BM_BITS) sets *pend and returns; >= -1 -- k_rloc's answer
 // (the location index, -1 none).  *sid_out: the server chosen (valid whenever *pend is set).
 constexpr int32_t RK_INLINE = -3, RK_DEFER = -2;
+template <bool FAST = false>
 __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
                           RouteOut &o);
 // the request's body length and whether it is chunked, re-read from its record where the 413
 // check needs them (kept in registers across the location walk they cost the route spills)
 __device__ __forceinline__ uint32_t req_body_len(const gm_req *rp) { return reinterpret_cast<const uint32_t *>(rp)[5]; }
 __device__ __forceinline__ bool req_chunked(const gm_req *rp) { return reinterpret_cast<const uint32_t *>(rp)[9] & GM_REQ_CHUNKED; }
+__device__ __forceinline__ uint32_t req_flags(const gm_req *rp) { return reinterpret_cast<const uint32_t *>(rp)[9] & 0xFFu; }
+template <bool FAST>
+__device__ __forceinline__ void route_locphase(const uint8_t *A, const gm_req *rp, const Rec &r, const RoutePre &pre,
+                                               const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb,
+                                               int32_t rk_in, bool *pend, const DServer &S, uint32_t sid);
 // client_max_body_size exceeded: 413, nothing proxied, no WAF phase
 __device__ __forceinline__ void too_large(RouteOut &o) {
     o.action = GM_ACT_TOO_LARGE; o.status = 413; o.ups = GM_NONE; o.waf = GM_WAF_OFF;
 }
-__device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const RoutePre &pre,
+// FAST: no out-of-line call while the host / URI words and the record are live.  A call there
+// made the compiler keep them in scratch around it -- stored and reloaded for every request, call
+// or not: the route took 1.05 ms alone per 10M C4 requests with the calls in place, 0.70 without.
+// So the wildcard step is inlined, an IPv6 literal host takes the arena-byte path, and the server
+// `if`s that need a call run after the location phase (where little is live): the first of them
+// that returns (or cannot be evaluated) replaces the location's result, as it would have ended the
+// request before that phase.  The rules / split / regex-location calls come after the words die.
+template <bool FAST = false>
+__device__ __forceinline__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const RoutePre &pre,
                           const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb, int32_t rk_in = RK_INLINE,
                           bool *pend = nullptr) {
     o.server = GM_NONE; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0;
@@ -965,14 +987,21 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
         uint32_t s = GM_NONE;
         int hl;
         if (r.host_len <= 32) {
-            hl = host_fast(pre.hw, r.host_len, t, h, pi, s);
+            hl = host_fast<FAST>(pre.hw, r.host_len, t, h, pi, s);
+            if (FAST && hl == -2) {   // an IPv6 literal: the arena-byte path
+                hl = validate_host(A + f_host, r.host_len);
+                if (hl >= 0) s = name_probe(h.names, t.names_mask, h.name_bytes, A + f_host, 0, (uint32_t)hl, pi);
+            }
         } else {
             hl = validate_host(A + f_host, r.host_len);
             if (hl >= 0) s = name_probe(h.names, t.names_mask, h.name_bytes, A + f_host, 0, (uint32_t)hl, pi);
         }
         if (hl < 0) bad = true;
         else {
-            if (s == GM_NONE) s = host_wildcards(A + f_host, hl, *t.self, pi);
+            if (s == GM_NONE && t.n_wild) {   // (no wildcard names: the port's default server)
+                if (FAST) s = host_wildcards_body<true>(A + f_host, hl, t, pi);
+                else s = host_wildcards(A + f_host, hl, *t.self, pi);
+            }
             if (s != GM_NONE) sid = s;
         }
     }
@@ -980,6 +1009,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
     if (bad || (P.ssl && !https)) { o.action = GM_ACT_BAD_REQUEST; o.status = 400; return; }
     const DServer S = h.servers[sid];
     // ---- server rewrite phase
+    uint32_t sif = GM_NONE;   // FAST: the first `if` left until after the location phase
     for (uint32_t i = 0; i < S.n_if; i++) {
         const DServerIf f = h.server_ifs[S.first_if + i];
         bool hit;
@@ -987,14 +1017,40 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
         else if (f.op == SIF_FLAGS) hit = (f.tt >> (r.flags & 3)) & 1u;
         else if (f.op == 0xFF) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; return; }
         else {
+            if (FAST) { sif = i; break; }   // this one and the rest: after the location phase
             const int g = server_if_generic(A, rp, *t.self, S.first_if + i, S.realip);
             if (g < 0) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; return; }
             hit = g != 0;
         }
         if (hit) { o.action = is_redirect(f.code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = f.code; return; }
     }
-    // ---- location: trie walk (exact, longest prefix, auto_redirect), then regex locations.
-    // The first 32 URI bytes come from registers (a window shifted one dword per 4 bytes).
+    route_locphase<FAST>(A, rp, r, pre, t, h, o, rkb, rk_in, pend, S, sid);
+    if (FAST && sif != GM_NONE) {
+        for (uint32_t i = sif; i < S.n_if; i++) {
+            const DServerIf f = h.server_ifs[S.first_if + i];
+            int g;
+            if (f.op == SIF_RETURN) g = 1;
+            else if (f.op == SIF_FLAGS) g = (f.tt >> (req_flags(rp) & 3)) & 1u;
+            else if (f.op == 0xFF) g = -1;
+            else g = server_if_generic(A, rp, *t.self, S.first_if + i, S.realip);
+            if (g == 0) continue;
+            o.loc = GM_NONE; o.ups = GM_NONE; o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF;
+            o.waf = GM_WAF_OFF;
+            if (g < 0) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; }
+            else { o.action = is_redirect(f.code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = f.code; }
+            break;
+        }
+    }
+}
+
+// route_one's location phase: trie walk (exact, longest prefix, auto_redirect), then regex
+// locations, then route_loc.  The first 32 URI bytes come from registers (a window shifted one
+// dword per 4 bytes).
+template <bool FAST>
+__device__ __forceinline__ void route_locphase(const uint8_t *A, const gm_req *rp, const Rec &r, const RoutePre &pre,
+                                               const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb,
+                                               int32_t rk_in, bool *pend, const DServer &S, uint32_t sid) {
+    const uint64_t f_uri = r.base;
     const uint8_t *u = A + f_uri;
     uint32_t uw[8];
 #pragma unroll
@@ -1078,7 +1134,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
             if (loc < 0) loc = best;
         }
     }
-    route_loc(A, rp, t, h, loc, o);
+    route_loc<FAST>(A, rp, t, h, loc, o);
 }
 
 // The rest of route_one once the location is known (loc < 0: none): location kinds, rules and
@@ -1088,6 +1144,7 @@ __device__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, con
 // server's limit when none) before that location's rewrite phase (ngx_http_core_find_config_phase);
 // a chunked body only when it is read -- by the proxying location, the final one after an
 // internal redirect (the chunked body filter)
+template <bool FAST>
 __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
                           RouteOut &o) {
     const uint32_t blen = req_body_len(rp);
@@ -1128,6 +1185,17 @@ __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, co
     o.action = GM_ACT_PROXY; o.status = 0; o.ups = L.upstream; o.waf = L.waf_mode;
 }
 
+// the verdict's two 16-byte halves (n_hits and first_hit_off 0: the WAF stages fill them in)
+__device__ __forceinline__ void write_verdict(gm_verdict *v, const GTab &t, const RouteOut &o) {
+    uint4 w0, w1;
+    w0.x = t.gen; w0.y = o.server; w0.z = o.loc; w0.w = o.ups;
+    w1.x = (uint32_t)o.action | ((uint32_t)o.kind << 8) | ((uint32_t)o.bucket << 16) | ((uint32_t)o.match << 24);
+    w1.y = (uint32_t)o.waf;   // n_hits = 0
+    w1.z = 0;                 // first_hit_off
+    w1.w = o.status;
+    uint4 *dst = reinterpret_cast<uint4 *>(v);
+    dst[0] = w0; dst[1] = w1;
+}
 // ============================================================================ kernels
 constexpr int ROUTE_BLOCK = 256;
 // register target (waves per SIMD) of the route beside the WAF scan: the scan's workgroup holds
@@ -1204,6 +1272,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
     __syncthreads();
     const uint32_t nn = TAIL ? *q.count : n;
     const uint32_t stride = gridDim.x * blockDim.x;
+    constexpr bool FASTK = !RK && !TAIL;   // route_one without calls while its words are live
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nn; x += stride) {
         uint32_t i = x;
         RouteOut o;
@@ -1223,9 +1292,10 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
         } else {
             r = load_rec(reqs + i);
             route_prefetch(A, arena_len, r, pre);
-            route_one(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
-                      RK && q.list ? RK_DEFER : RK_INLINE, &pend);
+            route_one<FASTK>(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
+                             RK && q.list ? RK_DEFER : RK_INLINE, &pend);
         }
+        const uint32_t cloc = o.loc;
         if (RK && !TAIL) {   // deferred to k_rloc: appended, one atomic per wave
             const unsigned long long pm = __ballot(pend);
             if (pm) {
@@ -1244,23 +1314,16 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
                 }
             }
         }
-        uint4 w0, w1;
-        w0.x = t.gen; w0.y = o.server; w0.z = o.loc; w0.w = o.ups;
-        w1.x = (uint32_t)o.action | ((uint32_t)o.kind << 8) | ((uint32_t)o.bucket << 16) | ((uint32_t)o.match << 24);
-        w1.y = (uint32_t)o.waf;   // n_hits = 0
-        w1.z = 0;                 // first_hit_off
-        w1.w = o.status;
-        uint4 *dst = reinterpret_cast<uint4 *>(out + i);
-        if (!pend) { dst[0] = w0; dst[1] = w1; }
+        if (!pend) write_verdict(out + i, t, o);
         // per-location counter: the wave's first few distinct locations in one atomic each for all
         // their lanes (most waves: one to three locations), any lane left after four rounds its
         // own atomic (C3's ~50 distinct locations per wave took a round each)
         {
-            unsigned long long todo = __ballot(o.loc != GM_NONE);
+            unsigned long long todo = __ballot(cloc != GM_NONE);
             for (int round = 0; todo && round < 4; round++) {
                 const int leader = __ffsll(todo) - 1;
-                const uint32_t lk = __shfl(o.loc, leader);
-                const unsigned long long same = __ballot(o.loc == lk) & todo;
+                const uint32_t lk = __shfl(cloc, leader);
+                const unsigned long long same = __ballot(cloc == lk) & todo;
                 if ((threadIdx.x & 63) == (uint32_t)leader) {
                     if (use_hist) atomicAdd(&hist[lk], (uint32_t)__popcll(same));
                     else atomicAdd(&counters[lk], (unsigned long long)__popcll(same));
@@ -1268,8 +1331,8 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
                 todo &= ~same;
             }
             if ((todo >> (threadIdx.x & 63)) & 1ull) {
-                if (use_hist) atomicAdd(&hist[o.loc], 1u);
-                else atomicAdd(&counters[o.loc], 1ull);
+                if (use_hist) atomicAdd(&hist[cloc], 1u);
+                else atomicAdd(&counters[cloc], 1ull);
             }
         }
         if (TAIL) continue;

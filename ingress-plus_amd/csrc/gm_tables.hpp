@@ -373,6 +373,7 @@ struct TabHeader {
     uint64_t off_realip, off_cidrs;
     uint64_t off_alw_rl;           // always-run members' rule lists (zones << 24 | rule)
     uint64_t off_lit_chk;          // DLitChk per DLit
+    uint32_t n_wild, pad_wild;     // wildcard server names (both tables)
 };
 // The route's hot tables -- ports, the three name tables, servers, server ifs, small-location
 // lists, locations and the name strings -- are laid out first and contiguously in the image;
@@ -404,6 +405,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const DLitChk *lit_chk;
     uint32_t n_always_lds, n_alw_groups, n_alw_slices, n_rsl, n_rk_prefilter;
     uint32_t n_ports, names_mask, wild_head_mask, wild_tail_mask, edges_mask, lit_mask;
+    uint32_t n_wild;             // wildcard server names (0: k_route skips the wildcard step)
     uint32_t n_locs, n_sigs, n_sig_regex, n_always, n_lits, bloom_log2, bloom_mul, bloom_pk, ctx_mul;
     uint32_t gen;
     // this struct's copy in device memory: a kernel hands *self (not its kernel argument) to
