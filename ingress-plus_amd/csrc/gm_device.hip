@@ -657,6 +657,7 @@ struct RouteOut {
     uint32_t server, loc, ups, status;
     uint8_t action, kind, bucket, match;
     uint16_t waf;
+    uint16_t slow, pad;  // FAST route_one: the request needs an out-of-line step (the SLOW pass)
     int32_t pend_best;   // a request deferred to the regex-location kernels: its longest prefix match
 };
 
@@ -934,6 +935,7 @@ __device__ __forceinline__ void route_prefetch(const uint8_t *A, uint64_t alen, 
 // RLOC_BM_BITS regex locations (longer URIs / larger servers run rloc_prefiltered in the lane)
 constexpr uint32_t RLOC_URI_CAP = 256, RLOC_BM_BITS = 2048;
 constexpr uint32_t RLOC_STATUS_WORD = 16;   // batch status word: requests deferred to k_rloc
+constexpr uint32_t SLOW_STATUS_WORD = 17;   // batch status word: requests for k_route's SLOW pass
 // rk_in: RK_INLINE -- a prefiltered regex step runs here; RK_DEFER -- one that k_rloc can take
 // (URI <= RLOC_URI_CAP, n_rloc <= RLOC_BM_BITS) sets *pend and returns; >= -1 -- k_rloc's answer
 // (the location index, -1 none).  *sid_out: the server chosen (valid whenever *pend is set).
@@ -945,7 +947,6 @@ __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, co
 // check needs them (kept in registers across the location walk they cost the route spills)
 __device__ __forceinline__ uint32_t req_body_len(const gm_req *rp) { return reinterpret_cast<const uint32_t *>(rp)[5]; }
 __device__ __forceinline__ bool req_chunked(const gm_req *rp) { return reinterpret_cast<const uint32_t *>(rp)[9] & GM_REQ_CHUNKED; }
-__device__ __forceinline__ uint32_t req_flags(const gm_req *rp) { return reinterpret_cast<const uint32_t *>(rp)[9] & 0xFFu; }
 template <bool FAST>
 __device__ __forceinline__ void route_locphase(const uint8_t *A, const gm_req *rp, const Rec &r, const RoutePre &pre,
                                                const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb,
@@ -954,19 +955,20 @@ __device__ __forceinline__ void route_locphase(const uint8_t *A, const gm_req *r
 __device__ __forceinline__ void too_large(RouteOut &o) {
     o.action = GM_ACT_TOO_LARGE; o.status = 413; o.ups = GM_NONE; o.waf = GM_WAF_OFF;
 }
-// FAST: no out-of-line call while the host / URI words and the record are live.  A call there
-// made the compiler keep them in scratch around it -- stored and reloaded for every request, call
-// or not: the route took 1.05 ms alone per 10M C4 requests with the calls in place, 0.70 without.
-// So the wildcard step is inlined, an IPv6 literal host takes the arena-byte path, and the server
-// `if`s that need a call run after the location phase (where little is live): the first of them
-// that returns (or cannot be evaluated) replaces the location's result, as it would have ended the
-// request before that phase.  The rules / split / regex-location calls come after the words die.
+// FAST: no out-of-line call at all.  A call anywhere in the step made the compiler keep the
+// step's values (the record, the host / URI words, addresses) in scratch around it -- stored and
+// reloaded for every request, whether it calls or not: the route took 1.05 ms alone per 10M C4
+// requests with the calls in the kernel, 0.63 with none.  The wildcard step is inlined, an IPv6
+// literal host takes the arena-byte path; a request that needs a generic server `if`, the
+// regex-location prefilter or a rules / split route stops with o.slow set, and k_route's SLOW
+// pass (a second launch over the list of such requests) routes it again with the calls.
 template <bool FAST = false>
 __device__ __forceinline__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const RoutePre &pre,
                           const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb, int32_t rk_in = RK_INLINE,
                           bool *pend = nullptr) {
     o.server = GM_NONE; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0;
     o.action = GM_ACT_NO_LISTENER; o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF;
+    o.slow = 0;
     o.pend_best = -1;
     const uint64_t f_uri = r.base, f_host = r.base + r.uri_len + r.args_len + r.hdr_len + r.body_len;
     // ---- listen port
@@ -1009,7 +1011,6 @@ __device__ __forceinline__ void route_one(const uint8_t *A, uint64_t alen, const
     if (bad || (P.ssl && !https)) { o.action = GM_ACT_BAD_REQUEST; o.status = 400; return; }
     const DServer S = h.servers[sid];
     // ---- server rewrite phase
-    uint32_t sif = GM_NONE;   // FAST: the first `if` left until after the location phase
     for (uint32_t i = 0; i < S.n_if; i++) {
         const DServerIf f = h.server_ifs[S.first_if + i];
         bool hit;
@@ -1017,7 +1018,7 @@ __device__ __forceinline__ void route_one(const uint8_t *A, uint64_t alen, const
         else if (f.op == SIF_FLAGS) hit = (f.tt >> (r.flags & 3)) & 1u;
         else if (f.op == 0xFF) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; return; }
         else {
-            if (FAST) { sif = i; break; }   // this one and the rest: after the location phase
+            if (FAST) { o.slow = 1; return; }
             const int g = server_if_generic(A, rp, *t.self, S.first_if + i, S.realip);
             if (g < 0) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; return; }
             hit = g != 0;
@@ -1025,22 +1026,6 @@ __device__ __forceinline__ void route_one(const uint8_t *A, uint64_t alen, const
         if (hit) { o.action = is_redirect(f.code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = f.code; return; }
     }
     route_locphase<FAST>(A, rp, r, pre, t, h, o, rkb, rk_in, pend, S, sid);
-    if (FAST && sif != GM_NONE) {
-        for (uint32_t i = sif; i < S.n_if; i++) {
-            const DServerIf f = h.server_ifs[S.first_if + i];
-            int g;
-            if (f.op == SIF_RETURN) g = 1;
-            else if (f.op == SIF_FLAGS) g = (f.tt >> (req_flags(rp) & 3)) & 1u;
-            else if (f.op == 0xFF) g = -1;
-            else g = server_if_generic(A, rp, *t.self, S.first_if + i, S.realip);
-            if (g == 0) continue;
-            o.loc = GM_NONE; o.ups = GM_NONE; o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF;
-            o.waf = GM_WAF_OFF;
-            if (g < 0) { o.action = GM_ACT_UNSUPPORTED; o.status = 0; }
-            else { o.action = is_redirect(f.code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = f.code; }
-            break;
-        }
-    }
 }
 
 // route_one's location phase: trie walk (exact, longest prefix, auto_redirect), then regex
@@ -1130,6 +1115,8 @@ __device__ __forceinline__ void route_locphase(const uint8_t *A, const gm_req *r
                 *pend = true;
                 o.pend_best = best;
                 return;
+            } else if (FAST) {   // (a server without regex locations: none matches)
+                if (S.rk_on || S.n_rloc) { o.slow = 1; return; }
             } else loc = rloc_first_match(*t.self, S, sid, u, r.uri_len, rkb);
             if (loc < 0) loc = best;
         }
@@ -1157,6 +1144,7 @@ __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, co
     DLoc L = h.locs[loc];
     if (!chunked && blen > L.body_max) { too_large(o); return; }
     uint32_t fin = (uint32_t)loc;
+    if (FAST && (L.kind == LK_IRL_RULES || L.kind == LK_IRL_SPLIT)) { o.slow = 1; return; }
     if (L.kind == LK_IRL_RULES) {
         const DRules R = t.rules[L.route];
         const int idx = rules_generic(A, rp, *t.self, L.route, h.servers[o.server].realip);
@@ -1229,7 +1217,10 @@ inline uint32_t route_lds(const GTab &t, bool beside) { return route_hot16(t) + 
 // u: its $uri's first 32 bytes (two uint4; the slices' first two 16-byte steps read them instead
 // of an arena line each)
 struct RlocQ { uint2 *list; uint32_t *count; int32_t *loc; uint4 *st; int32_t *best; uint4 *u; };
-template <int WPE, bool RK = false, bool TAIL = false>
+// SLOW: the second pass over the requests a FAST pass listed (q.list / q.count): the whole route
+// with its out-of-line steps, the verdict and the location counter (blk2rec and the hit counts
+// were written by the first pass)
+template <int WPE, bool RK = false, bool TAIL = false, bool SLOW = false>
 __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE))) void k_route(const gm_req *__restrict__ reqs, uint32_t n,
                                                        const uint8_t *__restrict__ A, uint64_t arena_len,
                                                        GTab tg, gm_verdict *__restrict__ out,
@@ -1270,9 +1261,10 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
     __shared__ uint32_t rkb[RK ? RK_BLOOM_WORDS : 1];
     if (RK) for (uint32_t k = threadIdx.x; k < RK_BLOOM_WORDS; k += blockDim.x) rkb[k] = t.rk_bloom[k];
     __syncthreads();
-    const uint32_t nn = TAIL ? *q.count : n;
+    const uint32_t nn = TAIL || SLOW ? *q.count : n;
     const uint32_t stride = gridDim.x * blockDim.x;
-    constexpr bool FASTK = !RK && !TAIL;   // route_one without calls while its words are live
+    // no out-of-line call in the first pass (the requests that need one go to q.list)
+    constexpr bool FASTK = !RK && !TAIL && !SLOW;
     for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < nn; x += stride) {
         uint32_t i = x;
         RouteOut o;
@@ -1287,15 +1279,28 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
             int32_t loc = q.loc[x];
             if (loc < 0) loc = q.best[x];
             o.server = e.y; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0; o.action = GM_ACT_NO_LISTENER;
-            o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF; o.pend_best = -1;
+            o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF; o.pend_best = -1; o.slow = 0;
             route_loc(A, reqs + i, t, h, loc, o);
         } else {
+            if (SLOW) i = q.list[x].x;
             r = load_rec(reqs + i);
             route_prefetch(A, arena_len, r, pre);
             route_one<FASTK>(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
                              RK && q.list ? RK_DEFER : RK_INLINE, &pend);
         }
-        const uint32_t cloc = o.loc;
+        const bool slow = FASTK && o.slow;
+        if (FASTK) {   // to the SLOW pass, one atomic per wave
+            const unsigned long long sm = __ballot(slow);
+            if (sm) {
+                const uint32_t lane = threadIdx.x & 63;
+                const int leader = __ffsll(sm) - 1;
+                uint32_t b = 0;
+                if (lane == (uint32_t)leader) b = atomicAdd(q.count, (uint32_t)__popcll(sm));
+                b = __shfl(b, leader);
+                if (slow) q.list[b + (uint32_t)__popcll(sm & ((1ull << lane) - 1))] = make_uint2(i, 0u);
+            }
+        }
+        const uint32_t cloc = slow ? GM_NONE : o.loc;   // (counted by the SLOW pass)
         if (RK && !TAIL) {   // deferred to k_rloc: appended, one atomic per wave
             const unsigned long long pm = __ballot(pend);
             if (pm) {
@@ -1314,7 +1319,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
                 }
             }
         }
-        if (!pend) write_verdict(out + i, t, o);
+        if (!pend && !slow) write_verdict(out + i, t, o);
         // per-location counter: the wave's first few distinct locations in one atomic each for all
         // their lanes (most waves: one to three locations), any lane left after four rounds its
         // own atomic (C3's ~50 distinct locations per wave took a round each)
@@ -1335,7 +1340,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
                 else atomicAdd(&counters[cloc], 1ull);
             }
         }
-        if (TAIL) continue;
+        if (TAIL || SLOW) continue;
         if (hcnt) {   // the WAF stages' per-request hit counts start the batch at zero
             hcnt[i] = 0;
             if (i + 1 == n) hcnt[n] = 0;
@@ -1447,6 +1452,7 @@ struct Scratch {
     int32_t *d_rqb = nullptr; size_t cap_rqb = 0;        // and its longest prefix match (the tail pass)
     unsigned long long *d_rqm = nullptr; size_t cap_rqm = 0;   // and its prefiltered-slice mask
     unsigned long long *d_bctr = nullptr; size_t cap_bctr = 0; // this batch's counters (k_ctr_commit)
+    uint2 *d_slow = nullptr; size_t cap_slow = 0;              // requests for k_route's SLOW pass
     unsigned long long *d_agree = nullptr, *h_agree = nullptr;  // gm_counters_allreduce's agreement words
     // the last gm_match_batch's arguments: gm_sync re-runs a batch whose dedupe set overflowed
     // (OV_SET) with the set doubled, until it fits -- only the caller's hit_cap voids a batch
@@ -1464,7 +1470,7 @@ struct Scratch {
                         (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp, (void *)d_wscr, (void *)d_wsum,
                         (void *)d_pk, (void *)d_pseg, (void *)d_pprog, (void *)d_ppat, (void *)d_ptemp,
                         (void *)d_usize, (void *)d_utemp, (void *)d_sreqs, (void *)d_sarena, (void *)d_sblk,
-                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm, (void *)d_rqu, (void *)d_bctr})
+                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm, (void *)d_rqu, (void *)d_bctr, (void *)d_slow})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
         if (h_agree) (void)hipHostFree(h_agree);
@@ -1879,6 +1885,13 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
             (e2 = grow(c, s, S->d_rqm, S->cap_rqm, n)) || (e2 = grow(c, s, S->d_rqu, S->cap_rqu, 2 * (size_t)n + 1))) return e2;
         q = RlocQ{S->d_rq, S->d_status + RLOC_STATUS_WORD, S->d_rql, S->d_rqs, S->d_rqb, S->d_rqu};
     }
+    // the first (FAST) route pass lists the requests that need an out-of-line step; the SLOW pass
+    // routes them (the RK passes keep their calls in line)
+    RlocQ qs{};
+    if (!rk) {
+        if (int e2 = grow(c, s, S->d_slow, S->cap_slow, n)) return e2;
+        qs.list = S->d_slow; qs.count = S->d_status + SLOW_STATUS_WORD;
+    }
     auto launch_rloc = [&](hipStream_t rs, uint32_t tail_blocks) -> int {
         // union-DFA slices of the servers that have them (config order: a request answered by one
         // slice skips the later ones), then the factor prefilter for the others
@@ -1921,7 +1934,12 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     };
     if (!waf) {
         if (rk) GM_ROUTE_LAUNCH(3, true, false, route_blocks, route_lds(t, false), s, reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), q);
-        else GM_ROUTE_LAUNCH(3, false, false, route_blocks, route_lds(t, false), s, reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), RlocQ{});
+        else {
+            GM_ROUTE_LAUNCH(3, false, false, route_blocks, route_lds(t, false), s, reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), qs);
+            HIPCHK(c, hipGetLastError());
+            k_route<3, false, false, true><<<route_blocks, ROUTE_BLOCK, route_lds(t, false), s>>>(
+                reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), qs);
+        }
         HIPCHK(c, hipGetLastError());
         if (rk) {
             const int e4 = launch_rloc(s, route_blocks);
@@ -2018,8 +2036,12 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         // early instead of stretching past the scan
         if (rk)
             GM_ROUTE_LAUNCH(GM_ROUTE_WPE, true, false, nb, route_lds(t, !serial), rs, reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial), q);
-        else
-            GM_ROUTE_LAUNCH(GM_ROUTE_WPE, false, false, nb, route_lds(t, !serial), rs, reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial), RlocQ{});
+        else {
+            GM_ROUTE_LAUNCH(GM_ROUTE_WPE, false, false, nb, route_lds(t, !serial), rs, reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial), qs);
+            HIPCHK(c, hipGetLastError());
+            k_route<GM_ROUTE_WPE, false, false, true><<<nb, ROUTE_BLOCK, route_lds(t, !serial), rs>>>(
+                reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial), qs);
+        }
         HIPCHK(c, hipGetLastError());
         int e3;
         if (rk && (e3 = launch_rloc(rs, nb))) return e3;
