@@ -2009,7 +2009,8 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     const bool serial = c->flags & GM_CREATE_SERIAL;
     hipStream_t rs = serial ? s : S->side;
 #ifndef GM_ROUTE_BPC
-#define GM_ROUTE_BPC 2   // route blocks per CU beside the scan (1: 5.86, 2: 5.41, 3: 5.60 ms per C4 step)
+#define GM_ROUTE_BPC 1   // route blocks per CU beside the scan (round 4, the call-free route: 1: 4.91,
+                         // 2: 5.09 ms per C4 step; before it, 1: 5.86, 2: 5.41, 3: 5.60)
 #endif
 #ifndef GM_ROUTE_PRIO
 #define GM_ROUTE_PRIO 0  // 1: the route at raised issue priority beside the scan (5.32 vs 5.06 ms per C4 step)
@@ -2027,8 +2028,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         HIPCHK(c, hipStreamWaitEvent(S->side, S->ev_fork, 0));
     }
     auto launch_route = [&]() -> int {
-        // beside the scan, 2 route blocks per CU: 1 leaves the route the tail of the step, 3+
-        // steal issue slots from the scan (measured on C4: 6.75 / 5.88 / 5.99 ms per step)
+        // beside the scan, GM_ROUTE_BPC route blocks per CU (more steal issue slots from the scan)
         const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
                                                                      (uint32_t)c->cu_count * (serial || route_after ? 8 : GM_ROUTE_BPC)));
         if (prof) HIPCHK(c, hipEventRecord(S->ev_route[0], rs));
@@ -2934,8 +2934,8 @@ static constexpr uint32_t kBuildFlags =
     defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_SCAN_NOBRANCH) || defined(GM_SCAN_VMASK)
     GM_BUILD_EXPERIMENT |
 #endif
-#if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 4 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != 32 || \
-    GM_ROUTE_BPC != 2 || GM_ROUTE_PRIO != 0 || GM_ROUTE_WPE != GM_ROUTE_WPE_SHIPPED || GM_EXP_GRIDMUL != 8 || \
+#if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != 32 || \
+    GM_ROUTE_BPC != 1 || GM_ROUTE_PRIO != 0 || GM_ROUTE_WPE != GM_ROUTE_WPE_SHIPPED || GM_EXP_GRIDMUL != 8 || \
     GM_EXP_WPE != 3 || GM_RLOC_CTX != 1 || GM_RLOC_PREF != 0 || GM_ALW_SLICE_GROUPS != 8 || GM_WIRE_WPE != 8 || \
     GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1 || GM_EXACT_BPC != 6 || !defined(GM_DFA_INL_SHIPPED)
     GM_BUILD_TUNING |
