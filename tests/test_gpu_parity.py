@@ -220,6 +220,35 @@ def test_waf_zone_boundaries(eng):
     assert (exp["n_hits"] >= 2).sum() > 3000
 
 
+def test_waf_prefix_regex_dfa_entry(eng):
+    """Prefix-mode regexes (k_waf_exact starts their anchored DFA after the verified prefix
+    literal, DLit.dfa_entry): case-insensitive prefixes, a case-sensitive regex whose prefix has
+    letters (no skip: the literal matches any case), a letter-free case-sensitive prefix (skip), a
+    regex that accepts right after its prefix, and `$` with the zone ending at, or one newline
+    after, the match -- against the oracle's PCRE."""
+    rules = [sigs.Rule("re", True, "ab", r"(abcd|efgh)\d+x"), sigs.Rule("re", False, "ab", r"Qwerty[0-9]{2}"),
+             sigs.Rule("re", False, "ab", r"12345[a-z]+"), sigs.Rule("re", True, "ab", r"wxyz\d*"),
+             sigs.Rule("re", False, "ab", r"mnopq\d+$"), sigs.Rule("re", True, "ab", r"zyxwv[^>]{0,4}on")]
+    b = workloads.c4_blob(sigs.SigSet(rules))
+    bodies = [b"ABCD12x", b"abcd12", b"..efgh9x", b"abcdx", b"qwerty12", b"Qwerty12", b"QWERTY12",
+              b"12345abc", b"12345", b"x12345Z", b"WXYZ", b"wxyz", b"mnopq12", b"mnopq12\n", b"mnopq12x",
+              b"mnopq12\n\n", b"ZYXWVabon", b"zyxwvabcdeon", b"zyxwv on", b"efgh", b"abcd9", b"abcd9X"]
+    items = []
+    for i, body in enumerate(bodies * 3):
+        it = {"host": "cafe.example.com", "uri": "/tea/x", "https": True}
+        pad = b"." * (i % 5)
+        if i % 2:
+            it["body"] = pad + body
+        else:
+            it["args"] = (pad + body).decode()
+            it["body"] = b"-" * (i % 3)
+        items.append(it)
+    reqs, arena = records.from_dicts(items)
+    got, gh, exp, eh = run_both(eng, b, reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "prefix-dfa-entry")
+    assert (exp["n_hits"] > 0).sum() > 20
+
+
 def test_e2e_kats_on_gpu(eng):
     adv = golden("advanced_routing.json")
     for case in adv["cases"]:
