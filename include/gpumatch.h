@@ -100,7 +100,12 @@ typedef struct gm_req {
                               /* gm_match_batch answers GM_ACT_BAD_REQUEST with that status     */
 #define GM_REQ_CHUNKED 0x10u  /* the body came chunked (Transfer-Encoding: chunked; body_len =  */
                               /* the decoded length): client_max_body_size applies when the     */
-                              /* proxying location reads it, not to a Content-Length up front   */
+                              /* proxying location reads it, not to a Content-Length up front.  */
+                              /* Set it for ANY body whose length was not announced up front --  */
+                              /* an HTTP/2 request whose DATA frames came without a              */
+                              /* content-length header included (nginx: content_length_n == -1);*/
+                              /* without it body_len is taken as a Content-Length (413 at find-  */
+                              /* config time, whatever the location does)                        */
 
 typedef struct gm_batch {
     const gm_req  *reqs;      /* n headers (device pointer unless GM_BATCH_HOST)          */

@@ -2424,7 +2424,7 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.key_parts = (const DKeyPart *)(b + h.off_key_parts);
     t.points = (const DPoint *)(b + h.off_points);
     t.peer_init = (const uint32_t *)(b + h.off_peer_init);
-    t.n_ups = h.n_ups; t.n_peers = h.n_peers;
+    t.n_ups = h.n_ups; t.n_peers = h.n_peers; t.n_servers = h.n_servers;
     t.loc_uri = (const DLocUri *)(b + h.off_loc_uri);
     t.decoders = h.decoders;
     t.alw = (const DAlwGroup *)(b + h.off_alw);

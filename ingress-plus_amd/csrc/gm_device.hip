@@ -2055,12 +2055,13 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
 #endif
     if (serial && (e = launch_route())) return e;
     if (mark(1)) return GM_E_HIP;
+    const uint32_t bcap = (uint32_t)std::min<size_t>(S->cap_surv / scan_blocks, 0xFFFFFFFFu);   // survivors per workgroup
     // persistent scan grid: one 1024-thread workgroup per CU (128 KiB LDS prefilter); every wave
     // owns a contiguous arena range and a private candidate region of wcap records
-    if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
-    else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
-    else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
-    else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks);
+    if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
+    else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
+    else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
+    else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
     HIPCHK(c, hipGetLastError());
     if (!serial && route_after) {   // the route beside the context filter, after the scan
         HIPCHK(c, hipEventRecord(S->ev_fork, s));
@@ -2072,7 +2073,6 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     if (!serial && route_after && (e = launch_route())) return e;
 #endif
     if (mark(2)) return GM_E_HIP;
-    const uint32_t bcap = (uint32_t)std::min<size_t>(S->cap_surv / scan_blocks, 0xFFFFFFFFu);
     // the continuation of overflowed candidate / survivor regions (a no-op launch otherwise)
     auto launch_direct = [&](const uint8_t *DA, uint64_t dl, const gm_req *DR, const uint32_t *b2r, const Dedup &d,
                              const uint64_t *dlp) -> int {
@@ -2088,7 +2088,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         return GM_OK;
     };
     k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, S->d_ccnt, W, t, S->d_surv, bcap, S->d_ccnt + W,
-                                                S->d_status, S->d_ccnt + 2 * W + scan_blocks);
+                                                S->d_status, S->d_ccnt + 2 * W + scan_blocks, GM_SCAN_CTX != 0);
     HIPCHK(c, hipGetLastError());
     // join: blk2rec, the verdicts and the zeroed counts are complete before the exact check
     if (!serial) HIPCHK(c, hipStreamWaitEvent(s, S->ev_join, 0));
@@ -2135,13 +2135,13 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         dd2.jepoch = S->epoch + 1;
         const uint8_t *SA = S->d_sarena;
         const gm_req *SR = S->d_sreqs;
-        if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
-        else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
-        else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
-        else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks);
+        if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
+        else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
+        else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
+        else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
         HIPCHK(c, hipGetLastError());
         k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, S->d_ccnt, W, t, S->d_surv, bcap, S->d_ccnt + W,
-                                                    S->d_status, S->d_ccnt + 2 * W + scan_blocks);
+                                                    S->d_status, S->d_ccnt + 2 * W + scan_blocks, GM_SCAN_CTX != 0);
         HIPCHK(c, hipGetLastError());
         k_waf_exact<<<exact_blocks, EXACT_BLOCK, 0, s>>>(SA, scap, SR, n, S->d_sblk, t, S->d_surv, bcap,
                                                          S->d_ccnt + W, scan_blocks, S->d_pairs, (uint32_t)S->cap_pairs,
@@ -2934,7 +2934,7 @@ static constexpr uint32_t kBuildFlags =
     defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_SCAN_NOBRANCH) || defined(GM_SCAN_VMASK)
     GM_BUILD_EXPERIMENT |
 #endif
-#if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != 32 || \
+#if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != (GM_SCAN_CTX ? 63 : 32) || GM_SCAN_CTX != 0 || GM_CTX_FLUSH != 32 || \
     GM_ROUTE_BPC != 1 || GM_ROUTE_PRIO != 0 || GM_ROUTE_WPE != GM_ROUTE_WPE_SHIPPED || GM_EXP_GRIDMUL != 8 || \
     GM_EXP_WPE != 3 || GM_RLOC_CTX != 1 || GM_RLOC_PREF != 0 || GM_ALW_SLICE_GROUPS != 8 || GM_WIRE_WPE != 8 || \
     GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1 || GM_EXACT_BPC != 6 || !defined(GM_DFA_INL_SHIPPED)

@@ -395,7 +395,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const uint8_t *name_bytes;
     const uint8_t *hot_base; uint32_t hot_len;   // the hot prefix (hot_len 0: larger than ROUTE_STAGE_BYTES)
     const DUpstream *ups; const DKeyPart *key_parts; const DPoint *points; const uint32_t *peer_init;
-    uint32_t n_ups, n_peers;
+    uint32_t n_ups, n_peers, n_servers;
     const DLocUri *loc_uri;
     uint32_t decoders;
     const DAlwGroup *alw; const DAlwSlice *alw_slices; const uint8_t *alw_pack; const uint32_t *alw_rule;

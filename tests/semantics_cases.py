@@ -57,6 +57,13 @@ def body_limit_case():
         ({"host": "other.example.com", "uri": "/", "body": b"d" * 9}, RETURN),           # default server's 404
         ({"host": "other.example.com", "uri": "/", "body": b"d" * big}, TOO_LARGE),      # before `return 404`
         ({"host": "other.example.com", "uri": "/", "body": b"d" * big, "chunked": True}, RETURN),
+        # HTTP/2 DATA frames without a content-length header: nginx's content_length_n is -1, so
+        # only a location that reads the body checks it -- the caller marks such a record
+        # GM_REQ_CHUNKED (gpumatch.h); parity-unpinned (no reference fixture covers HTTP/2 bodies)
+        ({"host": h, "uri": "/coffee", "body": b"z" * 2000, "chunked": True, "http2": True}, AUTO_301),
+        ({"host": "other.example.com", "uri": "/", "body": b"d" * big, "chunked": True, "http2": True}, RETURN),
+        ({"host": h, "uri": "/tea", "body": b"x" * 1025, "chunked": True, "http2": True}, TOO_LARGE),
+        ({"host": h, "uri": "/tea", "body": b"x" * 1025, "http2": True}, TOO_LARGE),   # with content-length
     ]
     return b, cases
 

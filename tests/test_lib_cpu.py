@@ -221,3 +221,46 @@ def test_in_tree_library_is_the_default_build():
     e.load(workloads.c1_blob(), 1)
     st = e.stats()
     assert st["build_flags"] == 0 and st["scratch_scale"] == 1.0 and st["set_shift"] == 0
+
+
+# The largest private segment (scratch per lane) any shipped kernel may have. The route's realip
+# instances are the largest (~1.8 KiB: the header walk's out-of-line leaves and their saves).
+PRIVATE_SEGMENT_MAX = 2048
+LLVM_BIN = "/opt/rocm/lib/llvm/bin"
+
+
+def _kernel_metadata(lib_path, tmp_path):
+    """The gfx950 code object's kernel descriptors: (name, uses_dynamic_stack, private bytes)."""
+    import subprocess
+    fb, co = str(tmp_path / "fatbin"), str(tmp_path / "gfx950.o")
+    subprocess.check_call([f"{LLVM_BIN}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}",
+                           lib_path, str(tmp_path / "stripped.so")])
+    subprocess.check_call([f"{LLVM_BIN}/clang-offload-bundler", "--unbundle", "--type=o",
+                           f"--input={fb}", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
+                           f"--output={co}"])
+    notes = subprocess.check_output([f"{LLVM_BIN}/llvm-readelf", "--notes", co], text=True)
+    out = []
+    for blk in notes.split("  - .agpr_count")[1:]:
+        name = re.search(r"\.name:\s+(\S+)", blk).group(1)
+        dyn = re.search(r"\.uses_dynamic_stack:\s+(\w+)", blk).group(1) == "true"
+        priv = int(re.search(r"\.private_segment_fixed_size:\s+(\d+)", blk).group(1))
+        out.append((name, dyn, priv))
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(f"{LLVM_BIN}/clang-offload-bundler"),
+                    reason="ROCm LLVM tools absent")
+def test_no_kernel_has_a_dynamic_stack(tmp_path):
+    """Round 4's illegal memory access (test_peer_selection_long_sequential_runs): a recursive
+    device function (parse_addr calling itself for an IPv6 address's dotted tail) gave k_peer_pick
+    `uses_dynamic_stack: true` beside a 1536 B fixed private segment. The runtime sizes scratch
+    from the fixed part, so the recursion's frames ran past the lane's scratch. Any recursive,
+    alloca or indirect call brings the dynamic stack back: fail the build, and bound the fixed
+    private segment every kernel may use."""
+    md = _kernel_metadata(engine.LIB_PATH, tmp_path)
+    assert len(md) > 100, "no gfx950 kernels found in libgpumatch.so"
+    assert any(n.startswith("_ZN12_GLOBAL__N_111k_waf_scan") or "k_waf_scan" in n for n, _, _ in md)
+    dyn = [n for n, d, _ in md if d]
+    assert not dyn, f"kernels with a dynamic stack: {dyn}"
+    big = [(n, p) for n, _, p in md if p > PRIVATE_SEGMENT_MAX]
+    assert not big, f"kernels over {PRIVATE_SEGMENT_MAX} B of private segment: {big}"
