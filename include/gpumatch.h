@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 7u   /* 7: GM_ACT_TOO_LARGE, GM_REQ_CHUNKED, gm_rejects, build flags; 6: n_rsl_reversed;
+#define GM_ABI_VERSION 8u   /* 8: PROXY protocol (gm_wire_msg 128 B, $proxy_protocol_addr in gm_req), last_redo;
+                               7: GM_ACT_TOO_LARGE, GM_REQ_CHUNKED, gm_rejects, build flags; 6: n_rsl_reversed;
                                5: gm_update_upstream / gm_peers_migrate; 4: union-DFA stats */
 
 /* ---------------------------------------------------------------- status codes */
@@ -65,6 +66,9 @@ extern "C" {
  * record is contiguous at arena[base ...] in this fixed field order (so only lengths are
  * stored):
  *     uri | args | hdrs | body | host | method | ruri | raddr
+ * followed by `paddr` (paddr_len = pad0[0] bytes): $proxy_protocol_addr, the source address of the
+ * connection's PROXY protocol header (`listen ... proxy_protocol`), its source port in pad1[0..1]
+ * (little-endian); paddr_len 0: no PROXY address (not a proxy_protocol listener, or "UNKNOWN").
  * The first four are the WAF-scanned zones.  `hdrs` is the header block exactly as parsed:
  * lines "Name: value\r\n" (the space after ':' optional; leading / trailing spaces of a value are
  * not part of it, tabs are -- nginx's header parser).
@@ -87,9 +91,9 @@ typedef struct gm_req {
     uint16_t port;          /* local listen port ($server_port)                             */
     uint16_t remote_port;
     uint8_t  flags;         /* GM_REQ_*                                                    */
-    uint8_t  pad0[3];
+    uint8_t  pad0[3];       /* [0] paddr_len; [1..2] GM_REQ_INVALID's HTTP status           */
     uint8_t  rid[16];       /* $request_id raw bytes                                        */
-    uint8_t  pad1[8];
+    uint8_t  pad1[8];       /* [0..1] $proxy_protocol_port                                  */
 } gm_req;
 
 #define GM_REQ_HTTPS   0x01u  /* connection is TLS: $scheme = https, $https = on          */
@@ -224,12 +228,15 @@ typedef struct gm_stats_t {
     uint32_t build_flags;
     /* the internal WAF capacity scale in effect (GM_CREATE_SCRATCH_SHIFT test hook; 1.0 normally) */
     float    scratch_scale;
-    /* batches gm_sync re-ran because the WAF dedupe set overflowed (cumulative, this ctx) */
+    /* WAF passes gm_sync ran because a dedupe set overflowed (cumulative, this ctx): continuation
+     * passes over the requests to redo, and whole re-runs of a stream's earlier batches */
     uint32_t n_set_reruns;
     uint32_t set_shift;          /* GM_CREATE_SET_SHIFT in effect (0 normally) */
     /* always-run union members: one per distinct (pattern, nocase) among the always-run regexes */
     uint32_t n_alw_members;
-    uint32_t reserved_stats[2];
+    /* the last dedupe-set continuation (gm_sync): requests redone, of the batch's */
+    uint32_t last_redo;
+    uint32_t reserved_stats[1];
 } gm_stats_t;
 
 /* gm_stats_t.build_flags: measurement / test variants compiled into the library.  bench.py refuses
@@ -323,13 +330,27 @@ typedef struct gm_wire_msg {
     uint32_t len;
     uint16_t port;            /* local listen port ($server_port)                          */
     uint16_t remote_port;
-    uint8_t  flags;           /* connection: GM_REQ_HTTPS, GM_REQ_HTTP2                    */
+    uint8_t  flags;           /* connection: GM_REQ_HTTPS, GM_REQ_HTTP2, GM_WIRE_PROXY_DONE */
     uint8_t  raddr_len;       /* $remote_addr text length, <= 40                           */
-    uint8_t  pad[2];
+    uint8_t  paddr_len;       /* GM_WIRE_PROXY_DONE: the connection's $proxy_protocol_addr  */
+    uint8_t  pad;
     uint8_t  rid[16];         /* $request_id raw bytes                                     */
-    uint8_t  raddr[40];       /* $remote_addr text                                         */
-    uint8_t  pad2[4];
-} gm_wire_msg;                /* 80 B */
+    uint8_t  raddr[40];       /* $remote_addr text (the TCP peer)                          */
+    uint16_t proxy_port;      /* GM_WIRE_PROXY_DONE: the connection's $proxy_protocol_port  */
+    uint8_t  pad2[2];
+    uint8_t  paddr[46];       /* GM_WIRE_PROXY_DONE: $proxy_protocol_addr text             */
+    uint8_t  pad3[2];
+} gm_wire_msg;                /* 128 B */
+/* PROXY protocol (`listen <port> proxy_protocol`, ConfigMap proxy-protocol: configmaps.go:145,
+ * nginx.ingress.tmpl:33,38, nginx.virtualserver.tmpl:35,40, nginx.tmpl:82-83).  A message on such a
+ * port is the start of its connection: it begins with a PROXY v1 ("PROXY TCP4 <src> <dst> <sport>
+ * <dport>\r\n", "PROXY UNKNOWN ...\r\n") or v2 (binary) header, which nginx reads before the
+ * request (ngx_proxy_protocol_read): its source address and port go to the record (paddr); a
+ * missing or broken header closes the connection with no response -- the record is GM_REQ_INVALID
+ * with status 444 (nginx's "close without a response" code).  GM_WIRE_PROXY_DONE marks a later
+ * (keep-alive) request of such a connection: no header is read, and the caller hands the
+ * connection's address in paddr / paddr_len / proxy_port (e.g. from its first request's record). */
+#define GM_WIRE_PROXY_DONE 0x40u
 
 /* Parse n requests into gm_req records + a payload arena (field order of gm_req, records
  * 16-B aligned and packed in request order).  Device pointers, asynchronous on `stream`;

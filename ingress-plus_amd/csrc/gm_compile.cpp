@@ -182,6 +182,7 @@ struct UpstreamIR {
     uint32_t method = UM_RR;
     std::string key;                 // hash / hash consistent key (complex value)
     bool defer = false;              // a construct the engine does not model
+    std::string sticky;              // NGINX Plus `sticky cookie <name> ...`: the cookie's name
     struct Peer { std::string addr; bool down = false; };
     std::vector<Peer> peers;
 };
@@ -347,6 +348,7 @@ struct Builder {
                 for (size_t q = 2; q < k.a.size(); q++) {
                     if (k.a[q] == "ssl") fl |= 1;
                     if (k.a[q] == "default_server" || k.a[q] == "default") fl |= 2;
+                    if (k.a[q] == "proxy_protocol") fl |= 4;
                 }
                 S.listens.push_back({port, fl});
             } else if (n == "server_name") {
@@ -429,8 +431,13 @@ struct Builder {
                 else if (k.a[1] == "two" && (k.a.size() == 2 || (k.a.size() == 3 && k.a[2] == "least_conn")))
                     U.method = UM_RANDOM2;
                 else U.defer = true;   // random two least_time=... (Plus)
+            } else if (m == "sticky" && k.a.size() >= 3 && k.a[1] == "cookie") {
+                // NGINX Plus session persistence (nginx-plus.ingress.tmpl:10, nginx.com/sticky-cookie-
+                // services, annotations.go:390-395): expires / domain / path / httponly / secure only
+                // shape the Set-Cookie of the response, not the choice
+                U.sticky = k.a[2];
             } else if (m == "least_time" || m == "sticky" || m == "queue" || m == "ntlm" || m == "hash") {
-                U.defer = true;
+                U.defer = true;   // sticky route / learn, ...
             }
             // keepalive, zone, keepalive_timeout / _requests: connection reuse, not the choice
         }
@@ -1301,6 +1308,53 @@ void chash_ring(const std::vector<std::string> &addrs, std::vector<DPoint> &poin
 }
 
 // ============================================================================ entry
+
+// RFC 1321 MD5 (the NGINX Plus sticky cookie's value is the hex MD5 of the peer's address text)
+static void md5_digest(const std::string &msg, uint32_t out[4]) {
+    static const uint32_t K[64] = {
+        0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501,
+        0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821,
+        0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+        0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a,
+        0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70,
+        0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+        0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+        0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+    static const int R[64] = {7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22,
+                              5, 9, 14, 20, 5, 9, 14, 20, 5, 9, 14, 20, 5, 9, 14, 20,
+                              4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23,
+                              6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21};
+    std::vector<uint8_t> m(msg.begin(), msg.end());
+    const uint64_t bits = (uint64_t)msg.size() * 8;
+    m.push_back(0x80);
+    while (m.size() % 64 != 56) m.push_back(0);
+    for (int i = 0; i < 8; i++) m.push_back((uint8_t)(bits >> (8 * i)));
+    uint32_t h[4] = {0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476};
+    for (size_t o = 0; o < m.size(); o += 64) {
+        uint32_t w[16];
+        for (int i = 0; i < 16; i++)
+            w[i] = m[o + 4 * i] | m[o + 4 * i + 1] << 8 | m[o + 4 * i + 2] << 16 | (uint32_t)m[o + 4 * i + 3] << 24;
+        uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
+        for (int i = 0; i < 64; i++) {
+            uint32_t f, g;
+            if (i < 16) { f = (b & c) | (~b & d); g = i; }
+            else if (i < 32) { f = (d & b) | (~d & c); g = (5 * i + 1) % 16; }
+            else if (i < 48) { f = b ^ c ^ d; g = (3 * i + 5) % 16; }
+            else { f = c ^ (b | ~d); g = (7 * i) % 16; }
+            const uint32_t x = a + f + K[i] + w[g];
+            a = d; d = c; c = b;
+            b = b + (x << R[i] | x >> (32 - R[i]));
+        }
+        h[0] += a; h[1] += b; h[2] += c; h[3] += d;
+    }
+    for (int i = 0; i < 4; i++) out[i] = h[i];   // little-endian words: bytes in digest order
+}
+static void put_md5(std::vector<uint32_t> &v, const std::string &addr) {
+    uint32_t d[4];
+    md5_digest(addr, d);
+    v.insert(v.end(), d, d + 4);
+}
+
 CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) {
     CompileResult R;
     gm_stats_t &st = R.stats;
@@ -1387,6 +1441,10 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 R.peer_ups.push_back((uint32_t)u);
             }
             bool defer = U->defer;
+            if (!U->sticky.empty()) {
+                const int sid = C.src("$cookie_" + U->sticky);
+                if (sid < 0) defer = true; else D.sticky = 1u + (uint32_t)sid;
+            }
             UpstreamMeta &um = R.ups_meta[u];
             um.has_block = true;
             um.method = U->method;
@@ -1445,19 +1503,20 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     // ---- ports
     std::vector<DPort> ports;
     std::map<int, int> port_idx;
+    std::set<int> def_seen;   // ports whose default_server is set (the first `default_server` wins)
     for (auto &S : M.servers)
         for (auto &l : S.listens) {
             auto it = port_idx.find(l.first);
             if (it == port_idx.end()) {
                 port_idx[l.first] = (int)ports.size();
-                ports.push_back(DPort{(uint32_t)l.first, 0, (uint32_t)S.id, 0xFFFFFFFFu});
+                ports.push_back(DPort{(uint32_t)l.first, 0, (uint32_t)S.id, 0u});
                 it = port_idx.find(l.first);
             }
             DPort &P = ports[it->second];
             if (l.second & 1) P.ssl = 1;
-            if ((l.second & 2) && P.pad == 0xFFFFFFFFu) { P.default_server = (uint32_t)S.id; P.pad = 0; }
+            if (l.second & 4) P.proxy = 1;   // proxy_protocol: ORed over the port's listens (ngx_http_add_addresses)
+            if ((l.second & 2) && !def_seen.count(l.first)) { P.default_server = (uint32_t)S.id; def_seen.insert(l.first); }
         }
-    for (auto &P : ports) P.pad = 0;
 
     // ---- server names: exact / wildcard-head / wildcard-tail hash tables, first wins
     struct NameKey { std::string name; int port; uint32_t server; };
@@ -1591,8 +1650,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 else if (hdr == "proxy_protocol") ri.type = RIP_PROXY;
                 else { ri.type = RIP_HEADER; ri.hdr_off = C.put_bytes(lower(hdr)); ri.hdr_len = (uint32_t)hdr.size(); }
                 // the address nginx would use is unknown to the engine: a hostname in
-                // set_real_ip_from, or the PROXY protocol header the records do not carry --
-                // requests whose verdict reads $remote_addr / $remote_port defer
+                // set_real_ip_from -- requests whose verdict reads $remote_addr / $remote_port
+                // defer (proxy_protocol reads the record's PROXY address, gm_parse_requests)
                 if (bad) { ri.type = RIP_UNKNOWN; st.n_rejected_other++; R.rejects.push_back("server: set_real_ip_from (not an address)"); }
                 D.realip = (uint32_t)realips.size();
                 realips.push_back(ri);
@@ -2268,6 +2327,11 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.n_key_parts = (uint32_t)key_parts.size(); h.n_points = (uint32_t)points.size();
     h.off_ups = I.put(dups); h.off_key_parts = I.put(key_parts); h.off_points = I.put(points);
     h.off_peer_init = I.put(peer_init);
+    {
+        std::vector<uint32_t> peer_md5;
+        for (const std::string &a : R.peer_addrs) put_md5(peer_md5, a);
+        h.off_peer_md5 = I.put(peer_md5);
+    }
     h.off_loc_uri = I.put(dluri);
     h.decoders = decoders;
     C.bytes.resize(C.bytes.size() + 64, 0);   // slack: vector compares may over-read
@@ -2367,6 +2431,11 @@ CompileResult update_upstream(const CompileResult &live, const std::string &name
     std::vector<uint8_t> bytes(b + h0.off_bytes, b + h0.total);
     h.off_ups = I.put(dups); h.off_key_parts = I.put(key_parts); h.off_points = I.put(points);
     h.off_peer_init = I.put(peer_init);
+    {
+        std::vector<uint32_t> peer_md5;
+        for (const std::string &a : R.peer_addrs) put_md5(peer_md5, a);
+        h.off_peer_md5 = I.put(peer_md5);
+    }
     h.off_loc_uri = I.put(dluri);
     h.off_bytes = I.put(bytes);
     I.buf.resize((I.buf.size() + 255) & ~size_t(255), 0);
@@ -2424,6 +2493,7 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.key_parts = (const DKeyPart *)(b + h.off_key_parts);
     t.points = (const DPoint *)(b + h.off_points);
     t.peer_init = (const uint32_t *)(b + h.off_peer_init);
+    t.peer_md5 = (const uint32_t *)(b + h.off_peer_md5);
     t.n_ups = h.n_ups; t.n_peers = h.n_peers; t.n_servers = h.n_servers;
     t.loc_uri = (const DLocUri *)(b + h.off_loc_uri);
     t.decoders = h.decoders;

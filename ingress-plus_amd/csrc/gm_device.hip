@@ -19,7 +19,9 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <chrono>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <atomic>
@@ -45,6 +47,7 @@ struct Rec {
     uint32_t port, rport, flags;
     uint32_t bad_status;     // GM_REQ_INVALID: the wire parser's HTTP status (pad0[1..2])
     uint32_t rid[4];
+    uint32_t paddr_len, pport;   // $proxy_protocol_addr (after raddr; pad0[0]) and its port (pad1[0..1])
 };
 
 __device__ __forceinline__ Rec load_rec(const gm_req *r) {
@@ -56,6 +59,7 @@ __device__ __forceinline__ Rec load_rec(const gm_req *r) {
     x.host_len = b.z & 0xFFFF; x.method_len = b.z >> 16; x.ruri_len = b.w & 0xFFFF; x.raddr_len = b.w >> 16;
     x.port = c.x & 0xFFFF; x.rport = c.x >> 16; x.flags = c.y & 0xFF; x.bad_status = c.y >> 16;   // pad0[1] | pad0[2] << 8
     x.rid[0] = c.z; x.rid[1] = c.w; x.rid[2] = d.x; x.rid[3] = d.y;
+    x.paddr_len = (c.y >> 8) & 0xFF; x.pport = d.z & 0xFFFF;
     return x;
 }
 
@@ -413,11 +417,16 @@ __device__ __noinline__ void realip_eval(Ctx &c, const GTab &t) {
     c.rip_state = RIPS_SAME;
     const uint32_t type = R->type;
     if (type == RIP_UNKNOWN) { c.rip_state = RIPS_UNKNOWN; return; }
-    if (type == RIP_PROXY) {   // the PROXY protocol address is not in the record
-        if (rip_trusted(t, R, a)) c.rip_state = RIPS_UNKNOWN;
-        return;
+    int rc;
+    if (type == RIP_PROXY) {
+        // ngx_http_realip_handler, NGX_HTTP_REALIP_PROXY: the connection's PROXY header address
+        // (none: declined) through ngx_http_get_forwarded_addr, then its port
+        if (c.r.paddr_len == 0) return;
+        rc = rip_forwarded(t, R, A + c.raddr + c.r.raddr_len, c.r.paddr_len, c.ra, c.ra_tmp);
+        if (rc != RIP_DECLINED) a.port = c.r.pport;
+    } else {
+        rc = type == RIP_XFWD ? rip_xfwd(c, t, R) : rip_one_header(c, t, R);
     }
-    const int rc = type == RIP_XFWD ? rip_xfwd(c, t, R) : rip_one_header(c, t, R);
     if (rc == RIP_DECLINED) return;
     c.ra_len = d_addr_text(a, c.ra_txt);
     c.rip_state = RIPS_NEW;
@@ -1400,6 +1409,8 @@ struct Generation {
     }
 };
 
+// batches a stream may hold before gm_sync (the next gm_match_batch completes them first)
+constexpr uint32_t PENDING_MAX = 64;
 // Everything one batch writes, per (ctx, stream): batches on different streams never share a
 // buffer, so gm_match_batch is thread-safe per ctx + stream pair without a ctx-wide lock.
 struct Scratch {
@@ -1433,6 +1444,7 @@ struct Scratch {
     uint8_t *d_wtemp = nullptr; size_t cap_wtemp = 0;
     uint8_t *d_wscr = nullptr; size_t cap_wscr = 0;   // the wire parser's per-wave $uri scratch
     uint8_t *d_wsum = nullptr; size_t cap_wsum = 0;   // and its pass-1 summaries (WireSum, 80 B each)
+    gm_wire_msg *d_wmsg = nullptr; size_t cap_wmsg = 0;   // and the descriptors past their PROXY headers
     uint32_t *d_pk = nullptr; size_t cap_pk = 0;     // peer selection: keys, values (x2: sorted),
     uint32_t *d_pseg = nullptr; size_t cap_pseg = 0; // per-upstream ranges, periodic programs
     uint4 *d_pprog = nullptr; size_t cap_pprog = 0;
@@ -1454,25 +1466,43 @@ struct Scratch {
     unsigned long long *d_bctr = nullptr; size_t cap_bctr = 0; // this batch's counters (k_ctr_commit)
     uint2 *d_slow = nullptr; size_t cap_slow = 0;              // requests for k_route's SLOW pass
     unsigned long long *d_agree = nullptr, *h_agree = nullptr;  // gm_counters_allreduce's agreement words
-    // the last gm_match_batch's arguments: gm_sync re-runs a batch whose dedupe set overflowed
-    // (OV_SET) with the set doubled, until it fits -- only the caller's hit_cap voids a batch
+    // gm_sync's continuation of an OV_SET batch: the requests to redo (bitmap, list), their sub-batch
+    uint32_t *d_redo = nullptr; size_t cap_redo = 0;
+    uint32_t *d_rlist = nullptr; size_t cap_rlist = 0;
+    uint64_t *d_rsize = nullptr, *d_rbase = nullptr; size_t cap_rsize = 0, cap_rbase = 0;
+    uint8_t *d_rtemp = nullptr; size_t cap_rtemp = 0;
+    gm_req *d_rsreq = nullptr; size_t cap_rsreq = 0;
+    uint8_t *d_rsarena = nullptr; size_t cap_rsarena = 0;
+    gm_verdict *d_rsout = nullptr; size_t cap_rsout = 0;
+    uint32_t *d_rsblk = nullptr; size_t cap_rsblk = 0;
+    uint32_t *d_rscnt = nullptr; size_t cap_rscnt = 0;
+    // each pending batch's final overflow bits (k_ctr_commit), one word per batch since the last
+    // gm_sync: later batches do not clear an earlier one's
+    uint32_t *d_ovlog = nullptr, *h_ovlog = nullptr;
+    // the batches enqueued since the last gm_sync, with their arguments: gm_sync completes a batch
+    // whose dedupe set overflowed (OV_SET) -- only the caller's hit_cap voids a batch
     struct Replay {
-        bool valid = false;
+        uint32_t slot = 0;   // its word of d_ovlog
         const void *gen = nullptr; uint64_t seq = 0;
         const gm_req *reqs = nullptr; const uint8_t *A = nullptr; uint64_t alen = 0; uint32_t n = 0;
         gm_verdict *out = nullptr; uint32_t *hits = nullptr; size_t hit_cap = 0; const uint64_t *dlen = nullptr;
         // GM_BATCH_HOST: the staged device copies and the caller's host buffers
         gm_verdict *h_out = nullptr; uint32_t *h_hits = nullptr; size_t h_hit_cap = 0;
-    } replay;
+    };
+    std::vector<Replay> pending;
+    bool last_is_batch = false;   // the stream's last call was a gm_match_batch (its scratch in place)
     ~Scratch() {
         for (void *p : {(void *)d_status, (void *)d_blk2rec, (void *)d_cand, (void *)d_surv, (void *)d_pairs,
                         (void *)d_jobs, (void *)d_set, (void *)d_cnt, (void *)d_start, (void *)d_ccnt,
                         (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp, (void *)d_wscr, (void *)d_wsum,
                         (void *)d_pk, (void *)d_pseg, (void *)d_pprog, (void *)d_ppat, (void *)d_ptemp,
                         (void *)d_usize, (void *)d_utemp, (void *)d_sreqs, (void *)d_sarena, (void *)d_sblk,
-                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm, (void *)d_rqu, (void *)d_bctr, (void *)d_slow})
+                        (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm, (void *)d_rqu, (void *)d_bctr, (void *)d_slow,
+                        (void *)d_redo, (void *)d_rlist, (void *)d_rsize, (void *)d_rbase, (void *)d_rtemp, (void *)d_rsreq,
+                        (void *)d_rsarena, (void *)d_rsout, (void *)d_rsblk, (void *)d_rscnt, (void *)d_ovlog, (void *)d_wmsg})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
+        if (h_ovlog) (void)hipHostFree(h_ovlog);
         if (h_agree) (void)hipHostFree(h_agree);
         if (d_agree) (void)hipFree(d_agree);
         for (auto &e : ev) if (e) (void)hipEventDestroy(e);
@@ -1491,6 +1521,7 @@ struct gm_ctx {
     double cap_scale = 1.0;                   // GM_CREATE_SCRATCH_SHIFT (test hook): internal WAF capacities
     uint32_t set_shift = 0;                   // GM_CREATE_SET_SHIFT (test hook): the dedupe set
     std::atomic<uint32_t> n_set_reruns{0};    // gm_sync re-runs of OV_SET batches
+    std::atomic<uint32_t> last_redo{0};       // requests the last continuation redid
     std::shared_mutex gen_mu;                 // shared: enqueueing batches; exclusive: the swap
     Generation *gen = nullptr;
     uint64_t publish_seq = 0;                 // bumped under gen_mu (exclusive) by every publish
@@ -1549,6 +1580,9 @@ static Scratch *scratch_for(gm_ctx *c, hipStream_t stream) {
     if (hipMalloc((void **)&s->d_status, STATUS_WORDS * 4) != hipSuccess ||
         hipHostMalloc((void **)&s->h_status, STATUS_WORDS * 4, hipHostMallocDefault) != hipSuccess ||
         hipMemset(s->d_status, 0, STATUS_WORDS * 4) != hipSuccess ||
+        hipMalloc((void **)&s->d_ovlog, PENDING_MAX * 4) != hipSuccess ||
+        hipHostMalloc((void **)&s->h_ovlog, PENDING_MAX * 4, hipHostMallocDefault) != hipSuccess ||
+        hipMemset(s->d_ovlog, 0, PENDING_MAX * 4) != hipSuccess ||
         hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming) != hipSuccess ||
@@ -1786,6 +1820,7 @@ int gm_stats(gm_ctx *c, gm_stats_t *out) {
     out->build_flags = build_flags();
     out->scratch_scale = (float)c->cap_scale;
     out->n_set_reruns = c->n_set_reruns.load();
+    out->last_redo = c->last_redo.load();
     out->set_shift = c->set_shift;
     std::lock_guard<std::mutex> l2(c->last_mu);
     out->last_candidates = c->last_candidates;
@@ -1844,8 +1879,229 @@ static int launch_always(gm_ctx *c, hipStream_t s, const Generation *g, const ui
     return GM_OK;
 }
 
+// ---- the WAF stages of one pass, shared by a batch (beside its route) and gm_sync's dedupe-set
+// continuation (a sub-batch of the requests to redo)
+struct WafCaps {
+    uint32_t scan_blocks, W, wcap, bcap, exact_blocks;
+    size_t scan_tmp;
+    uint32_t *xprof;
+    u32x4 *cand;
+};
+struct WafIO {
+    const uint8_t *A; uint64_t alen; const uint64_t *dlen;
+    const gm_req *reqs; uint32_t n;
+    const gm_verdict *out;     // verdicts (waf_active, the decoders' location)
+    const uint32_t *blk2rec;   // arena block -> first record (the route writes the batch's)
+    uint32_t nblk;
+};
+#ifndef GM_EXACT_BPC
+#define GM_EXACT_BPC 6
+#endif
+// grow the pair list keeping its first `keep` entries (the continuation appends to the first pass's)
+static int grow_keep(gm_ctx *c, hipStream_t s, unsigned long long *&p, size_t &cap, size_t need, size_t keep) {
+    if (need <= cap) return GM_OK;
+    unsigned long long *np = nullptr;
+    const size_t nc = need + need / 4;
+    HIPCHK(c, hipMalloc((void **)&np, nc * 8));
+    if (p && keep) HIPCHK(c, hipMemcpyAsync(np, p, std::min(keep, cap) * 8, hipMemcpyDeviceToDevice, s));
+    if (p) { HIPCHK(c, hipStreamSynchronize(s)); HIPCHK(c, hipFree(p)); }
+    p = np; cap = nc;
+    return GM_OK;
+}
+// capacities (host-known: the arena length and the request count, never a device count) and the
+// buffers grown to them; keep_pairs: entries of the pair list to preserve across a growth
+static int waf_buffers(gm_ctx *c, Scratch *S, uint64_t alen, uint32_t n, WafCaps &k, size_t keep_pairs = 0) {
+    hipStream_t s = S->stream;
+    int e;
+    // candidate records: 32 B (4 x u64) each, room for one per 64 arena bytes; survivors; unique
+    // pairs (2 per request on average) and jobs (1 per request); overflow is reported, never
+    // truncated silently
+    k.scan_blocks = (uint32_t)c->cu_count;
+    k.W = k.scan_blocks * SCAN_WAVES;
+    const uint32_t W = k.W;
+    // (GM_CREATE_SCRATCH_SHIFT, a test hook: scales these defaults, so the overflow continuations run on
+    // batches small enough for the oracle)
+    const double sc = c->cap_scale;
+    auto scaled = [sc](size_t x, size_t lo) { return std::max<size_t>(lo, (size_t)((double)x * sc)); };
+    const size_t ccap = scaled(4 * (alen / 64 + 16384) * S->cand_mult, 4 * W);
+    const size_t pcap0 = ((size_t)n * 2 + 65536) * S->list_mult, jcap0 = ((size_t)n + 65536) * S->list_mult;
+    const size_t pcap = scaled(pcap0, 64) + keep_pairs, jcap = scaled(jcap0, 64);
+    // the dedupe set holds every unique pair and job of the batch (the lists' fallback when they
+    // overflow): sized from the unscaled list capacities
+    size_t set_need = 1;
+    while (set_need < 2 * (pcap0 + jcap0)) set_need <<= 1;
+    set_need = std::max<size_t>(set_need >> c->set_shift, 1024);
+    k.scan_tmp = 0;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, k.scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
+    if ((e = grow(c, s, S->d_cand, S->cap_cand, std::max<size_t>(ccap, scaled((size_t)W * 4096, 4 * W))))) return e;
+    // scan-wave counts, ctx-block counts, scan-wave resume chunks, ctx-region resume records,
+    // then k_waf_exact's per-workgroup profiling partials (4 words each)
+    k.exact_blocks = (uint32_t)c->cu_count * GM_EXACT_BPC;
+    if ((e = grow(c, s, S->d_ccnt, S->cap_ccnt, 3 * (size_t)W + k.scan_blocks + 4 * (size_t)k.exact_blocks))) return e;
+    k.xprof = S->d_ccnt + 3 * (size_t)W + k.scan_blocks;
+    if ((e = grow(c, s, S->d_surv, S->cap_surv, std::min<size_t>(scaled((alen / 256 + 65536) * S->surv_mult, k.scan_blocks),
+                                                                 0xFFFFFFFFu)))) return e;
+    if ((e = grow_keep(c, s, S->d_pairs, S->cap_pairs, pcap, keep_pairs))) return e;
+    if ((e = grow(c, s, S->d_jobs, S->cap_jobs, jcap))) return e;
+    if ((e = grow(c, s, S->d_cnt, S->cap_cnt, (size_t)n + 1))) return e;
+    if ((e = grow(c, s, S->d_start, S->cap_start, (size_t)n + 1))) return e;
+    if ((e = grow(c, s, S->d_temp, S->cap_temp, k.scan_tmp))) return e;
+    if (set_need > S->cap_set) {
+        if ((e = grow(c, s, S->d_set, S->cap_set, set_need))) return e;
+        S->cap_set = set_need;   // exactly a power of two: the probe mask
+        S->epoch = 0;
+        HIPCHK(c, hipMemsetAsync(S->d_set, 0, S->cap_set * 8, s));
+    }
+    k.wcap = (uint32_t)std::min<size_t>(S->cap_cand / 4 / W, 0xFFFFFFFFu);   // records per wave
+    k.bcap = (uint32_t)std::min<size_t>(S->cap_surv / k.scan_blocks, 0xFFFFFFFFu);   // survivors per workgroup
+    k.cand = reinterpret_cast<u32x4 *>(S->d_cand);
+    return GM_OK;
+}
+// one epoch per pass over the set (two with decoders: the decoded pass's jobs take epoch + 1)
+static int next_epoch(gm_ctx *c, Scratch *S, const GTab &t) {
+    S->epoch += t.decoders ? 2 : 1;
+    if (S->epoch + (t.decoders ? 1 : 0) > 255) {   // epoch wrap: every slot becomes free again
+        S->epoch = 1;
+        HIPCHK(c, hipMemsetAsync(S->d_set, 0, S->cap_set * 8, S->stream));
+    }
+    return GM_OK;
+}
+
+static int launch_scan(gm_ctx *c, Scratch *S, const GTab &t, const WafCaps &k, const uint8_t *A, uint64_t alen,
+                       const uint64_t *dlen) {
+    hipStream_t s = S->stream;
+    const uint32_t W = k.W;
+#define GM_SCAN(PKV) k_waf_scan<PKV, SCAN_DEPTH><<<k.scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, k.cand, k.wcap, \
+        S->d_ccnt, dlen, S->d_ccnt + W + k.scan_blocks)
+    if (t.bloom_pk == BLOOM_PK_PERM) GM_SCAN(BLOOM_PK_PERM);
+    else if (t.bloom_pk == 1) GM_SCAN(1);
+    else if (t.bloom_pk == 2) GM_SCAN(2);
+    else GM_SCAN(3);
+#undef GM_SCAN
+    HIPCHK(c, hipGetLastError());
+    return GM_OK;
+}
+
+// scan -> (route_hook: the route beside it) -> context filter -> (join: the route's outputs) ->
+// exact check -> overflow continuation -> regex jobs -> always-run regexes, then the same stages
+// over the decoded views when the signature set declares parsers
+static int waf_stages(gm_ctx *c, Scratch *S, const Generation *g, const WafCaps &k, const WafIO &io, const Dedup &dd,
+                      const std::function<int()> &route_hook, bool join, const std::function<int(int)> &mark) {
+    hipStream_t s = S->stream;
+    const GTab &t = g->tab;
+    const uint32_t W = k.W, scan_blocks = k.scan_blocks, n = io.n;
+    int e;
+    // persistent scan grid: one 1024-thread workgroup per CU (128 KiB LDS prefilter); every wave
+    // owns a contiguous arena range and a private candidate region of wcap records
+    if ((e = launch_scan(c, S, t, k, io.A, io.alen, io.dlen))) return e;
+    if (route_hook && (e = route_hook())) return e;
+    if (mark(2)) return GM_E_HIP;
+    // the continuation of overflowed candidate / survivor regions (a no-op launch otherwise)
+    auto launch_direct = [&](const uint8_t *DA, uint64_t dl, const gm_req *DR, const uint32_t *b2r, const Dedup &d,
+                             const uint64_t *dlp) -> int {
+        uint32_t *res = S->d_ccnt + W + scan_blocks, *cres = S->d_ccnt + 2 * W + scan_blocks;
+#define GM_DIRECT(PKV) k_waf_direct<PKV><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(DA, dl, DR, n, b2r, t, k.cand, k.wcap, \
+            S->d_ccnt, res, cres, S->d_pairs, (uint32_t)S->cap_pairs, S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, d, dlp)
+        if (t.bloom_pk == BLOOM_PK_PERM) GM_DIRECT(BLOOM_PK_PERM);
+        else if (t.bloom_pk == 1) GM_DIRECT(1);
+        else if (t.bloom_pk == 2) GM_DIRECT(2);
+        else GM_DIRECT(3);
+#undef GM_DIRECT
+        HIPCHK(c, hipGetLastError());
+        return GM_OK;
+    };
+    auto launch_ctx = [&]() -> int {
+        k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(k.cand, k.wcap, S->d_ccnt, W, t, S->d_surv, k.bcap, S->d_ccnt + W,
+                                                    S->d_status, S->d_ccnt + 2 * W + scan_blocks);
+        HIPCHK(c, hipGetLastError());
+        return GM_OK;
+    };
+    auto launch_exact = [&](const uint8_t *XA, uint64_t xl, const gm_req *XR, const uint32_t *b2r, const Dedup &d,
+                            const uint64_t *xlp) -> int {
+        // persistent exact check: EXACT_BPC workgroups per CU, all resident
+        k_waf_exact<<<k.exact_blocks, EXACT_BLOCK, 0, s>>>(XA, xl, XR, n, b2r, t, S->d_surv, k.bcap,
+                                                           S->d_ccnt + W, scan_blocks, S->d_pairs, (uint32_t)S->cap_pairs,
+                                                           S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, d, xlp, k.xprof);
+        HIPCHK(c, hipGetLastError());
+        k_exact_prof<<<1, 256, 0, s>>>(k.xprof, k.exact_blocks, S->d_status);
+        HIPCHK(c, hipGetLastError());
+        return GM_OK;
+    };
+    if ((e = launch_ctx())) return e;
+    // join: blk2rec, the verdicts and the zeroed counts are complete before the exact check
+    if (join) HIPCHK(c, hipStreamWaitEvent(s, S->ev_join, 0));
+    if ((e = launch_exact(io.A, io.alen, io.reqs, io.blk2rec, dd, io.dlen))) return e;
+    if ((e = launch_direct(io.A, io.alen, io.reqs, io.blk2rec, dd, io.dlen))) return e;
+    if (mark(3)) return GM_E_HIP;
+    if (t.n_sig_regex) {
+        k_waf_regex<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(io.A, io.reqs, t, S->d_jobs, (uint32_t)S->cap_jobs, S->d_pairs,
+                                                               (uint32_t)S->cap_pairs, dd);
+        HIPCHK(c, hipGetLastError());
+    }
+    if ((e = launch_always(c, s, g, io.A, io.alen, io.reqs, n, S, dd, false, io.dlen))) return e;
+    if (!t.decoders) return GM_OK;
+    // ---- the request parsers' decoded views (gm_decode.inc): shadow records, same indices,
+    // then the WAF stages once more over them; hits land in the same dedupe set and counts
+    const size_t scap = 2 * (size_t)io.alen + 32 * (size_t)n + 4096;   // a view <= 2x its zones
+    const uint32_t snblk = (uint32_t)((scap >> BLK_SHIFT) + 1);
+    if ((e = grow(c, s, S->d_sreqs, S->cap_sreqs, (size_t)n))) return e;
+    if ((e = grow(c, s, S->d_sarena, S->cap_sarena, scap))) return e;
+    if ((e = grow(c, s, S->d_sblk, S->cap_sblk, snblk))) return e;
+    if ((e = grow(c, s, S->d_ssize, S->cap_ssize, (size_t)n + 2))) return e;
+    if ((e = grow(c, s, S->d_sbase, S->cap_sbase, (size_t)n + 2))) return e;
+    size_t dtmp = 0;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, dtmp, S->d_ssize, S->d_sbase, (int)n + 1, s));
+    if ((e = grow(c, s, S->d_stemp, S->cap_stemp, dtmp))) return e;
+    const uint32_t dblocks = (n + 255) / 256;
+    k_dec_size<<<dblocks, 256, 0, s>>>(io.reqs, io.A, n, t, io.out, S->d_ssize);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_stemp, dtmp, S->d_ssize, S->d_sbase, (int)n + 1, s));
+    uint64_t *slen = S->d_sbase + n + 1;   // the shadow arena's length, on the device
+    k_dec_emit<<<dblocks, 256, 0, s>>>(io.reqs, io.A, n, t, io.out, S->d_sbase, S->d_sreqs, S->d_sarena, scap,
+                                       S->d_sblk, snblk, slen, S->d_status);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemsetAsync(S->d_status + 2, 0, 4, s));   // the job list restarts (pairs continue)
+    k_status_pass<<<1, 64, 0, s>>>(S->d_status);   // the continuations restart too
+    HIPCHK(c, hipGetLastError());
+    Dedup dd2 = dd;
+    dd2.jepoch = dd.epoch + 1;
+    const uint8_t *SA = S->d_sarena;
+    const gm_req *SR = S->d_sreqs;
+    if ((e = launch_scan(c, S, t, k, SA, scap, slen))) return e;
+    if ((e = launch_ctx())) return e;
+    if ((e = launch_exact(SA, scap, SR, S->d_sblk, dd2, slen))) return e;
+    if ((e = launch_direct(SA, scap, SR, S->d_sblk, dd2, slen))) return e;
+    if (t.n_sig_regex) {
+        k_waf_regex<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(SA, SR, t, S->d_jobs, (uint32_t)S->cap_jobs, S->d_pairs,
+                                                               (uint32_t)S->cap_pairs, dd2);
+        HIPCHK(c, hipGetLastError());
+    }
+    return launch_always(c, s, g, SA, scap, SR, n, S, dd2, true, slen);
+}
+
+// hit emission: offsets by an exclusive scan of the per-request counts (request order), the
+// pairs into their slots, each request's ids sorted (continuation: remap / redo / np1, see
+// k_hits_scatter)
+static int emit_hits(gm_ctx *c, Scratch *S, const Generation *g, uint32_t n, gm_verdict *out, uint32_t *hit_ids,
+                     size_t hit_cap, unsigned long long *ctr, const Dedup &dd, const uint32_t *redo, uint32_t np1,
+                     const uint32_t *remap) {
+    hipStream_t s = S->stream;
+    size_t scan_tmp = 0;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
+    if (int e = grow(c, s, S->d_temp, S->cap_temp, scan_tmp)) return e;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_temp, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
+    k_hits_scatter<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(S->d_pairs, (uint32_t)S->cap_pairs, S->d_cnt, S->d_start,
+                                                              hit_ids, hit_cap, ctr, g->tab.n_locs, S->d_status, dd,
+                                                              redo, np1, remap);
+    HIPCHK(c, hipGetLastError());
+    k_hits_finalize<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8)), 256, 0, s>>>(
+        S->d_start, n, out, hit_ids, hit_cap, S->d_status);
+    HIPCHK(c, hipGetLastError());
+    return GM_OK;
+}
+
 static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *reqs, const uint8_t *A, uint64_t alen,
-                     uint32_t n, gm_verdict *out, uint32_t *hit_ids, size_t hit_cap, const uint64_t *dlen) {
+                     uint32_t n, gm_verdict *out, uint32_t *hit_ids, size_t hit_cap, const uint64_t *dlen, uint32_t slot) {
     hipStream_t s = S->stream;
     const GTab &t = g->tab;
     const bool waf = t.n_sigs > 0 && (t.n_lits > 0 || t.n_sig_regex > 0);
@@ -1866,7 +2122,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     HIPCHK(c, hipMemsetAsync(S->d_bctr, 0, nctr * 8, s));
     auto commit = [&]() -> int {
         k_ctr_commit<<<std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)((nctr + 255) / 256), (uint32_t)c->cu_count)), 256, 0, s>>>(
-            S->d_bctr, g->d_counters, (uint32_t)g->n_counters, S->d_status);
+            S->d_bctr, g->d_counters, (uint32_t)g->n_counters, S->d_status, S->d_ovlog + slot);
         HIPCHK(c, hipGetLastError());
         return GM_OK;
     };
@@ -1949,58 +2205,14 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         return mark(1) ? GM_E_HIP : GM_OK;
     }
     int e;
-    // ---- capacities (host-known: the arena length and the request count, never a device count)
-    // candidate records: 32 B (4 x u64) each, room for one per 64 arena bytes; survivors; unique
-    // pairs (2 per request on average) and jobs (1 per request); overflow is reported, never
-    // truncated silently
-    const uint32_t scan_blocks = (uint32_t)c->cu_count;
-    const uint32_t W = scan_blocks * SCAN_WAVES;
-    // (GM_CREATE_SCRATCH_SHIFT, a test hook: scales these defaults, so the overflow continuations run on
-    // batches small enough for the oracle)
-    const double sc = c->cap_scale;
-    auto scaled = [sc](size_t x, size_t lo) { return std::max<size_t>(lo, (size_t)((double)x * sc)); };
-    const size_t ccap = scaled(4 * (alen / 64 + 16384) * S->cand_mult, 4 * W);
-    const size_t pcap0 = ((size_t)n * 2 + 65536) * S->list_mult, jcap0 = ((size_t)n + 65536) * S->list_mult;
-    const size_t pcap = scaled(pcap0, 64), jcap = scaled(jcap0, 64);
-    // the dedupe set holds every unique pair and job of the batch (the lists' fallback when they
-    // overflow): sized from the unscaled list capacities
-    size_t set_need = 1;
-    while (set_need < 2 * (pcap0 + jcap0)) set_need <<= 1;
-    set_need = std::max<size_t>(set_need >> c->set_shift, 1024);
-    size_t scan_tmp = 0;
-    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
+    WafCaps k{};
+    if ((e = waf_buffers(c, S, alen, n, k))) return e;
     if ((e = grow(c, s, S->d_blk2rec, S->cap_blk, nblk))) return e;
-    if ((e = grow(c, s, S->d_cand, S->cap_cand, std::max<size_t>(ccap, scaled((size_t)W * 4096, 4 * W))))) return e;
-    // scan-wave counts, ctx-block counts, scan-wave resume chunks, ctx-region resume records,
-    // then k_waf_exact's per-workgroup profiling partials (4 words each)
-#ifndef GM_EXACT_BPC
-#define GM_EXACT_BPC 6
-#endif
-    const uint32_t exact_blocks = (uint32_t)c->cu_count * GM_EXACT_BPC;
-    if ((e = grow(c, s, S->d_ccnt, S->cap_ccnt, 3 * (size_t)W + scan_blocks + 4 * (size_t)exact_blocks))) return e;
-    uint32_t *const xprof = S->d_ccnt + 3 * (size_t)W + scan_blocks;
-    if ((e = grow(c, s, S->d_surv, S->cap_surv, std::min<size_t>(scaled((alen / 256 + 65536) * S->surv_mult, scan_blocks),
-                                                                 0xFFFFFFFFu)))) return e;
-    if ((e = grow(c, s, S->d_pairs, S->cap_pairs, pcap))) return e;
-    if ((e = grow(c, s, S->d_jobs, S->cap_jobs, jcap))) return e;
-    if ((e = grow(c, s, S->d_cnt, S->cap_cnt, (size_t)n + 1))) return e;
-    if ((e = grow(c, s, S->d_start, S->cap_start, (size_t)n + 1))) return e;
-    if ((e = grow(c, s, S->d_temp, S->cap_temp, scan_tmp))) return e;
-    if (set_need > S->cap_set) {
-        if ((e = grow(c, s, S->d_set, S->cap_set, set_need))) return e;
-        S->cap_set = set_need;   // exactly a power of two: the probe mask
-        S->epoch = 0;
-        HIPCHK(c, hipMemsetAsync(S->d_set, 0, S->cap_set * 8, s));
-    }
+    if ((e = grow(c, s, S->d_redo, S->cap_redo, ((size_t)n + 31) / 32))) return e;
+    HIPCHK(c, hipMemsetAsync(S->d_redo, 0, (((size_t)n + 31) / 32) * 4, s));
     // one epoch per batch (two with decoders: the decoded pass's jobs take epoch + 1)
-    S->epoch += t.decoders ? 2 : 1;
-    if (S->epoch + (t.decoders ? 1 : 0) > 255) {   // epoch wrap: every slot becomes free again
-        S->epoch = 1;
-        HIPCHK(c, hipMemsetAsync(S->d_set, 0, S->cap_set * 8, s));
-    }
-    const uint32_t wcap = (uint32_t)std::min<size_t>(S->cap_cand / 4 / W, 0xFFFFFFFFu);   // records per wave
-    u32x4 *cand = reinterpret_cast<u32x4 *>(S->d_cand);
-    Dedup dd{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, out, S->d_cnt, S->d_status};
+    if ((e = next_epoch(c, S, t))) return e;
+    Dedup dd{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, out, S->d_cnt, S->d_status, S->d_redo};
 
     // ---- fork: k_route on the side stream, beside the WAF scan (independent inputs; its waves
     // fit beside the scan's one workgroup per CU; issued after the scan so the scan claims the
@@ -2015,25 +2227,15 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
 #ifndef GM_ROUTE_PRIO
 #define GM_ROUTE_PRIO 0  // 1: the route at raised issue priority beside the scan (5.32 vs 5.06 ms per C4 step)
 #endif
-    // GM_EXP_ROUTE_AFTER (measurement build): the route after the scan, beside the context
-    // filter -- the scan alone runs 3.4-3.8 ms instead of 4.8, but the step is longer (6.46 vs
-    // 5.89 ms per 10M C4 requests): the route beside the scan is the shipped schedule
-#ifdef GM_EXP_ROUTE_AFTER
-    constexpr bool route_after = true;
-#else
-    constexpr bool route_after = false;
-#endif
-    if (!serial && !route_after) {
+    if (!serial) {
         HIPCHK(c, hipEventRecord(S->ev_fork, s));
         HIPCHK(c, hipStreamWaitEvent(S->side, S->ev_fork, 0));
     }
     auto launch_route = [&]() -> int {
         // beside the scan, GM_ROUTE_BPC route blocks per CU (more steal issue slots from the scan)
         const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
-                                                                     (uint32_t)c->cu_count * (serial || route_after ? 8 : GM_ROUTE_BPC)));
+                                                                     (uint32_t)c->cu_count * (serial ? 8 : GM_ROUTE_BPC)));
         if (prof) HIPCHK(c, hipEventRecord(S->ev_route[0], rs));
-        // raised issue priority beside the scan: the route's short latency-bound waves finish
-        // early instead of stretching past the scan
         if (rk)
             GM_ROUTE_LAUNCH(GM_ROUTE_WPE, true, false, nb, route_lds(t, !serial), rs, reqs, n, A, alen, t, out, ctr, S->d_blk2rec, nblk, S->d_cnt, GM_ROUTE_PRIO, dlen, route_hist_n(t, !serial), q);
         else {
@@ -2050,123 +2252,236 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         S->route_side = true;
         return GM_OK;
     };
-#ifdef GM_EXP_ROUTE_FIRST   // measurement build: the route beside the scan, enqueued before it (older waves)
-    if (!serial && !route_after && (e = launch_route())) return e;
-#endif
     if (serial && (e = launch_route())) return e;
     if (mark(1)) return GM_E_HIP;
-    const uint32_t bcap = (uint32_t)std::min<size_t>(S->cap_surv / scan_blocks, 0xFFFFFFFFu);   // survivors per workgroup
-    // persistent scan grid: one 1024-thread workgroup per CU (128 KiB LDS prefilter); every wave
-    // owns a contiguous arena range and a private candidate region of wcap records
-    if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
-    else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
-    else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
-    else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(A, alen, t, cand, wcap, S->d_ccnt, dlen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
-    HIPCHK(c, hipGetLastError());
-    if (!serial && route_after) {   // the route beside the context filter, after the scan
-        HIPCHK(c, hipEventRecord(S->ev_fork, s));
-        HIPCHK(c, hipStreamWaitEvent(S->side, S->ev_fork, 0));
-    }
-#ifndef GM_EXP_ROUTE_FIRST
-    if (!serial && (e = launch_route())) return e;
-#else
-    if (!serial && route_after && (e = launch_route())) return e;
-#endif
-    if (mark(2)) return GM_E_HIP;
-    // the continuation of overflowed candidate / survivor regions (a no-op launch otherwise)
-    auto launch_direct = [&](const uint8_t *DA, uint64_t dl, const gm_req *DR, const uint32_t *b2r, const Dedup &d,
-                             const uint64_t *dlp) -> int {
-        uint32_t *res = S->d_ccnt + W + scan_blocks, *cres = S->d_ccnt + 2 * W + scan_blocks;
-#define GM_DIRECT(PKV) k_waf_direct<PKV><<<scan_blocks, SCAN_BLOCK, SCAN_LDS_BYTES, s>>>(DA, dl, DR, n, b2r, t, cand, wcap, \
-            S->d_ccnt, res, cres, S->d_pairs, (uint32_t)S->cap_pairs, S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, d, dlp)
-        if (t.bloom_pk == BLOOM_PK_PERM) GM_DIRECT(BLOOM_PK_PERM);
-        else if (t.bloom_pk == 1) GM_DIRECT(1);
-        else if (t.bloom_pk == 2) GM_DIRECT(2);
-        else GM_DIRECT(3);
-#undef GM_DIRECT
-        HIPCHK(c, hipGetLastError());
-        return GM_OK;
-    };
-    k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, S->d_ccnt, W, t, S->d_surv, bcap, S->d_ccnt + W,
-                                                S->d_status, S->d_ccnt + 2 * W + scan_blocks, GM_SCAN_CTX != 0);
-    HIPCHK(c, hipGetLastError());
-    // join: blk2rec, the verdicts and the zeroed counts are complete before the exact check
-    if (!serial) HIPCHK(c, hipStreamWaitEvent(s, S->ev_join, 0));
-    // persistent exact check: EXACT_BPC workgroups per CU, all resident
-    k_waf_exact<<<exact_blocks, EXACT_BLOCK, 0, s>>>(A, alen, reqs, n, S->d_blk2rec, t, S->d_surv, bcap,
-                                                     S->d_ccnt + W, scan_blocks, S->d_pairs, (uint32_t)S->cap_pairs,
-                                                         S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, dd, dlen, xprof);
-    HIPCHK(c, hipGetLastError());
-    k_exact_prof<<<1, 256, 0, s>>>(xprof, exact_blocks, S->d_status);
-    HIPCHK(c, hipGetLastError());
-    if ((e = launch_direct(A, alen, reqs, S->d_blk2rec, dd, dlen))) return e;
-    if (mark(3)) return GM_E_HIP;
-    if (t.n_sig_regex) {
-        k_waf_regex<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(A, reqs, t, S->d_jobs, (uint32_t)S->cap_jobs, S->d_pairs,
-                                                               (uint32_t)S->cap_pairs, dd);
-        HIPCHK(c, hipGetLastError());
-    }
-    if ((e = launch_always(c, s, g, A, alen, reqs, n, S, dd, false, dlen))) return e;
-    if (t.decoders) {
-        // ---- the request parsers' decoded views (gm_decode.inc): shadow records, same indices,
-        // then the WAF stages once more over them; hits land in the same dedupe set and counts
-        const size_t scap = 2 * (size_t)alen + 32 * (size_t)n + 4096;   // a view <= 2x its zones
-        const uint32_t snblk = (uint32_t)((scap >> BLK_SHIFT) + 1);
-        if ((e = grow(c, s, S->d_sreqs, S->cap_sreqs, (size_t)n))) return e;
-        if ((e = grow(c, s, S->d_sarena, S->cap_sarena, scap))) return e;
-        if ((e = grow(c, s, S->d_sblk, S->cap_sblk, snblk))) return e;
-        if ((e = grow(c, s, S->d_ssize, S->cap_ssize, (size_t)n + 2))) return e;
-        if ((e = grow(c, s, S->d_sbase, S->cap_sbase, (size_t)n + 2))) return e;
-        size_t dtmp = 0;
-        HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, dtmp, S->d_ssize, S->d_sbase, (int)n + 1, s));
-        if ((e = grow(c, s, S->d_stemp, S->cap_stemp, dtmp))) return e;
-        const uint32_t dblocks = (n + 255) / 256;
-        k_dec_size<<<dblocks, 256, 0, s>>>(reqs, A, n, t, out, S->d_ssize);
-        HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_stemp, dtmp, S->d_ssize, S->d_sbase, (int)n + 1, s));
-        uint64_t *slen = S->d_sbase + n + 1;   // the shadow arena's length, on the device
-        k_dec_emit<<<dblocks, 256, 0, s>>>(reqs, A, n, t, out, S->d_sbase, S->d_sreqs, S->d_sarena, scap,
-                                           S->d_sblk, snblk, slen, S->d_status);
-        HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipMemsetAsync(S->d_status + 2, 0, 4, s));   // the job list restarts (pairs continue)
-        k_status_pass<<<1, 64, 0, s>>>(S->d_status);   // the continuations restart too
-        HIPCHK(c, hipGetLastError());
-        Dedup dd2 = dd;
-        dd2.jepoch = S->epoch + 1;
-        const uint8_t *SA = S->d_sarena;
-        const gm_req *SR = S->d_sreqs;
-        if (t.bloom_pk == BLOOM_PK_PERM) k_waf_scan<BLOOM_PK_PERM, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
-        else if (t.bloom_pk == 1) k_waf_scan<1, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
-        else if (t.bloom_pk == 2) k_waf_scan<2, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
-        else k_waf_scan<3, SCAN_DEPTH><<<scan_blocks, SCAN_BLOCK, SCAN_DYN_LDS, s>>>(SA, scap, t, cand, wcap, S->d_ccnt, slen, S->d_ccnt + W + scan_blocks, S->d_surv, bcap, S->d_ccnt + W, S->d_status);
-        HIPCHK(c, hipGetLastError());
-        k_waf_ctx<<<scan_blocks, VER_BLOCK, 0, s>>>(cand, wcap, S->d_ccnt, W, t, S->d_surv, bcap, S->d_ccnt + W,
-                                                    S->d_status, S->d_ccnt + 2 * W + scan_blocks, GM_SCAN_CTX != 0);
-        HIPCHK(c, hipGetLastError());
-        k_waf_exact<<<exact_blocks, EXACT_BLOCK, 0, s>>>(SA, scap, SR, n, S->d_sblk, t, S->d_surv, bcap,
-                                                         S->d_ccnt + W, scan_blocks, S->d_pairs, (uint32_t)S->cap_pairs,
-                                                             S->d_jobs, (uint32_t)S->cap_jobs, S->d_status, dd2, slen, xprof);
-        HIPCHK(c, hipGetLastError());
-        k_exact_prof<<<1, 256, 0, s>>>(xprof, exact_blocks, S->d_status);
-        HIPCHK(c, hipGetLastError());
-        if ((e = launch_direct(SA, scap, SR, S->d_sblk, dd2, slen))) return e;
-        if (t.n_sig_regex) {
-            k_waf_regex<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(SA, SR, t, S->d_jobs, (uint32_t)S->cap_jobs, S->d_pairs,
-                                                                   (uint32_t)S->cap_pairs, dd2);
-            HIPCHK(c, hipGetLastError());
-        }
-        if ((e = launch_always(c, s, g, SA, scap, SR, n, S, dd2, true, slen))) return e;
-    }
+    const WafIO io{A, alen, dlen, reqs, n, out, S->d_blk2rec, nblk};
+    if ((e = waf_stages(c, S, g, k, io, dd, serial ? std::function<int()>() : std::function<int()>(launch_route), !serial,
+                        mark))) return e;
     // ---- hit emission: offsets by an exclusive scan of the per-request counts (request order)
-    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_temp, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
-    k_hits_scatter<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(S->d_pairs, (uint32_t)S->cap_pairs, S->d_cnt, S->d_start,
-                                                              hit_ids, hit_cap, ctr, t.n_locs, S->d_status, dd);
-    HIPCHK(c, hipGetLastError());
-    k_hits_finalize<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8)), 256, 0, s>>>(
-        S->d_start, n, out, hit_ids, hit_cap, S->d_status);
-    HIPCHK(c, hipGetLastError());
+    if ((e = emit_hits(c, S, g, n, out, hit_ids, hit_cap, ctr, dd, nullptr, 0, nullptr))) return e;
     if ((e = commit())) return e;
     if (mark(4)) return GM_E_HIP;
+    return GM_OK;
+}
+
+// A batch's record on its stream until gm_sync completes it: the arguments, for the dedupe set's
+// continuation (the stream's last batch: only the requests with a refused insert are redone) or a
+// whole re-run (an earlier batch of the stream, whose scratch later batches have reused)
+static int enqueue_batch(gm_ctx *c, Scratch *S, const Generation *g, const Scratch::Replay &rp) {
+    return run_batch(c, S, g, rp.reqs, rp.A, rp.alen, rp.n, rp.out, rp.hits, rp.hit_cap, rp.dlen, rp.slot);
+}
+
+// GM_TRACE_SYNC=1 (environment): gm_sync's phases with host timestamps on stderr (diagnostics)
+static bool trace_sync() {
+    static const bool on = getenv("GM_TRACE_SYNC") != nullptr;
+    return on;
+}
+static void trace(const char *what) {
+    if (!trace_sync()) return;
+    static auto t0 = std::chrono::steady_clock::now();
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    fprintf(stderr, "[gm_sync %10.3f ms] %s\n", ms, what);
+}
+
+// GM_BATCH_HOST: the staged verdicts and hits back to the caller's host buffers
+static int copy_back(gm_ctx *c, Scratch *S, const Scratch::Replay &rp) {
+    if (!rp.h_out) return GM_OK;
+    HIPCHK(c, hipMemcpyAsync(rp.h_out, rp.out, (size_t)rp.n * sizeof(gm_verdict), hipMemcpyDeviceToHost, S->stream));
+    if (rp.h_hits && rp.h_hit_cap)
+        HIPCHK(c, hipMemcpyAsync(rp.h_hits, rp.hits, rp.h_hit_cap * 4, hipMemcpyDeviceToHost, S->stream));
+    return GM_OK;
+}
+
+// read the stream's status words (and the pending batches' overflow words) to the host
+static int read_status(gm_ctx *c, Scratch *S) {
+    HIPCHK(c, hipMemcpyAsync(S->h_status, S->d_status, STATUS_WORDS * 4, hipMemcpyDeviceToHost, S->stream));
+    HIPCHK(c, hipMemcpyAsync(S->h_ovlog, S->d_ovlog, PENDING_MAX * 4, hipMemcpyDeviceToHost, S->stream));
+    HIPCHK(c, hipStreamSynchronize(S->stream));
+    return GM_OK;
+}
+
+// a batch whose dedupe set overflowed, re-run whole with the set doubled until it fits (a stream's
+// earlier batch, or the rare case a continuation cannot take): ov = its final overflow bits
+static int rerun_whole(gm_ctx *c, Scratch *S, const Scratch::Replay &rp0, uint32_t &ov) {
+    Scratch::Replay rp = rp0;
+    rp.slot = 0;
+    for (;;) {
+        if (S->list_mult >= 64) return GM_OK;   // at its largest: ov keeps OV_SET, reported by the caller
+        S->list_mult *= 2;
+        std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+        if (c->gen != rp.gen || c->publish_seq != rp.seq)
+            return fail(c, GM_E_OVERFLOW, "WAF dedupe set full and the generation changed before the batch could be "
+                                          "re-run: retry it");
+        c->n_set_reruns++;
+        DoneGuard G(S);
+        int e = enqueue_batch(c, S, c->gen, rp);
+        if (e || (e = copy_back(c, S, rp)) || (e = G.done(c))) return e;
+        lk.unlock();
+        if ((e = read_status(c, S))) return e;
+        ov = S->h_ovlog[0];
+        if (!(ov & OV_SET)) return GM_OK;
+    }
+}
+
+// The dedupe set of the stream's last batch overflowed (OV_SET): only the requests with a refused
+// insert are redone (k_redo_*), as a sub-batch of their WAF zones through the same stages with a
+// set twice as large (doubled again while it overflows), and the emission merges both passes.
+// The first pass left its pairs in [0, np1), its counts, the route's verdicts and location counters
+// (k_hits_scatter / k_hits_finalize / k_ctr_commit held back on OV_SET).  done = false: the
+// continuation does not apply (the caller re-runs the batch whole).
+static int set_continuation(gm_ctx *c, Scratch *S, const Scratch::Replay &rp, uint32_t ov1, uint32_t &ov, bool &done) {
+    done = false;
+    hipStream_t s = S->stream;
+    if (ov1 & (OV_PAIRS | OV_HITS | OV_DEC)) return GM_OK;   // the first pass's lists are incomplete / void
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    if (c->gen != rp.gen || c->publish_seq != rp.seq)
+        return fail(c, GM_E_OVERFLOW, "WAF dedupe set full and the generation changed before the batch could be "
+                                      "completed: retry it");
+    const Generation *g = c->gen;
+    const GTab &t = g->tab;
+    const uint32_t n = rp.n;
+    const uint32_t np1 = S->h_status[1];
+    int e;
+    DoneGuard G(S);
+    // the requests to redo
+    if ((e = grow(c, s, S->d_rlist, S->cap_rlist, (size_t)n))) return e;
+    HIPCHK(c, hipMemsetAsync(S->d_status + REDO_STATUS_WORD, 0, 4, s));
+    k_redo_list<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(S->d_redo, n, S->d_rlist, S->d_cnt, S->d_status + REDO_STATUS_WORD);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(S->h_status + REDO_STATUS_WORD, S->d_status + REDO_STATUS_WORD, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const uint32_t m = S->h_status[REDO_STATUS_WORD];
+    trace("continuation: requests listed");
+    if (m == 0 || m > n) { G.armed = false; return mark_done(c, S); }
+    c->last_redo = m;
+    // their zones gathered into a sub-batch
+    if ((e = grow(c, s, S->d_rsize, S->cap_rsize, (size_t)m + 1)) || (e = grow(c, s, S->d_rbase, S->cap_rbase, (size_t)m + 1)))
+        return e;
+    size_t tmp = 0;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, S->d_rsize, S->d_rbase, (int)m + 1, s));
+    if ((e = grow(c, s, S->d_rtemp, S->cap_rtemp, tmp))) return e;
+    k_redo_size<<<(m + 255) / 256, 256, 0, s>>>(rp.reqs, S->d_rlist, m, S->d_rsize);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_rtemp, tmp, S->d_rsize, S->d_rbase, (int)m + 1, s));
+    uint64_t sub_len = 0;
+    HIPCHK(c, hipMemcpyAsync(&sub_len, S->d_rbase + m, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    trace("continuation: sub-batch sized");
+    const uint32_t snblk = (uint32_t)((sub_len >> BLK_SHIFT) + 1);
+    if ((e = grow(c, s, S->d_rsreq, S->cap_rsreq, (size_t)m)) || (e = grow(c, s, S->d_rsarena, S->cap_rsarena, sub_len + 1024)) ||
+        (e = grow(c, s, S->d_rsout, S->cap_rsout, (size_t)m)) || (e = grow(c, s, S->d_rsblk, S->cap_rsblk, snblk)) ||
+        (e = grow(c, s, S->d_rscnt, S->cap_rscnt, (size_t)m + 1)))
+        return e;
+    HIPCHK(c, hipMemsetAsync(S->d_rsarena + sub_len, 0, 1024, s));
+    k_redo_emit<<<(m + 255) / 256, 256, 0, s>>>(rp.reqs, rp.A, rp.out, S->d_rlist, m, S->d_rbase, sub_len, S->d_rsreq,
+                                                S->d_rsarena, S->d_rsout, S->d_rsblk, snblk);
+    HIPCHK(c, hipGetLastError());
+    const WafIO io{S->d_rsarena, sub_len, nullptr, S->d_rsreq, m, S->d_rsout, S->d_rsblk, snblk};
+    const std::function<int(int)> nomark = [](int) { return GM_OK; };
+    for (;;) {
+        // a set twice the size that overflowed, fresh; the sub-batch's pairs follow the first pass's
+        if (S->list_mult >= 64) { ov = OV_SET; G.armed = false; return mark_done(c, S); }
+        S->list_mult *= 2;
+        if ((e = grow(c, s, S->d_set, S->cap_set, 2 * S->cap_set))) return e;
+        S->cap_set = (size_t)1 << (63 - __builtin_clzll(S->cap_set));   // (grow pads; the mask needs a power of two)
+        S->epoch = 0;
+        HIPCHK(c, hipMemsetAsync(S->d_set, 0, S->cap_set * 8, s));
+        WafCaps k{};
+        if ((e = waf_buffers(c, S, sub_len, m, k, np1))) return e;
+        if ((e = next_epoch(c, S, t))) return e;
+        k_redo_status<<<1, 64, 0, s>>>(S->d_status, np1);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemsetAsync(S->d_rscnt, 0, ((size_t)m + 1) * 4, s));
+        c->n_set_reruns++;
+        const Dedup dd{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, S->d_rsout, S->d_rscnt, S->d_status, nullptr};
+        trace("continuation: sub-batch enqueued");
+        if ((e = waf_stages(c, S, g, k, io, dd, std::function<int()>(), false, nomark))) return e;
+        if ((e = read_status(c, S))) return e;
+        trace("continuation: sub-batch done");
+        const uint32_t ov2 = S->h_status[3];
+        if (ov2 & (OV_PAIRS | OV_DEC)) { G.armed = false; return mark_done(c, S); }   // whole re-run instead
+        if (!(ov2 & OV_SET)) break;
+    }
+    // merge: the sub-requests' counts, then the emission over the whole batch and the commit
+    k_redo_merge<<<(m + 255) / 256, 256, 0, s>>>(S->d_rlist, m, S->d_rscnt, S->d_cnt);
+    HIPCHK(c, hipGetLastError());
+    const Dedup dd0{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, rp.out, S->d_cnt, S->d_status, nullptr};
+    if ((e = emit_hits(c, S, g, n, rp.out, rp.hits, rp.hit_cap, S->d_bctr, dd0, S->d_redo, np1, S->d_rlist))) return e;
+    const size_t nctr = std::max<size_t>(g->n_counters, 1);
+    k_ctr_commit<<<std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)((nctr + 255) / 256), (uint32_t)c->cu_count)), 256, 0, s>>>(
+        S->d_bctr, g->d_counters, (uint32_t)g->n_counters, S->d_status, S->d_ovlog + rp.slot);
+    HIPCHK(c, hipGetLastError());
+    if ((e = copy_back(c, S, rp))) return e;
+    if ((e = G.done(c))) return e;
+    lk.unlock();
+    if ((e = read_status(c, S))) return e;
+    trace("continuation: emitted");
+    ov = S->h_ovlog[rp.slot];
+    done = true;
+    return GM_OK;
+}
+
+// Complete the stream's pending batches (gm_sync): overflow bits per batch, OV_SET batches
+// completed (the last by the continuation, earlier ones re-run whole), errors reported.
+static int sync_pending(gm_ctx *c, Scratch *S) {
+    int e;
+    trace("sync: start");
+    if ((e = read_status(c, S))) return e;
+    trace("sync: pending batches done");
+    {
+        std::lock_guard<std::mutex> lk(c->last_mu);
+        memcpy(c->last_status, S->h_status, STATUS_WORDS * 4);
+        c->last_candidates = S->h_status[6];
+        c->last_ctx_pass = S->h_status[7];
+        c->last_jobs = S->h_status[2];
+        c->last_pairs = S->h_status[1];
+        c->last_hits = S->h_status[4];
+        if (S->ev_pending) {
+            for (int k = 0; k < 4; k++) {
+                c->last_ms[k] = 0;
+                if (k + 1 < S->ev_used) (void)hipEventElapsedTime(&c->last_ms[k], S->ev[k], S->ev[k + 1]);
+            }
+            // stage 0 = the route on the side stream (its own time); stage 1 = the scan
+            if (S->route_side) (void)hipEventElapsedTime(&c->last_ms[0], S->ev_route[0], S->ev_route[1]);
+            S->ev_pending = false;
+        }
+    }
+    const uint32_t parse_ov = S->h_status[PARSE_STATUS_WORD + 3], upuri_ov = S->h_status[UPURI_STATUS_WORD];
+    std::vector<Scratch::Replay> pend;
+    pend.swap(S->pending);
+    const bool last_in_place = S->last_is_batch;
+    S->last_is_batch = false;
+    uint32_t any = 0;
+    for (const auto &rp : pend) any |= S->h_ovlog[rp.slot];
+    // the next batch on this stream gets twice the buffer that overflowed (bounded)
+    if ((any & OV_CAND) && S->cand_mult < 64) S->cand_mult *= 2;
+    if ((any & OV_SURV) && S->surv_mult < 64) S->surv_mult *= 2;
+    if ((any & (OV_PAIRS | OV_JOBS)) && S->list_mult < 64) S->list_mult *= 2;
+    std::vector<uint32_t> ovs(pend.size());
+    for (size_t i = 0; i < pend.size(); i++) ovs[i] = S->h_ovlog[pend[i].slot];
+    uint32_t err = 0;
+    // the last batch first: its scratch (pairs, counts, redo bits) is still in place
+    for (size_t i = pend.size(); i-- > 0;) {
+        uint32_t ov = ovs[i];
+        if (ov & OV_SET) {
+            bool done = false;
+            if (i + 1 == pend.size() && last_in_place && (e = set_continuation(c, S, pend[i], ov, ov, done))) return e;
+            if (!done && (e = rerun_whole(c, S, pend[i], ov))) return e;
+            if (i + 1 == pend.size()) {
+                std::lock_guard<std::mutex> lk(c->last_mu);
+                c->last_hits = S->h_status[4];
+            }
+        }
+        err |= ov;
+    }
+    if (parse_ov) return fail(c, GM_E_OVERFLOW, "gm_parse_requests: arena capacity exceeded");
+    if (upuri_ov) return fail(c, GM_E_OVERFLOW, "gm_upstream_uris: output capacity exceeded");
+    if (err & OV_HITS) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded (the batch's counters were not committed)");
+    // candidate / survivor / pair / job overflows were completed on the device (k_waf_direct, the
+    // set-based scatter and regex runs): the batch is whole, the buffers grow for speed
+    if (err & OV_SET) return fail(c, GM_E_OVERFLOW, "WAF dedupe set full at its largest size (64x: > ~380 unique hits + "
+                                                    "regex jobs per request); the batch's counters were not committed");
+    if (err & OV_DEC) return fail(c, GM_E_OVERFLOW, "decoded-view arena capacity exceeded");
     return GM_OK;
 }
 
@@ -2177,28 +2492,40 @@ int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit
     hipStream_t s = (hipStream_t)stream;
     Scratch *S = scratch_for(c, s);
     if (!S) return fail(c, GM_E_NOMEM, t_err);
+    // the stream's pending batches are recorded until gm_sync; past PENDING_MAX unsynced batches the
+    // oldest are completed here first (synchronously), so no batch's overflow goes unreported
+    if (S->pending.size() >= PENDING_MAX) {
+        const int e0 = sync_pending(c, S);
+        if (e0) return e0;
+    }
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
     const Generation *g = c->gen;
     if (!g) return fail(c, GM_E_NOGEN, "no generation loaded");
-    S->replay.valid = false;
+    S->last_is_batch = false;
     if (in->n == 0) { HIPCHK(c, hipMemsetAsync(S->d_status, 0, BATCH_STATUS_WORDS * 4, s)); S->ev_pending = false; return GM_OK; }
     if (((uintptr_t)in->arena & 15) || ((uintptr_t)in->reqs & 15) || ((uintptr_t)out & 15))
         return fail(c, GM_E_INVAL, "reqs / arena / out must be 16-byte aligned");
     if (hit_cap > 0xFFFFFFFFull) hit_cap = 0xFFFFFFFFull;   // hit offsets are u32
     DoneGuard G(S);
-    Scratch::Replay &rp = S->replay;
+    Scratch::Replay rp;
     rp.gen = g; rp.seq = c->publish_seq; rp.n = in->n; rp.alen = in->arena_len;
-    rp.h_out = nullptr; rp.h_hits = nullptr; rp.h_hit_cap = 0;
+    rp.slot = (uint32_t)S->pending.size();
     if (!(in->flags & GM_BATCH_HOST)) {
-        const int e = run_batch(c, S, g, in->reqs, in->arena, in->arena_len, in->n, out, hit_ids, hit_ids ? hit_cap : 0,
-                                in->arena_len_dev);
-        if (e) return e;
         rp.reqs = in->reqs; rp.A = in->arena; rp.out = out; rp.hits = hit_ids; rp.hit_cap = hit_ids ? hit_cap : 0;
         rp.dlen = in->arena_len_dev;
-        rp.valid = true;
+        const int e = enqueue_batch(c, S, g, rp);
+        if (e) return e;
+        S->pending.push_back(rp);
+        S->last_is_batch = true;
         return G.done(c);
     }
-    // host buffers: stage reqs + arena + verdicts + hits through HBM (PCIe both ways)
+    // host buffers: stage reqs + arena + verdicts + hits through HBM (PCIe both ways); a stream
+    // holds one staged batch at a time (the staging buffer is reused), so earlier ones complete first
+    if (!S->pending.empty()) {
+        const int e0 = sync_pending(c, S);
+        if (e0) return e0;
+        rp.slot = 0;
+    }
     size_t rq = (size_t)in->n * sizeof(gm_req), ar = (in->arena_len + 255) & ~255ull;
     size_t vo = (size_t)in->n * sizeof(gm_verdict), ho = hit_cap * 4;
     size_t tot = rq + ar + vo + ho + 1024;
@@ -2209,16 +2536,16 @@ int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit
     uint8_t *da = p; p += ar;
     gm_verdict *dv = (gm_verdict *)p; p += (vo + 255) & ~255ull;
     uint32_t *dh = (uint32_t *)p;
+    if (in->arena_len_dev) return fail(c, GM_E_INVAL, "arena_len_dev with GM_BATCH_HOST");
     HIPCHK(c, hipMemcpyAsync(dr, in->reqs, rq, hipMemcpyHostToDevice, s));
     if (in->arena_len) HIPCHK(c, hipMemcpyAsync(da, in->arena, in->arena_len, hipMemcpyHostToDevice, s));
-    if (in->arena_len_dev) return fail(c, GM_E_INVAL, "arena_len_dev with GM_BATCH_HOST");
-    e = run_batch(c, S, g, dr, da, in->arena_len, in->n, dv, dh, hit_ids ? hit_cap : 0, nullptr);
-    if (e) return e;
-    HIPCHK(c, hipMemcpyAsync(out, dv, vo, hipMemcpyDeviceToHost, s));
-    if (hit_ids && hit_cap) HIPCHK(c, hipMemcpyAsync(hit_ids, dh, ho, hipMemcpyDeviceToHost, s));
     rp.reqs = dr; rp.A = da; rp.out = dv; rp.hits = dh; rp.hit_cap = hit_ids ? hit_cap : 0; rp.dlen = nullptr;
     rp.h_out = out; rp.h_hits = hit_ids; rp.h_hit_cap = hit_ids ? hit_cap : 0;
-    rp.valid = true;
+    e = enqueue_batch(c, S, g, rp);
+    if (e) return e;
+    if ((e = copy_back(c, S, rp))) return e;
+    S->pending.push_back(rp);
+    S->last_is_batch = true;
     return G.done(c);
 }
 
@@ -2229,66 +2556,7 @@ int gm_sync(gm_ctx *c, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     Scratch *S = scratch_for(c, s);
     if (!S) return fail(c, GM_E_NOMEM, t_err);
-    uint32_t ov;
-    for (;;) {
-        HIPCHK(c, hipMemcpyAsync(S->h_status, S->d_status, STATUS_WORDS * 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipStreamSynchronize(s));
-        {
-            std::lock_guard<std::mutex> lk(c->last_mu);
-            memcpy(c->last_status, S->h_status, STATUS_WORDS * 4);
-            c->last_candidates = S->h_status[6];
-            c->last_ctx_pass = S->h_status[7];
-            c->last_jobs = S->h_status[2];
-            c->last_pairs = S->h_status[1];
-            c->last_hits = S->h_status[4];
-            if (S->ev_pending) {
-                for (int k = 0; k < 4; k++) {
-                    c->last_ms[k] = 0;
-                    if (k + 1 < S->ev_used) (void)hipEventElapsedTime(&c->last_ms[k], S->ev[k], S->ev[k + 1]);
-                }
-                // stage 0 = the route on the side stream (its own time); stage 1 = the scan
-                if (S->route_side) (void)hipEventElapsedTime(&c->last_ms[0], S->ev_route[0], S->ev_route[1]);
-                S->ev_pending = false;
-            }
-        }
-        ov = S->h_status[3];
-        // the next batch on this stream gets twice the buffer that overflowed (bounded)
-        if ((ov & OV_CAND) && S->cand_mult < 64) S->cand_mult *= 2;
-        if ((ov & OV_SURV) && S->surv_mult < 64) S->surv_mult *= 2;
-        const uint32_t list_before = S->list_mult;
-        if ((ov & (OV_PAIRS | OV_JOBS | OV_SET)) && S->list_mult < 64) S->list_mult *= 2;
-        // the dedupe set overflowed (more unique hits + regex jobs than its sizing, e.g. an attack
-        // burst): the batch is re-run here with the set doubled -- its counters were not committed
-        // (k_ctr_commit) -- until it fits, so the caller sees a whole batch
-        Scratch::Replay &rp = S->replay;
-        if (!(ov & OV_SET) || !rp.valid || S->list_mult == list_before) break;
-        std::shared_lock<std::shared_mutex> lk(c->gen_mu);
-        if (c->gen != rp.gen || c->publish_seq != rp.seq) {
-            rp.valid = false;
-            return fail(c, GM_E_OVERFLOW, "WAF dedupe set full and the generation changed before the batch could be "
-                                          "re-run: retry it");
-        }
-        c->n_set_reruns++;
-        DoneGuard G(S);
-        int e = run_batch(c, S, c->gen, rp.reqs, rp.A, rp.alen, rp.n, rp.out, rp.hits, rp.hit_cap, rp.dlen);
-        if (e) { rp.valid = false; return e; }
-        if (rp.h_out) {
-            HIPCHK(c, hipMemcpyAsync(rp.h_out, rp.out, (size_t)rp.n * sizeof(gm_verdict), hipMemcpyDeviceToHost, s));
-            if (rp.h_hits && rp.h_hit_cap)
-                HIPCHK(c, hipMemcpyAsync(rp.h_hits, rp.hits, rp.h_hit_cap * 4, hipMemcpyDeviceToHost, s));
-        }
-        if ((e = G.done(c))) { rp.valid = false; return e; }
-    }
-    S->replay.valid = false;
-    if (S->h_status[PARSE_STATUS_WORD + 3]) return fail(c, GM_E_OVERFLOW, "gm_parse_requests: arena capacity exceeded");
-    if (S->h_status[UPURI_STATUS_WORD]) return fail(c, GM_E_OVERFLOW, "gm_upstream_uris: output capacity exceeded");
-    if (ov & OV_HITS) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded (the batch's counters were not committed)");
-    // candidate / survivor / pair / job overflows were completed on the device (k_waf_direct, the
-    // set-based scatter and regex runs): the batch is whole, the buffers grow for speed
-    if (ov & OV_SET) return fail(c, GM_E_OVERFLOW, "WAF dedupe set full at its largest size (64x: > ~380 unique hits + "
-                                                   "regex jobs per request); the batch's counters were not committed");
-    if (ov & OV_DEC) return fail(c, GM_E_OVERFLOW, "decoded-view arena capacity exceeded");
-    return GM_OK;
+    return sync_pending(c, S);
 }
 
 int gm_counters(gm_ctx *c, uint64_t *out, size_t n) {
@@ -2689,6 +2957,8 @@ extern "C" int gm_normalize_uris(gm_ctx *c, const uint8_t *arena, const uint64_t
     // after it reports OK (no stale match-batch overflow)
     Scratch *S = scratch_for(c, (hipStream_t)stream);
     if (!S) return fail(c, GM_E_NOMEM, t_err);
+    S->last_is_batch = false;   // (the batch status words are cleared: a pending batch's continuation
+                                //  becomes a whole re-run)
     HIPCHK(c, hipMemsetAsync(S->d_status, 0, STATUS_WORDS * 4, (hipStream_t)stream));
     S->ev_pending = false;
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 16));
@@ -2723,6 +2993,26 @@ extern "C" int gm_parse_requests(gm_ctx *c, const uint8_t *wire, const gm_wire_m
     if ((e = grow(c, s, S->d_wscr, S->cap_wscr, (size_t)blocks * WIRE_WAVES * WIRE_SCR))) return e;
     if ((e = grow(c, s, S->d_wsum, S->cap_wsum, (size_t)n * sizeof(WireSum)))) return e;
     WireSum *wsum = reinterpret_cast<WireSum *>(S->d_wsum);
+    // PROXY protocol: on a generation with a `listen ... proxy_protocol` port the descriptors go
+    // through k_wire_proxy first (their headers read, the messages advanced past them); the parse
+    // passes read the copies.  The generation's port table decides (shared lock: the copy of the
+    // flags is taken before the launch, the kernel reads the image the lock keeps alive until the
+    // stream's completion event)
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    DoneGuard G(S);
+    const Generation *g = c->gen;
+    bool proxy = false;
+    if (g) {
+        const DPort *ports = reinterpret_cast<const DPort *>(g->host_image.data() + g->hdr.off_ports);
+        for (uint32_t k = 0; k < g->hdr.n_ports; k++) proxy |= ports[k].proxy != 0;
+    }
+    if (proxy) {
+        if ((e = grow(c, s, S->d_wmsg, S->cap_wmsg, (size_t)n))) return e;
+        k_wire_proxy<<<std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8), 256, 0, s>>>(wire, msgs, n, g->tab,
+                                                                                                   S->d_wmsg);
+        HIPCHK(c, hipGetLastError());
+        msgs = S->d_wmsg;
+    }
     k_wire_size<<<blocks, 64 * WIRE_WAVES, 0, s>>>(wire, msgs, n, S->d_wsize, S->d_wscr, wsum);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_wtemp, tmp, S->d_wsize, S->d_wbase, (int)n + 1, s));
@@ -2733,7 +3023,7 @@ extern "C" int gm_parse_requests(gm_ctx *c, const uint8_t *wire, const gm_wire_m
     k_wire_emit_full<<<blocks, 64 * WIRE_WAVES, 0, s>>>(wire, msgs, n, S->d_wsize, S->d_wbase, reqs, arena, arena_cap,
                                                         S->d_wscr, wsum);
     HIPCHK(c, hipGetLastError());
-    return GM_OK;
+    return G.done(c);
 }
 
 // The last gm_parse_requests' per-request slot sizes on `stream` (size pass), for debugging.
@@ -2934,7 +3224,7 @@ static constexpr uint32_t kBuildFlags =
     defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_SCAN_NOBRANCH) || defined(GM_SCAN_VMASK)
     GM_BUILD_EXPERIMENT |
 #endif
-#if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != (GM_SCAN_CTX ? 63 : 32) || GM_SCAN_CTX != 0 || GM_CTX_FLUSH != 32 || \
+#if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != 32 || \
     GM_ROUTE_BPC != 1 || GM_ROUTE_PRIO != 0 || GM_ROUTE_WPE != GM_ROUTE_WPE_SHIPPED || GM_EXP_GRIDMUL != 8 || \
     GM_EXP_WPE != 3 || GM_RLOC_CTX != 1 || GM_RLOC_PREF != 0 || GM_ALW_SLICE_GROUPS != 8 || GM_WIRE_WPE != 8 || \
     GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1 || GM_EXACT_BPC != 6 || !defined(GM_DFA_INL_SHIPPED)

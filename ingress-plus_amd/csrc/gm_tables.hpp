@@ -24,7 +24,7 @@ struct DPort {               // one entry per distinct listen port
     uint32_t port;
     uint32_t ssl;            // any `listen <port> ssl`
     uint32_t default_server; // `default_server` or first server listening on the port
-    uint32_t pad;
+    uint32_t proxy;          // any `listen <port> ... proxy_protocol` (nginx ORs the option per port)
 };
 
 // open-addressing hash: exact names and wildcard keys, keyed by (port index, lowercase name)
@@ -61,7 +61,7 @@ constexpr uint32_t BODY_UNLIMITED = 0xFFFFFFFFu;
 // ngx_http_realip_module (set_real_ip_from / real_ip_header / real_ip_recursive,
 // version1/nginx.ingress.tmpl:46-49, version2/nginx.virtualserver.tmpl:64-72, ConfigMap keys
 // configmaps.go:153-169): the header the client address is taken from, and the trusted proxies
-// RIP_PROXY: real_ip_header proxy_protocol (the PROXY header's address is not in a record);
+// RIP_PROXY: real_ip_header proxy_protocol (the record's paddr, from the PROXY header);
 // RIP_UNKNOWN: a set_real_ip_from value that is not an address (nginx resolves host names)
 enum : uint32_t { RIP_XREALIP = 1, RIP_XFWD = 2, RIP_PROXY = 3, RIP_HEADER = 4, RIP_UNKNOWN = 5 };
 struct DRealIp {
@@ -261,7 +261,7 @@ struct DUpstream {
     uint32_t method;         // UM_*
     uint32_t first_part, n_parts;    // hash key: DKeyPart list (literal text and variables)
     uint32_t first_point, n_points;  // UM_CHASH: sorted, de-duplicated DPoint ring
-    uint32_t pad;
+    uint32_t sticky;         // NGINX Plus `sticky cookie <name>`: 1 + the DSrc index of $cookie_<name>; 0 none
 };
 constexpr uint32_t KEY_PART_VAR = 0xFFFFFFFFu;
 struct DKeyPart { uint32_t off; uint32_t len; };   // len KEY_PART_VAR: off = DSrc index
@@ -360,6 +360,7 @@ struct TabHeader {
     uint64_t off_hot_end;          // [off_ports, off_hot_end): the route's hot tables, contiguous
     uint32_t n_ups, n_peers, n_key_parts, n_points;
     uint64_t off_ups, off_key_parts, off_points, off_peer_init;   // peer_init: u32 GM_PEER_DOWN per peer
+    uint64_t off_peer_md5;   // 16-byte MD5 of each peer's address text ("ip:port"): NGINX Plus sticky cookie
     uint64_t off_loc_uri;          // DLocUri per location
     uint32_t decoders, pad_dec;    // the signature set's request parsers (DEC_*)
     uint32_t n_always_lds;         // always[0, n_always_lds) are in union-DFA groups
@@ -395,6 +396,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const uint8_t *name_bytes;
     const uint8_t *hot_base; uint32_t hot_len;   // the hot prefix (hot_len 0: larger than ROUTE_STAGE_BYTES)
     const DUpstream *ups; const DKeyPart *key_parts; const DPoint *points; const uint32_t *peer_init;
+    const uint32_t *peer_md5;   // 4 words per peer (off_peer_md5)
     uint32_t n_ups, n_peers, n_servers;
     const DLocUri *loc_uri;
     uint32_t decoders;

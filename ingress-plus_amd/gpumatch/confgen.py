@@ -225,12 +225,39 @@ def path_or_default(path) -> str:
     return path if path else "/"
 
 
-def _create_upstream(ing_ex, name, backend, p):
-    """ingress.go:266-305 (OSS branch): default server 127.0.0.1:8181 when no endpoints
-    (version1/config.go:194-206)."""
+def parse_sticky_service(service: str):
+    """annotations.go:511-524 parseStickyService: "serviceName=<svc> <cookie spec>" ->
+    (service, cookie spec); ValueError for a bad declaration."""
+    parts = service.split(" ", 1)
+    if len(parts) != 2:
+        raise ValueError(f"Invalid sticky-cookie service format: {service}")
+    name_parts = parts[0].split("=")
+    if len(name_parts) != 2:
+        raise ValueError(f"Invalid sticky-cookie service format: {name_parts}")
+    return name_parts[1], parts[1]
+
+
+def get_session_persistence_services(ing: dict) -> dict:
+    """annotations.go:387-399: nginx.com/sticky-cookie-services split on ";" (a bad entry is logged
+    and ignored)."""
+    out = {}
+    v = ((ing.get("metadata") or {}).get("annotations") or {}).get("nginx.com/sticky-cookie-services")
+    if v is not None:
+        for svc in str(v).split(";"):
+            try:
+                name, sticky = parse_sticky_service(svc)
+            except ValueError:
+                continue
+            out[name] = sticky
+    return out
+
+
+def _create_upstream(ing_ex, name, backend, p, sticky=""):
+    """ingress.go:266-305: default server 127.0.0.1:8181 when no endpoints (version1/config.go:
+    194-206); under NGINX Plus the service's sticky cookie (ingress.go:272)."""
     ups = {"Name": name, "UpstreamServers": [{"Address": "127.0.0.1", "Port": "8181",
                                               "MaxFails": 1, "FailTimeout": "10s"}],
-           "LBMethod": p["LBMethod"]}
+           "LBMethod": p["LBMethod"], "StickyCookie": sticky}
     key = backend["serviceName"] + _svc_port(backend)
     endps = (ing_ex.get("Endpoints") or {}).get(key)
     if endps:
@@ -278,17 +305,19 @@ def _create_location(path, upstream, p, rewrite=""):
             "LocationSnippets": list(p["LocationSnippets"])}
 
 
-def generate_nginx_cfg(ing_ex: dict, pems: dict, is_minion: bool, base: dict) -> dict:
-    """ingress.go:47-231 generateNginxCfg (OSS, no JWT/health-check/grpc paths)."""
+def generate_nginx_cfg(ing_ex: dict, pems: dict, is_minion: bool, base: dict, is_plus: bool = False) -> dict:
+    """ingress.go:47-231 generateNginxCfg (no JWT/health-check/grpc paths; is_plus: the session
+    persistence services, ingress.go:50)."""
     ing = ing_ex["Ingress"]
     p = parse_annotations(ing, base)
+    sp = get_session_persistence_services(ing) if is_plus else {}
     rewrites = get_rewrites(ing)   # ingress.go:51
     spec = ing.get("spec") or {}
     upstreams = {}
     default_backend = spec.get("backend")
     if default_backend is not None:
         name = get_name_for_upstream(ing, "", default_backend)
-        upstreams[name] = _create_upstream(ing_ex, name, default_backend, p)
+        upstreams[name] = _create_upstream(ing_ex, name, default_backend, p, sp.get(default_backend["serviceName"], ""))
     servers = []
     for rule in spec.get("rules") or []:
         if not rule.get("http"):
@@ -316,7 +345,7 @@ def generate_nginx_cfg(ing_ex: dict, pems: dict, is_minion: bool, base: dict) ->
             be = path["backend"]
             ups_name = get_name_for_upstream(ing, host, be)
             if ups_name not in upstreams:
-                upstreams[ups_name] = _create_upstream(ing_ex, ups_name, be, p)
+                upstreams[ups_name] = _create_upstream(ing_ex, ups_name, be, p, sp.get(be["serviceName"], ""))
             loc = _create_location(path_or_default(path.get("path", "")), upstreams[ups_name], p,
                                    rewrites.get(be["serviceName"], ""))
             locations.append(loc)
@@ -894,6 +923,8 @@ def render_ingress(cfg: dict) -> str:
             L.append(f"\t{u['LBMethod']};")
         for s in u["UpstreamServers"]:
             L.append(f"\tserver {s['Address']}:{s['Port']} max_fails={s['MaxFails']} fail_timeout={s['FailTimeout']};")
+        if u.get("StickyCookie"):   # nginx-plus.ingress.tmpl:9-11
+            L.append(f"\tsticky cookie {u['StickyCookie']};")
         if cfg.get("Keepalive"):
             L.append(f"\tkeepalive {cfg['Keepalive']};")
         L.append("}")
@@ -1021,6 +1052,32 @@ def render_virtual_server(cfg: dict) -> str:
     return "\n".join(L) + "\n"
 
 
+def _go_parse_bool(x: str):
+    """strconv.ParseBool: 1 t T TRUE true True / 0 f F FALSE false False; None otherwise."""
+    if x in ("1", "t", "T", "TRUE", "true", "True"):
+        return True
+    if x in ("0", "f", "F", "FALSE", "false", "False"):
+        return False
+    return None
+
+
+def configmap_params(data: dict, params: dict | None = None) -> dict:
+    """ParseConfigMap for the PROXY protocol and realip keys (configmaps.go:145-169): proxy-protocol
+    and real-ip-recursive through GetMapKeyAsBool (an invalid bool is logged and ignored),
+    real-ip-header verbatim, set-real-ip-from split on "," (GetMapKeyAsStringSlice, no trimming)."""
+    p = dict(params or default_config_params())
+    for key, field in (("proxy-protocol", "ProxyProtocol"), ("real-ip-recursive", "RealIPRecursive")):
+        if key in data:
+            b = _go_parse_bool(data[key])
+            if b is not None:
+                p[field] = b
+    if "real-ip-header" in data:
+        p["RealIPHeader"] = data["real-ip-header"]
+    if "set-real-ip-from" in data:
+        p["SetRealIPFrom"] = data["set-real-ip-from"].split(",")
+    return p
+
+
 def render_main(params: dict | None = None, wallarm_global_mode: str | None = None) -> str:
     """The http{} part of version1/nginx.tmpl that affects request classification:
     the default server (:81-102) and the conf.d include point (:128-129)."""
@@ -1032,8 +1089,9 @@ def render_main(params: dict | None = None, wallarm_global_mode: str | None = No
     if wallarm_global_mode:
         L.append(f"    wallarm_mode {wallarm_global_mode};")
     L += ["    map $http_upgrade $connection_upgrade {", "        default upgrade;", "        ''      close;", "    }",
-          "    server {", "        listen 80 default_server;",
-          f"        listen 443 ssl default_server{' http2' if p.get('HTTP2') else ''};",
+          "    server {", f"        listen 80 default_server{' proxy_protocol' if p.get('ProxyProtocol') else ''};",
+          f"        listen 443 ssl default_server{' http2' if p.get('HTTP2') else ''}"
+          f"{' proxy_protocol' if p.get('ProxyProtocol') else ''};",
           "        ssl_certificate /etc/nginx/secrets/default;", "        ssl_certificate_key /etc/nginx/secrets/default;",
           "        server_name _;", f'        server_tokens "{p.get("ServerTokens", "on")}";', "        access_log off;"]
     if p.get("HealthStatus"):
@@ -1048,13 +1106,14 @@ def render_main(params: dict | None = None, wallarm_global_mode: str | None = No
 
 # --------------------------------------------------------------------------- convenience
 
-def ingress_files(ingresses, base=None, wildcard=False, secrets=()):
-    """Configurator.AddOrUpdateIngress for a list of plain Ingress objects -> {file stem: text}."""
+def ingress_files(ingresses, base=None, wildcard=False, secrets=(), endpoints=None, is_plus=False):
+    """Configurator.AddOrUpdateIngress for a list of plain Ingress objects -> {file stem: text};
+    endpoints: {"<svc><port>": ["ip:port", ...]} (IngressEx.Endpoints)."""
     base = base or default_config_params()
     out = {}
     for ing in ingresses:
-        ex = {"Ingress": ing, "Endpoints": {}}
-        cfg = generate_nginx_cfg(ex, tls_pems(ing, wildcard, secrets), False, base)
+        ex = {"Ingress": ing, "Endpoints": endpoints or {}}
+        cfg = generate_nginx_cfg(ex, tls_pems(ing, wildcard, secrets), False, base, is_plus=is_plus)
         out[object_meta_to_file_name(ing)] = render_ingress(cfg)
     return out
 

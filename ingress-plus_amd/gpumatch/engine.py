@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GM_LIB") or os.path.join(os.path.dirname(HERE), "libgpumatch.so")
 
 GM_OK = 0
-GM_ABI_VERSION = 7   # include/gpumatch.h
+GM_ABI_VERSION = 8   # include/gpumatch.h
 GM_E_OVERFLOW = -4
 GM_E_STALE = -9
 GM_E_COMM = -7
@@ -61,7 +61,7 @@ class GmStats(ctypes.Structure):
                 [(f, ctypes.c_uint32) for f in STATS_FIELDS_WAF] +
                 [("scratch_scale", ctypes.c_float), ("n_set_reruns", ctypes.c_uint32),
                  ("set_shift", ctypes.c_uint32), ("n_alw_members", ctypes.c_uint32),
-                 ("reserved_stats", ctypes.c_uint32 * 2)])
+                 ("last_redo", ctypes.c_uint32), ("reserved_stats", ctypes.c_uint32 * 1)])
 
 
 class GmBatch(ctypes.Structure):
@@ -177,6 +177,7 @@ class Engine:
         d = {f: getattr(s, f) for f in STATS_FIELDS + STATS_FIELDS64 + STATS_FIELDS_MS + STATS_FIELDS_WAF}
         d["scratch_scale"] = s.scratch_scale
         d["n_set_reruns"] = s.n_set_reruns
+        d["last_redo"] = s.last_redo
         d["set_shift"] = s.set_shift
         d["n_alw_members"] = s.n_alw_members
         return d

@@ -157,3 +157,59 @@ def gen_requests(n: int, seed: int = records.SEED_BASE + 40, hot: tuple = (), up
     rid = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
     return records.build(n, fields, np.full(n, 80), np.zeros(n, np.uint8), rid=rid,
                          remote_port=rng.integers(1024, 65535, n))
+
+
+# ---------------------------------------------------------------- NGINX Plus sticky cookie
+# Ingresses rendered by the Plus template (nginx-plus.ingress.tmpl:9-11) with
+# nginx.com/sticky-cookie-services (annotations.go:387-399, 511-524) over three balancing methods.
+STICKY_METHODS = ("round_robin", "least_conn", "random two least_conn")
+
+
+def sticky_endpoints(k: int) -> list:
+    return [f"10.9.{k}.{j + 1}:80" for j in range(5 + k)]
+
+
+def sticky_ingresses():
+    """(ingress objects, endpoints) for the sticky workload: ingress k balances svc-k with
+    STICKY_METHODS[k] and sticky cookie srv_<k> (svc-x, never declared sticky, balances without);
+    an invalid sticky declaration is ignored, as ParseConfigMap's log-and-ignore does."""
+    ings, eps = [], {}
+    for k, m in enumerate(STICKY_METHODS):
+        ann = {"nginx.org/lb-method": m,
+               "nginx.com/sticky-cookie-services": f"serviceName=svc-{k} srv_{k} expires=1h path=/;bad-entry"}
+        ings.append({"metadata": {"name": f"sticky{k}", "namespace": "default", "annotations": ann},
+                     "spec": {"rules": [{"host": f"s{k}.example.com", "http": {"paths": [
+                         {"path": "/", "backend": {"serviceName": f"svc-{k}", "servicePort": 80}},
+                         {"path": "/x", "backend": {"serviceName": "svc-x", "servicePort": 80}}]}}]}})
+        eps[f"svc-{k}80"] = sticky_endpoints(k)
+    eps["svc-x80"] = ["10.9.9.1:80", "10.9.9.2:80"]
+    return ings, eps
+
+
+def sticky_blob() -> bytes:
+    from . import confgen
+    ings, eps = sticky_ingresses()
+    return blob.make_blob(confgen.render_main(), confgen.ingress_files(ings, endpoints=eps, is_plus=True))
+
+
+def sticky_requests(n: int, seed: int = records.SEED_BASE + 77, down=()):
+    """Requests to the sticky ingresses with a srv_<k> cookie that names a peer (its hex MD5), a
+    down peer, another upstream's peer, no peer (stale), an uppercase or short value, or none."""
+    import hashlib
+    rng = np.random.Generator(np.random.PCG64(seed))
+    items = []
+    for i in range(n):
+        k = int(rng.integers(0, len(STICKY_METHODS)))
+        eps = sticky_endpoints(k)
+        r = int(rng.integers(0, 10))
+        hx = hashlib.md5(eps[int(rng.integers(0, len(eps)))].encode()).hexdigest()
+        cookie = {0: hx, 1: hx, 2: hx, 3: hashlib.md5(b"10.9.9.1:80").hexdigest(), 4: "0" * 32, 5: hx.upper(),
+                  6: hx[:31], 7: None, 8: hx, 9: hx}[r]
+        hdrs = []
+        if cookie is not None:
+            name = f"srv_{k}" if r != 9 else f"srv_{(k + 1) % len(STICKY_METHODS)}"   # another upstream's cookie
+            hdrs.append(("Cookie", f"a=b; {name}={cookie}" if rng.random() < 0.5 else f"{name}={cookie}"))
+        uri = "/x" if rng.random() < 0.1 else "/"
+        items.append({"host": f"s{k}.example.com", "uri": uri, "headers": hdrs, "port": 80,
+                      "rid": bytes(rng.integers(0, 256, 16, dtype=np.uint8)), "raddr": f"10.200.{i % 200}.{i % 250 + 1}"})
+    return records.from_dicts(items)

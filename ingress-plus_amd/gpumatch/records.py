@@ -14,6 +14,7 @@ from __future__ import annotations
 import numpy as np
 
 FIELDS = ("uri", "args", "hdrs", "body", "host", "method", "ruri", "raddr")
+_FIELDS = FIELDS
 SCAN_FIELDS = ("uri", "args", "hdrs", "body")
 
 REQ_DTYPE = np.dtype([
@@ -80,8 +81,10 @@ def list_seg(items) -> Seg:
 
 # --------------------------------------------------------------------------- builder
 
-def build(n: int, fields: dict, port, flags, rid=None, remote_port=None, chunk: int = 1 << 17):
-    """Assemble headers + arena.  ``fields[name]`` is a list of Seg (concatenated per record)."""
+def build(n: int, fields: dict, port, flags, rid=None, remote_port=None, chunk: int = 1 << 17, proxy_port=None):
+    """Assemble headers + arena.  ``fields[name]`` is a list of Seg (concatenated per record); an
+    optional "paddr" field ($proxy_protocol_addr, <= 46 bytes, after raddr) and proxy_port."""
+    FIELDS = _FIELDS + (("paddr",) if "paddr" in fields else ())
     lens = {}
     for f in FIELDS:
         segs = fields.get(f, [])
@@ -106,8 +109,16 @@ def build(n: int, fields: dict, port, flags, rid=None, remote_port=None, chunk: 
 
     reqs = np.zeros(n, dtype=REQ_DTYPE)
     reqs["base"] = base
-    for f in FIELDS:
+    for f in _FIELDS:
         reqs[LEN_FIELD[f]] = lens[f]
+    if "paddr" in fields:
+        if lens["paddr"].max(initial=0) > 46:
+            raise ValueError("paddr longer than 46")
+        reqs["pad0"][:, 0] = lens["paddr"]
+        if proxy_port is not None:
+            pp = np.asarray(proxy_port, dtype=np.int64) * (lens["paddr"] > 0)
+            reqs["pad1"][:, 0] = pp & 0xFF
+            reqs["pad1"][:, 1] = pp >> 8
     reqs["port"] = port
     reqs["flags"] = flags
     if remote_port is not None:
@@ -133,25 +144,40 @@ def build(n: int, fields: dict, port, flags, rid=None, remote_port=None, chunk: 
     return reqs, arena[:arena_len] if arena_len else arena[:0]
 
 
+# the payload as the wire parser writes it: the eight fields, then $proxy_protocol_addr (its length
+# in pad0[0], gpumatch.h)
+WIRE_FIELDS = FIELDS + ("paddr",)
+
+
+def field_len(r, f: str) -> int:
+    return int(r["pad0"][0]) if f == "paddr" else int(r[LEN_FIELD[f]])
+
+
 def field_bytes(reqs, arena, i: int, name: str) -> bytes:
     """Python accessor used by tests."""
     r = reqs[i]
     off = int(r["base"])
-    for f in FIELDS:
-        L = int(r[LEN_FIELD[f]])
+    for f in WIRE_FIELDS:
+        L = field_len(r, f)
         if f == name:
             return bytes(arena[off:off + L])
         off += L
     raise KeyError(name)
 
 
+def proxy_port(r) -> int:
+    """$proxy_protocol_port of a record (pad1[0..1])."""
+    return int(r["pad1"][0]) | int(r["pad1"][1]) << 8
+
+
 def from_dicts(items: list[dict]):
     """Build a batch from explicit requests (KAT fixtures).  Keys: host, method, uri, args,
     headers (list of (name, value)), body, https, http2, chunked, port, rid (bytes16/hex), raddr,
-    ruri, remote_port."""
+    ruri, remote_port, paddr / proxy_port (the PROXY protocol source)."""
     n = len(items)
-    cols = {f: [] for f in FIELDS}
-    ports, flags, rids, rports = [], [], [], []
+    proxy = any("paddr" in it for it in items)
+    cols = {f: [] for f in FIELDS + (("paddr",) if proxy else ())}
+    ports, flags, rids, rports, pports = [], [], [], [], []
     for it in items:
         hdrs = it.get("headers", [])
         hb = b"".join((k.encode() if isinstance(k, str) else k) + b": " +
@@ -175,9 +201,12 @@ def from_dicts(items: list[dict]):
             rid = bytes.fromhex(rid)
         rids.append(np.frombuffer(rid, dtype=np.uint8))
         rports.append(int(it.get("remote_port", 40000)))
-    fields = {f: [list_seg(cols[f])] for f in FIELDS}
+        if proxy:   # $proxy_protocol_addr / port, as gm_parse_requests leaves them
+            cols["paddr"].append(it.get("paddr", ""))
+            pports.append(int(it.get("proxy_port", 0)))
+    fields = {f: [list_seg(cols[f])] for f in cols}
     return build(n, fields, np.array(ports), np.array(flags), np.stack(rids) if n else None,
-                 np.array(rports))
+                 np.array(rports), proxy_port=np.array(pports) if proxy else None)
 
 
 # --------------------------------------------------------------------------- text pools

@@ -13,9 +13,29 @@ from . import records
 
 WIRE_MSG_DTYPE = np.dtype([
     ("off", "<u8"), ("len", "<u4"), ("port", "<u2"), ("remote_port", "<u2"), ("flags", "u1"),
-    ("raddr_len", "u1"), ("pad", "u1", (2,)), ("rid", "u1", (16,)), ("raddr", "u1", (40,)), ("pad2", "u1", (4,)),
+    ("raddr_len", "u1"), ("paddr_len", "u1"), ("pad", "u1"), ("rid", "u1", (16,)), ("raddr", "u1", (40,)),
+    ("proxy_port", "<u2"), ("pad2", "u1", (2,)), ("paddr", "u1", (46,)), ("pad3", "u1", (2,)),
 ])
-assert WIRE_MSG_DTYPE.itemsize == 80
+assert WIRE_MSG_DTYPE.itemsize == 128
+WIRE_PROXY_DONE = 0x40   # a keep-alive request of a proxy_protocol connection (gpumatch.h)
+
+
+def proxy_v1(src: str, dst: str = "10.0.0.1", sport: int = 51234, dport: int = 443, fam: str | None = None) -> bytes:
+    """A PROXY protocol v1 header line ("PROXY TCP4 src dst sport dport\\r\\n")."""
+    fam = fam or ("TCP6" if ":" in src else "TCP4")
+    return f"PROXY {fam} {src} {dst} {sport} {dport}\r\n".encode()
+
+
+def proxy_v2(src: str, dst: str = "10.0.0.1", sport: int = 51234, dport: int = 443, command: int = 1,
+             transport: int = 1, tlv: bytes = b"") -> bytes:
+    """A PROXY protocol v2 header (binary): signature, version 2 | command, family | transport, length,
+    the addresses and ports, then optional TLV bytes."""
+    import ipaddress
+    a, d = ipaddress.ip_address(src), ipaddress.ip_address(dst)
+    fam = 1 if a.version == 4 else 2
+    body = a.packed + d.packed + sport.to_bytes(2, "big") + dport.to_bytes(2, "big") + tlv
+    return (b"\r\n\r\n\x00\r\nQUIT\n" + bytes([0x20 | command, fam << 4 | transport]) +
+            len(body).to_bytes(2, "big") + body)
 
 
 def _b(x):
@@ -79,13 +99,19 @@ def build(messages, conn=None, seed=0, align=1):
         msgs[i]["raddr"][:len(ra)] = np.frombuffer(ra, np.uint8)
         rid = c.get("rid")
         msgs[i]["rid"] = np.frombuffer(rid, np.uint8) if rid is not None else rng.integers(0, 256, 16, dtype=np.uint8)
+        if c.get("proxy_done"):   # a keep-alive request: the connection's PROXY address, from the caller
+            msgs[i]["flags"] |= WIRE_PROXY_DONE
+            pa = _b(c.get("paddr", b""))[:46]
+            msgs[i]["paddr_len"] = len(pa)
+            msgs[i]["paddr"][:len(pa)] = np.frombuffer(pa, np.uint8)
+            msgs[i]["proxy_port"] = c.get("proxy_port", 0)
     wire = np.frombuffer(b"".join(parts) or b"\0", dtype=np.uint8).copy()
     return wire, msgs
 
 
 def arena_bound(msgs) -> int:
-    """The arena capacity gm_parse_requests always fits in: sum of align16(2 * len + raddr_len)."""
-    return int((((2 * msgs["len"].astype(np.int64) + msgs["raddr_len"]) + 15) & ~15).sum()) + 16
+    """The arena capacity gm_parse_requests always fits in: sum of align16(2 * len + raddr_len + 46)."""
+    return int((((2 * msgs["len"].astype(np.int64) + msgs["raddr_len"] + 46) + 15) & ~15).sum()) + 16
 
 
 # ---------------------------------------------------------------- synthetic mix
@@ -168,3 +194,52 @@ def synthetic(n: int, seed: int = 0xC0FFEE + 7, edge_rate: float = 0.15):
         out.append(serialize(it))
     conn = [{"https": bool(rng.random() < 0.5), "rid": bytes(reqs[i]["rid"])} for i in range(n)]
     return out, conn
+
+
+# ---------------------------------------------------------------- PROXY protocol cases
+def proxy_cases():
+    """Messages on a proxy_protocol listener (port 80 plain, 443 TLS) and what nginx 1.17.3's
+    ngx_proxy_protocol_read makes of them: (message bytes, conn dict, expected) with expected
+    either 444 (no response: a broken / missing header, or no request after it) or the record's
+    (paddr, proxy_port, uri).  The KATs of tests/test_wire.py and the GPU parity test use them."""
+    req = serialize({"uri": "/tea", "host": "cafe.example.com"})
+    v6 = proxy_v2("2001:db8:0:0:0:0:0:1", "2001:db8::2", 443, 8443)
+    C = {"https": False, "port": 80}
+    cases = [
+        (proxy_v1("192.168.0.1", "192.168.0.11", 56324, 80) + req, C, (b"192.168.0.1", 56324, b"/tea")),
+        (proxy_v1("2001:DB8::1", "2001:db8::2", 1, 80) + req, C, (b"2001:DB8::1", 1, b"/tea")),   # v1: as sent
+        (b"PROXY UNKNOWN\r\n" + req, C, (b"", 0, b"/tea")),
+        (b"PROXY UNKNOWN ffff:f...f:ffff ffff:f...f:ffff 65535 65535\r\n" + req, C, (b"", 0, b"/tea")),
+        (proxy_v1("10.0.0.5:99", "10.0.0.1", 7, 80) + req, C, (b"10.0.0.5:99", 7, b"/tea")),   # chars only
+        (proxy_v1("1.2.3.4", "5.6.7.8", 0, 0) + req, C, (b"1.2.3.4", 0, b"/tea")),
+        (b"PROXY TCP4 1.2.3.4 5.6.7.8 080 80\r\n" + req, C, (b"1.2.3.4", 80, b"/tea")),   # ngx_atoi
+        (proxy_v2("203.0.113.7", "10.0.0.1", 40001, 80) + req, C, (b"203.0.113.7", 40001, b"/tea")),
+        (v6 + req, {"https": True, "port": 443}, (b"2001:db8::1", 443, b"/tea")),          # ngx_sock_ntop
+        (proxy_v2("203.0.113.7", "10.0.0.1", 40001, 80, tlv=b"\x04\x00\x01x") + req, C,
+         (b"203.0.113.7", 40001, b"/tea")),                                                 # TLVs skipped
+        (proxy_v2("203.0.113.7", "10.0.0.1", 1, 80, command=0) + req, C, (b"", 0, b"/tea")),    # LOCAL
+        (proxy_v2("203.0.113.7", "10.0.0.1", 1, 80, transport=2) + req, C, (b"", 0, b"/tea")),  # DGRAM
+        (proxy_v2("::ffff:1.2.3.4", "::1", 9, 80) + req, C, (b"::ffff:1.2.3.4", 9, b"/tea")),
+        # broken or missing: nginx closes the connection
+        (req, C, 444),
+        (b"PROXY TCP4 1.2.3.4 5.6.7.8 99999 80\r\n" + req, C, 444),
+        (b"PROXY TCP4 1.2.3.4 5.6.7.8 -1 80\r\n" + req, C, 444),
+        (b"PROXY TCP4 1.2.3.4 5.6.7.8  80\r\n" + req, C, 444),                  # empty port
+        (b"PROXY TCP5 1.2.3.4 5.6.7.8 1 80\r\n" + req, C, 444),
+        (b"PROXY TCP4 1.2.3.g 5.6.7.8 1 80\r\n" + req, C, 444),
+        (b"PROXY TCP4 1.2.3.4\r\n" + req, C, 444),
+        (b"proxy TCP4 1.2.3.4 5.6.7.8 1 80\r\n" + req, C, 444),
+        (b"PROXY TCP4 1.2.3.4 5.6.7.8 1 80", C, 444),                           # no CRLF at all
+        (proxy_v1("1.2.3.4"), C, 444),                                          # no request after it
+        (b"\r\n\r\n\x00\r\nQUIT\n\x11\x11\x00\x0c" + bytes(12) + req, C, 444),   # v2, version 1
+        (b"\r\n\r\n\x00\r\nQUIT\n\x21\x11\x01\x00" + bytes(12), C, 444),         # length past the end
+        (b"\r\n\r\n\x00\r\nQUIT\n\x21\x11\x00\x08" + bytes(8) + req, C, 444),    # INET, too short
+        (b"PROXY TCP4 " + b"1" * 60 + b" 5.6.7.8 1 80\r\n" + req, C, (b"", 1, b"/tea")),   # too long to be an address
+        # keep-alive: the caller's copy of the connection's address, no header read
+        (req, {"https": False, "port": 80, "proxy_done": True, "paddr": "198.51.100.9", "proxy_port": 333},
+         (b"198.51.100.9", 333, b"/tea")),
+        # not a proxy_protocol port: a PROXY line is a (bad) request line
+        (proxy_v1("1.2.3.4") + req, {"https": False, "port": 8080}, 400),
+        (req, {"https": False, "port": 8080}, (b"", 0, b"/tea")),
+    ]
+    return cases

@@ -185,7 +185,7 @@ typedef struct {
 } orip_t;
 
 typedef struct {
-    int id; int nports; int ports[16]; int ssl[16]; int def[16];
+    int id; int nports; int ports[16]; int ssl[16]; int def[16]; int pp[16];   /* pp: proxy_protocol */
     char *cmbs;               /* server-level client_max_body_size, NULL inherited */
     int64_t body_max;         /* limit in effect for a request with no location (-1 none) */
     orip_t rip;
@@ -221,6 +221,7 @@ typedef struct {
     int npeers; char **addr; int *down;
     int first_peer;
     opoint_t *ring; int nring;
+    char *sticky;             /* NGINX Plus `sticky cookie <name>`: "$cookie_<name>", NULL none */
 } oups_t;
 
 typedef struct orc_ctx {
@@ -763,12 +764,16 @@ static void add_server(build_t *B, dir_t *s, int http_waf) {
             if (!strncmp(a, "unix:", 5)) continue;
             const char *colon = strrchr(a, ':');
             int port = atoi(colon ? colon + 1 : a);
-            int ssl = 0, def = 0;
+            int ssl = 0, def = 0, pp = 0;
             for (int k = 2; k < d->nargs; k++) {
                 if (!strcmp(d->args[k], "ssl")) ssl = 1;
                 if (!strcmp(d->args[k], "default_server") || !strcmp(d->args[k], "default")) def = 1;
+                if (!strcmp(d->args[k], "proxy_protocol")) pp = 1;
             }
-            if (S.nports < 16) { S.ports[S.nports] = port; S.ssl[S.nports] = ssl; S.def[S.nports] = def; S.nports++; }
+            if (S.nports < 16) {
+                S.ports[S.nports] = port; S.ssl[S.nports] = ssl; S.def[S.nports] = def; S.pp[S.nports] = pp;
+                S.nports++;
+            }
         } else if (!strcmp(n, "server_name")) {
             for (int k = 1; k < d->nargs; k++) {
                 S.names = realloc(S.names, sizeof(char *) * (S.nnames + 1));
@@ -1178,6 +1183,12 @@ static void build_upstreams(orc_ctx *c) {
                 else if (!strcmp(k->args[1], "two") && (k->nargs == 2 || (k->nargs == 3 && !strcmp(k->args[2], "least_conn"))))
                     U->method = OM_RANDOM2;
                 else defer = 1;
+            } else if (!strcmp(m, "sticky") && k->nargs >= 3 && !strcmp(k->args[1], "cookie")) {
+                /* expires= / domain= / path= / httponly / secure: the response's Set-Cookie only */
+                char b[300];
+                snprintf(b, sizeof b, "$cookie_%s", k->args[2]);
+                free(U->sticky);
+                U->sticky = strdup(b);
             } else if (!strcmp(m, "least_time") || !strcmp(m, "sticky") || !strcmp(m, "queue") ||
                        !strcmp(m, "ntlm") || !strcmp(m, "hash")) defer = 1;
         }
@@ -1329,7 +1340,7 @@ int orc_info(orc_ctx *c, uint32_t *out4) {
 /* ------------------------------------------------------------------ request access */
 typedef struct {
     const gm_req *r; const uint8_t *a;
-    sv uri, args, hdrs, body, host, method, ruri, raddr;
+    sv uri, args, hdrs, body, host, method, ruri, raddr, paddr;
     const srv_t *S;        /* the server (its realip settings), NULL before it is known */
     int rip;               /* 0 not evaluated, 1 unchanged, 2 replaced, 3 unknown to the engine */
     char ra[64]; int ra_len; oaddr_t raddr2;
@@ -1345,7 +1356,8 @@ static void rq_init(rq_t *q, const gm_req *r, const uint8_t *arena) {
     q->host = (sv){p, r->host_len}; p += r->host_len;
     q->method = (sv){p, r->method_len}; p += r->method_len;
     q->ruri = (sv){p, r->ruri_len}; p += r->ruri_len;
-    q->raddr = (sv){p, r->raddr_len};
+    q->raddr = (sv){p, r->raddr_len}; p += r->raddr_len;
+    q->paddr = (sv){p, r->pad0[0]};   /* $proxy_protocol_addr */
     q->S = NULL; q->rip = 0;
 }
 
@@ -1360,12 +1372,20 @@ static void orc_realip(rq_t *q) {
     oaddr_t a;
     memset(&a, 0, sizeof a);
     if (!(q->raddr.n > 0 && q->raddr.n < 46 && o_parse_addr(q->raddr.p, q->raddr.n, &a))) a.fam = 0;
-    if (S->rtype == 3) {   /* proxy_protocol: the address is in the PROXY header, not the record */
-        if (a.fam && o_cidr_match(S, &a)) q->rip = 3;
+    int rc = 0;
+    if (S->rtype == 3) {
+        /* NGX_HTTP_REALIP_PROXY: the connection's PROXY address (none: declined) through
+         * ngx_http_get_forwarded_addr, then the PROXY source port */
+        if (!a.fam || q->paddr.n == 0) return;
+        rc = o_fwd_internal(S, &a, q->paddr.p, q->paddr.n);
+        if (rc == 0) return;
+        a.port = q->r->pad1[0] | q->r->pad1[1] << 8;
+        q->raddr2 = a;
+        q->ra_len = o_ntop(&a, q->ra);
+        q->rip = 2;
         return;
     }
     if (!a.fam) return;
-    int rc = 0;
     int pos = 0; sv hn, vv;
     if (S->rtype == 2) {
         /* every X-Forwarded-For line, last first (ngx_http_get_forwarded_addr over the array) */
@@ -2437,10 +2457,88 @@ static int orc_parse_one(const uint8_t *b, int n, orc_rl_t *R, obuf_t *uri, obuf
     return 0;
 }
 
+/* ngx_proxy_protocol_read (nginx 1.17.3 src/core/ngx_proxy_protocol.c) over the connection's
+ * first bytes b[0, n): the header's length, or -1 for a missing / broken header (nginx logs
+ * "broken header" and closes the connection).  v1: "PROXY TCP4|TCP6 <src> <dst> <sport> <dport>"
+ * CRLF -- the source address kept as sent (hex digits, ':' and '.'), the port a decimal 0..65535,
+ * the destination fields not checked, the line's end the first CRLF after the source port;
+ * "PROXY UNKNOWN" ... CRLF: no address.  v2: the 12-byte signature, version 2, a length that fits;
+ * PROXY command over STREAM with AF_INET / AF_INET6 gives the source address (ngx_sock_ntop) and
+ * port; LOCAL, other transports or families: no address.  *alen = 0 when there is no address. */
+static int o_proxy_read(const uint8_t *b, int n, char *addr, int *alen, int *port) {
+    static const uint8_t sig[12] = {'\r', '\n', '\r', '\n', 0, '\r', '\n', 'Q', 'U', 'I', 'T', '\n'};
+    *alen = 0; *port = 0;
+    if (n >= 16 && !memcmp(b, sig, 12)) {
+        if (b[12] >> 4 != 2) return -1;
+        int len = b[14] << 8 | b[15];
+        if (n - 16 < len) return -1;
+        int end = 16 + len;
+        if ((b[12] & 15) != 1 || (b[13] & 15) != 1) return end;
+        oaddr_t a; memset(&a, 0, sizeof a);
+        int fam = b[13] >> 4;
+        if (fam == 1) {
+            if (len < 12) return -1;
+            a.fam = 4; memcpy(a.b, b + 16, 4); *port = b[24] << 8 | b[25];
+        } else if (fam == 2) {
+            if (len < 36) return -1;
+            a.fam = 6; memcpy(a.b, b + 16, 16); *port = b[48] << 8 | b[49];
+        } else return end;
+        *alen = o_ntop(&a, addr);
+        return end;
+    }
+    if (n < 8 || memcmp(b, "PROXY ", 6)) return -1;
+    int p = 6;
+    if (n - 6 >= 7 && !memcmp(b + 6, "UNKNOWN", 7)) p += 7;
+    else {
+        if (n - 6 < 5 || memcmp(b + 6, "TCP", 3) || (b[9] != '4' && b[9] != '6') || b[10] != ' ') return -1;
+        p = 11;
+        int a0 = p;
+        for (;;) {
+            if (p == n) return -1;
+            int ch = b[p++];
+            if (ch == ' ') break;
+            if (ch != ':' && ch != '.' && !isxdigit(ch)) return -1;
+        }
+        int al = p - a0 - 1;
+        while (1) { if (p == n) return -1; if (b[p++] == ' ') break; }
+        int p0 = p;
+        while (1) { if (p == n) return -1; if (b[p++] == ' ') break; }
+        int pl = p - p0 - 1;
+        if (pl == 0) return -1;
+        long v = 0;
+        for (int k = 0; k < pl; k++) {
+            if (!isdigit(b[p0 + k]) || v > 100000000L) return -1;
+            v = v * 10 + (b[p0 + k] - '0');
+        }
+        if (v > 65535) return -1;
+        *port = (int)v;
+        if (al <= 46) { memcpy(addr, b + a0, (size_t)al); *alen = al; }   /* longer: never an address */
+    }
+    for (; p + 1 < n; p++) if (b[p] == '\r' && b[p + 1] == '\n') return p + 2;
+    *alen = 0; *port = 0;
+    return -1;
+}
+
+/* the generation's `listen ... proxy_protocol` ports (ORed over every listen of a port) */
+int orc_proxy_ports(orc_ctx *c, uint16_t *out, int cap) {
+    int k = 0;
+    for (int s = 0; s < c->nsrv; s++)
+        for (int i = 0; i < c->srv[s].nports; i++) {
+            if (!c->srv[s].pp[i]) continue;
+            int seen = 0;
+            for (int j = 0; j < k; j++) seen |= out[j] == c->srv[s].ports[i];
+            if (!seen && k < cap) out[k++] = (uint16_t)c->srv[s].ports[i];
+        }
+    return k;
+}
+
 /* n requests -> gm_req records + a packed payload arena (gm_req field order, 16-B aligned
- * bases).  Returns the arena length, or -1 if `cap` is too small. */
-int64_t orc_parse_requests(const uint8_t *wire, const gm_wire_msg *msgs, uint32_t n, gm_req *reqs, uint8_t *arena,
-                           uint64_t cap) {
+ * bases).  Returns the arena length, or -1 if `cap` is too small.  pports[0, npp): the listen
+ * ports with proxy_protocol: a message there starts with its connection's PROXY header (unless
+ * GM_WIRE_PROXY_DONE: a keep-alive request, the caller's paddr / proxy_port) -- a broken or
+ * missing one, or one with no request after it, gives an invalid record with status 444. */
+int64_t orc_parse_requests_pp(const uint8_t *wire, const gm_wire_msg *msgs, uint32_t n, gm_req *reqs, uint8_t *arena,
+                              uint64_t cap, const uint16_t *pports, int npp) {
     obuf_t uri = {0}, hdrs = {0}, body = {0};
     uint64_t o = 0;
     int64_t rc = 0;
@@ -2449,7 +2547,22 @@ int64_t orc_parse_requests(const uint8_t *wire, const gm_wire_msg *msgs, uint32_
         orc_rl_t R;
         const uint8_t *host; int host_len;
         uri.n = hdrs.n = body.n = 0;
-        int st = orc_parse_one(wire + m->off, (int)m->len, &R, &uri, &hdrs, &body, &host, &host_len);
+        int proxy = 0;
+        for (int j = 0; j < npp; j++) proxy |= pports[j] == m->port;
+        const uint8_t *mb = wire + m->off;
+        int mn = (int)m->len;
+        char pa[64]; int pal = 0, pport = 0, st;
+        if (proxy && (m->flags & GM_WIRE_PROXY_DONE)) {
+            pal = m->paddr_len <= 46 ? m->paddr_len : 0;
+            memcpy(pa, m->paddr, (size_t)pal);
+            pport = m->proxy_port;
+            st = -1;
+        } else if (proxy) {
+            int used = o_proxy_read(mb, mn, pa, &pal, &pport);
+            if (used < 0 || used >= mn) { st = 444; pal = 0; pport = 0; }
+            else { mb += used; mn -= used; st = -1; }
+        } else st = -1;
+        if (st < 0) st = orc_parse_one(mb, mn, &R, &uri, &hdrs, &body, &host, &host_len);
         gm_req *r = &reqs[k];
         memset(r, 0, sizeof *r);
         r->base = o;
@@ -2457,7 +2570,9 @@ int64_t orc_parse_requests(const uint8_t *wire, const gm_wire_msg *msgs, uint32_
         memcpy(r->rid, m->rid, 16);
         const int ra = m->raddr_len > 40 ? 40 : m->raddr_len;
         r->flags = m->flags & (GM_REQ_HTTPS | GM_REQ_HTTP2);
-        const uint8_t *seg[8]; size_t len[8] = {0};
+        r->pad0[0] = (uint8_t)pal;
+        if (pal) { r->pad1[0] = (uint8_t)pport; r->pad1[1] = (uint8_t)(pport >> 8); }
+        const uint8_t *seg[9]; size_t len[9] = {0};
         if (st) {
             r->flags |= GM_REQ_INVALID;
             r->pad0[1] = (uint8_t)(st & 0xFF); r->pad0[2] = (uint8_t)(st >> 8);
@@ -2473,17 +2588,75 @@ int64_t orc_parse_requests(const uint8_t *wire, const gm_wire_msg *msgs, uint32_
             seg[6] = R.target; len[6] = (size_t)R.target_len;
         }
         seg[7] = m->raddr; len[7] = (size_t)ra;
+        seg[8] = (const uint8_t *)pa; len[8] = (size_t)pal;
         r->uri_len = (uint32_t)len[0]; r->args_len = (uint32_t)len[1]; r->hdr_len = (uint32_t)len[2];
         r->body_len = (uint32_t)len[3]; r->host_len = (uint16_t)len[4]; r->method_len = (uint16_t)len[5];
         r->ruri_len = (uint16_t)len[6]; r->raddr_len = (uint16_t)len[7];
         size_t tot = 0;
-        for (int f = 0; f < 8; f++) tot += len[f];
+        for (int f = 0; f < 9; f++) tot += len[f];
         if (o + tot > cap) { rc = -1; break; }
-        for (int f = 0; f < 8; f++) if (len[f]) { memcpy(arena + o, seg[f], len[f]); o += len[f]; }
+        for (int f = 0; f < 9; f++) if (len[f]) { memcpy(arena + o, seg[f], len[f]); o += len[f]; }
         while (o & 15) { if (o < cap) arena[o] = 0; o++; }
     }
     free(uri.p); free(hdrs.p); free(body.p);
     return rc < 0 ? -1 : (int64_t)o;
+}
+int64_t orc_parse_requests(const uint8_t *wire, const gm_wire_msg *msgs, uint32_t n, gm_req *reqs, uint8_t *arena,
+                           uint64_t cap) {
+    return orc_parse_requests_pp(wire, msgs, n, reqs, arena, cap, NULL, 0);
+}
+
+
+/* RFC 1321 MD5, written from the RFC's round definitions (F, G, H, I and the four rounds of 16
+ * operations), for the NGINX Plus sticky cookie: its value is the lowercase hex MD5 of the peer's
+ * address text */
+#define MD5_ROT(x, c) (((x) << (c)) | ((x) >> (32 - (c))))
+static void o_md5_block(uint32_t st[4], const uint8_t b[64]) {
+    uint32_t X[16];
+    for (int i = 0; i < 16; i++) X[i] = (uint32_t)b[4 * i] | (uint32_t)b[4 * i + 1] << 8 | (uint32_t)b[4 * i + 2] << 16 | (uint32_t)b[4 * i + 3] << 24;
+    uint32_t a = st[0], bb = st[1], c = st[2], d = st[3];
+#define FF(a, b, c, d, k, s, t) a = b + MD5_ROT(a + (((b) & (c)) | (~(b) & (d))) + X[k] + (t), s)
+#define GG(a, b, c, d, k, s, t) a = b + MD5_ROT(a + (((b) & (d)) | ((c) & ~(d))) + X[k] + (t), s)
+#define HH(a, b, c, d, k, s, t) a = b + MD5_ROT(a + ((b) ^ (c) ^ (d)) + X[k] + (t), s)
+#define II(a, b, c, d, k, s, t) a = b + MD5_ROT(a + ((c) ^ ((b) | ~(d))) + X[k] + (t), s)
+    FF(a, bb, c, d, 0, 7, 0xd76aa478); FF(d, a, bb, c, 1, 12, 0xe8c7b756); FF(c, d, a, bb, 2, 17, 0x242070db); FF(bb, c, d, a, 3, 22, 0xc1bdceee);
+    FF(a, bb, c, d, 4, 7, 0xf57c0faf); FF(d, a, bb, c, 5, 12, 0x4787c62a); FF(c, d, a, bb, 6, 17, 0xa8304613); FF(bb, c, d, a, 7, 22, 0xfd469501);
+    FF(a, bb, c, d, 8, 7, 0x698098d8); FF(d, a, bb, c, 9, 12, 0x8b44f7af); FF(c, d, a, bb, 10, 17, 0xffff5bb1); FF(bb, c, d, a, 11, 22, 0x895cd7be);
+    FF(a, bb, c, d, 12, 7, 0x6b901122); FF(d, a, bb, c, 13, 12, 0xfd987193); FF(c, d, a, bb, 14, 17, 0xa679438e); FF(bb, c, d, a, 15, 22, 0x49b40821);
+    GG(a, bb, c, d, 1, 5, 0xf61e2562); GG(d, a, bb, c, 6, 9, 0xc040b340); GG(c, d, a, bb, 11, 14, 0x265e5a51); GG(bb, c, d, a, 0, 20, 0xe9b6c7aa);
+    GG(a, bb, c, d, 5, 5, 0xd62f105d); GG(d, a, bb, c, 10, 9, 0x02441453); GG(c, d, a, bb, 15, 14, 0xd8a1e681); GG(bb, c, d, a, 4, 20, 0xe7d3fbc8);
+    GG(a, bb, c, d, 9, 5, 0x21e1cde6); GG(d, a, bb, c, 14, 9, 0xc33707d6); GG(c, d, a, bb, 3, 14, 0xf4d50d87); GG(bb, c, d, a, 8, 20, 0x455a14ed);
+    GG(a, bb, c, d, 13, 5, 0xa9e3e905); GG(d, a, bb, c, 2, 9, 0xfcefa3f8); GG(c, d, a, bb, 7, 14, 0x676f02d9); GG(bb, c, d, a, 12, 20, 0x8d2a4c8a);
+    HH(a, bb, c, d, 5, 4, 0xfffa3942); HH(d, a, bb, c, 8, 11, 0x8771f681); HH(c, d, a, bb, 11, 16, 0x6d9d6122); HH(bb, c, d, a, 14, 23, 0xfde5380c);
+    HH(a, bb, c, d, 1, 4, 0xa4beea44); HH(d, a, bb, c, 4, 11, 0x4bdecfa9); HH(c, d, a, bb, 7, 16, 0xf6bb4b60); HH(bb, c, d, a, 10, 23, 0xbebfbc70);
+    HH(a, bb, c, d, 13, 4, 0x289b7ec6); HH(d, a, bb, c, 0, 11, 0xeaa127fa); HH(c, d, a, bb, 3, 16, 0xd4ef3085); HH(bb, c, d, a, 6, 23, 0x04881d05);
+    HH(a, bb, c, d, 9, 4, 0xd9d4d039); HH(d, a, bb, c, 12, 11, 0xe6db99e5); HH(c, d, a, bb, 15, 16, 0x1fa27cf8); HH(bb, c, d, a, 2, 23, 0xc4ac5665);
+    II(a, bb, c, d, 0, 6, 0xf4292244); II(d, a, bb, c, 7, 10, 0x432aff97); II(c, d, a, bb, 14, 15, 0xab9423a7); II(bb, c, d, a, 5, 21, 0xfc93a039);
+    II(a, bb, c, d, 12, 6, 0x655b59c3); II(d, a, bb, c, 3, 10, 0x8f0ccc92); II(c, d, a, bb, 10, 15, 0xffeff47d); II(bb, c, d, a, 1, 21, 0x85845dd1);
+    II(a, bb, c, d, 8, 6, 0x6fa87e4f); II(d, a, bb, c, 15, 10, 0xfe2ce6e0); II(c, d, a, bb, 6, 15, 0xa3014314); II(bb, c, d, a, 13, 21, 0x4e0811a1);
+    II(a, bb, c, d, 4, 6, 0xf7537e82); II(d, a, bb, c, 11, 10, 0xbd3af235); II(c, d, a, bb, 2, 15, 0x2ad7d2bb); II(bb, c, d, a, 9, 21, 0xeb86d391);
+#undef FF
+#undef GG
+#undef HH
+#undef II
+    st[0] += a; st[1] += bb; st[2] += c; st[3] += d;
+}
+/* lowercase hex of MD5(p[0, n)) into out[33] */
+void orc_md5_hex(const char *p, int n, char *out) {
+    uint32_t st[4] = {0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476};
+    int i = 0;
+    for (; i + 64 <= n; i += 64) o_md5_block(st, (const uint8_t *)p + i);
+    uint8_t tail[128] = {0};
+    int r = n - i;
+    memcpy(tail, p + i, (size_t)r);
+    tail[r] = 0x80;
+    int tl = r + 1 + 8 <= 64 ? 64 : 128;
+    uint64_t bits = (uint64_t)n * 8;
+    for (int k = 0; k < 8; k++) tail[tl - 8 + k] = (uint8_t)(bits >> (8 * k));
+    o_md5_block(st, tail);
+    if (tl == 128) o_md5_block(st, tail + 64);
+    for (int k = 0; k < 16; k++) sprintf(out + 2 * k, "%02x", (st[k / 4] >> (8 * (k % 4))) & 0xFF);
+    out[32] = 0;
 }
 
 /* ------------------------------------------------------------------ peer selection (§8 f3) */
@@ -2632,7 +2805,24 @@ int orc_select_peers(orc_ctx *c, const gm_req *reqs, const uint8_t *arena, const
         oups_t *U = c->uby[v[i].upstream_id];
         if (!U || U->method == OM_DEFER) { out[i] = GM_PEER_DEFER; continue; }
         if (U->npeers == 0) continue;
-        int p;
+        int p = -1;
+        if (U->sticky) {
+            /* the cookie names a live peer by the hex MD5 of its address: that peer, counted with
+             * the batch (it does not take part in the round-robin / least_conn sequence) */
+            rq_t q; rq_init(&q, &reqs[i], arena);
+            if (v[i].server_id < (uint32_t)c->nsrv) q.S = &c->srv[v[i].server_id];
+            ev_t E = {c, &q, &sc, 0, NULL, NULL};
+            sv ck = eval_complex(&E, U->sticky);
+            if (ck.n == 32) {
+                for (int j = 0; j < U->npeers && p < 0; j++) {
+                    char h[33];
+                    orc_md5_hex(U->addr[j], (int)strlen(U->addr[j]), h);
+                    if (!memcmp(h, ck.p, 32) && LIVE(j)) p = j;
+                }
+            }
+            sc_reset(&sc);
+            if (p >= 0) { picks[U->first_peer + p]++; out[i] = (uint32_t)(U->first_peer + p); continue; }
+        }
         if (U->method == OM_LEAST_CONN) {
             p = orc_lc(U, st);
             if (p >= 0) st[U->first_peer + p].conns++;   /* least_conn sees its own picks at once */

@@ -32,6 +32,9 @@ def lib():
         L.orc_pcre_match.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.orc_set_prefilter.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.orc_factor.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.orc_proxy_ports.restype = ctypes.c_int
+        L.orc_proxy_ports.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.orc_md5_hex.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p]
         _lib = L
     return _lib
 
@@ -65,6 +68,12 @@ class Oracle:
             raise RuntimeError("oracle hit buffer too small")
         return out, hits[:tot]
 
+    def proxy_ports(self):
+        """The listen ports with proxy_protocol, from the oracle's own reading of the config."""
+        out = np.zeros(64, dtype=np.uint16)
+        k = lib().orc_proxy_ports(self.h, out.ctypes.data, 64)
+        return [int(x) for x in out[:k]]
+
 
 def murmur2(b: bytes) -> int:
     return int(lib().orc_murmur2(b, len(b)))
@@ -74,20 +83,23 @@ def pcre_match(pat: str, subj: bytes, caseless: bool = False) -> int:
     return int(lib().orc_pcre_match(pat.encode(), 1 if caseless else 0, subj, len(subj)))
 
 
-def parse_requests(wire: np.ndarray, msgs: np.ndarray):
-    """oracle/gm_oracle.c orc_parse_requests: HTTP/1.x bytes -> (gm_req records, arena)."""
+def parse_requests(wire: np.ndarray, msgs: np.ndarray, proxy_ports=()):
+    """oracle/gm_oracle.c orc_parse_requests_pp: HTTP/1.x bytes -> (gm_req records, arena);
+    proxy_ports: the listen ports with proxy_protocol (Oracle.proxy_ports())."""
     from gpumatch.records import REQ_DTYPE
     L = lib()
-    L.orc_parse_requests.restype = ctypes.c_int64
-    L.orc_parse_requests.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
-                                     ctypes.c_void_p, ctypes.c_uint64]
+    L.orc_parse_requests_pp.restype = ctypes.c_int64
+    L.orc_parse_requests_pp.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
     n = len(msgs)
     reqs = np.zeros(n, dtype=REQ_DTYPE)
-    cap = int((2 * msgs["len"].astype(np.int64) + msgs["raddr_len"] + 16).sum()) + 16
+    cap = int((2 * msgs["len"].astype(np.int64) + msgs["raddr_len"] + 64).sum()) + 16
     arena = np.zeros(cap, dtype=np.uint8)
     w = np.ascontiguousarray(wire)
     m = np.ascontiguousarray(msgs)
-    tot = L.orc_parse_requests(w.ctypes.data, m.ctypes.data, n, reqs.ctypes.data, arena.ctypes.data, cap)
+    pp = np.ascontiguousarray(np.asarray(list(proxy_ports) or [0], dtype=np.uint16))
+    tot = L.orc_parse_requests_pp(w.ctypes.data, m.ctypes.data, n, reqs.ctypes.data, arena.ctypes.data, cap,
+                                  pp.ctypes.data, len(proxy_ports))
     if tot < 0:
         raise RuntimeError("oracle parse: arena capacity")
     return reqs, arena[:tot]

@@ -196,15 +196,37 @@ def realip_header_port_case():
 
 
 def realip_proxy_protocol_case():
-    """real_ip_header proxy_protocol: the PROXY header's address is not in a record, so a trusted
-    connection's verdict that reads $remote_addr defers; an untrusted one is decided."""
+    """real_ip_header proxy_protocol (examples/proxy-protocol/README.md): a trusted connection's
+    $remote_addr is its PROXY header's source address (the record's paddr, gm_parse_requests); no
+    PROXY address (a record without one, "PROXY UNKNOWN") or an untrusted peer keeps the peer's;
+    a PROXY address that is no address is declined too."""
     vs = _rules_vs("pp.example.com", {"variable": "$remote_addr"}, ADDRS)
     b = _vs_blob(vs, SetRealIPFrom=["10.0.0.0/8"], RealIPHeader="proxy_protocol", ProxyProtocol=True)
     h = "pp.example.com"
     cases = [
-        ({"host": h, "uri": "/", "raddr": "10.9.9.9"}, UNSUPPORTED),
+        ({"host": h, "uri": "/", "raddr": "10.9.9.9"}, 0xFF),                                   # no PROXY address
         ({"host": h, "uri": "/", "raddr": "1.2.3.4"}, 3),
-        ({"host": h, "uri": "/", "raddr": "10.0.0.5"}, UNSUPPORTED),
+        ({"host": h, "uri": "/", "raddr": "10.0.0.5"}, 0),
+        ({"host": h, "uri": "/", "raddr": "10.9.9.9", "paddr": "1.2.3.4", "proxy_port": 5555}, 3),
+        ({"host": h, "uri": "/", "raddr": "10.9.9.9", "paddr": "2001:db8::1", "proxy_port": 1}, 1),
+        ({"host": h, "uri": "/", "raddr": "10.9.9.9", "paddr": "2001:DB8:0::1", "proxy_port": 1}, 1),   # ntop
+        ({"host": h, "uri": "/", "raddr": "8.8.8.8", "paddr": "1.2.3.4", "proxy_port": 5555}, 0xFF),  # untrusted
+        ({"host": h, "uri": "/", "raddr": "10.9.9.9", "paddr": "1.2.3", "proxy_port": 5555}, 0xFF),   # no address
+        ({"host": h, "uri": "/", "raddr": "10.9.9.9", "paddr": "10.0.0.5:99", "proxy_port": 7}, 0),   # addr:port
+    ]
+    return b, cases
+
+
+def proxy_port_case():
+    """real_ip_header proxy_protocol: $remote_port becomes the PROXY header's source port."""
+    vs = _rules_vs("pport.example.com", {"variable": "$remote_port"}, ["5555", "40000"])
+    b = _vs_blob(vs, SetRealIPFrom=["0.0.0.0/0"], RealIPHeader="proxy_protocol", ProxyProtocol=True)
+    h = "pport.example.com"
+    cases = [
+        ({"host": h, "uri": "/", "raddr": "10.9.9.9", "paddr": "1.2.3.4", "proxy_port": 5555}, 0),
+        ({"host": h, "uri": "/", "raddr": "10.9.9.9"}, 1),                    # no PROXY address: the peer's
+        ({"host": h, "uri": "/", "raddr": "10.9.9.9", "paddr": "1.2.3.4", "proxy_port": 40000}, 1),
+        ({"host": h, "uri": "/", "raddr": "10.9.9.9", "paddr": "zz", "proxy_port": 5555}, 1),   # declined
     ]
     return b, cases
 
@@ -255,4 +277,5 @@ def http_unknown_case():
 ROUTE_CASES = {"body_limit": body_limit_case, "vs_body": vs_body_case, "http_unknown": http_unknown_case}
 # expected: the rules route's match index (0xFF default), or UNSUPPORTED for a deferred verdict
 MATCH_CASES = {"realip_xff": realip_xff_case, "realip_xrealip": realip_xrealip_case,
-               "realip_header_port": realip_header_port_case, "realip_proxy_protocol": realip_proxy_protocol_case}
+               "realip_header_port": realip_header_port_case, "realip_proxy_protocol": realip_proxy_protocol_case,
+               "realip_proxy_port": proxy_port_case}

@@ -201,3 +201,30 @@ def test_large_upstreams_round_robin_fallback(torch_dev):
     hid = names.index(peers.upstream_name(0))
     sel = (up == hid) & (v["action"] == 0)
     assert (got[sel] == engine.GM_PEER_DEFER).any() and (got[sel] < g.n_peers).any()
+
+
+def test_sticky_cookie_parity(torch_dev):
+    """NGINX Plus `sticky cookie` on the GPU (nginx-plus.ingress.tmpl:9-11,
+    annotations.go:387-399): round robin, least_conn and random two least_conn upstreams with a
+    srv_<k> cookie naming a peer by the hex MD5 of its address -- present, naming a down peer,
+    stale, malformed, another upstream's, absent -- every pick and the whole state equal the
+    oracle's over two batches with peers going down between them.  Parity unpinned (no Plus)."""
+    torch, dev = torch_dev
+    b = peers.sticky_blob()
+    g = Gpu(torch, dev, b)
+    o = Oracle(b, 1)
+    bal = Balancer(o)
+    assert g.n_peers == bal.n_peers and g.e.stats()["n_upstreams_deferred"] == 0
+    for k, down in enumerate([(), (1, 4, 9)]):
+        st = bal.state.copy()
+        st["flags"][:] = 0
+        st["flags"][list(down)] = 1
+        bal.state[:] = st
+        g.set_state(st)
+        reqs, arena = peers.sticky_requests(60_000, seed=records.SEED_BASE + 300 + k)
+        v, got = g.match_select(reqs, arena)
+        ev, _ = o.match(reqs, arena)
+        assert np.array_equal(v, ev)
+        exp = bal.select(reqs, arena, ev)
+        _check(f"sticky batch {k}", got, exp, g.state_np(), bal.state)
+    assert (got < g.n_peers).sum() > 40_000

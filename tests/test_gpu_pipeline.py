@@ -221,11 +221,12 @@ def test_void_batch_commits_no_counters(torch_dev):
 
 
 @pytest.mark.parametrize("host", [True, False])
-def test_set_overflow_reruns_whole_batch(torch_dev, host):
-    """a dedupe-set overflow (OV_SET: more unique hits + regex jobs than the set holds --
-    an attack burst) no longer voids the batch.  With the set shrunk (GM_CREATE_SET_SHIFT) the first
-    run overflows it; gm_sync re-runs the batch with the set doubled until it fits and returns GM_OK:
-    verdicts and hits equal the oracle's, and the counters hold exactly one batch."""
+def test_set_overflow_continuation(torch_dev, host):
+    """a dedupe-set overflow (OV_SET: more unique hits + regex jobs than the set holds
+    -- an attack burst) neither voids the batch nor re-runs it whole.  With the set shrunk
+    (GM_CREATE_SET_SHIFT) the first pass overflows it; gm_sync redoes only the requests whose
+    inserts were refused, as a sub-batch with a set twice as large, and returns GM_OK: verdicts and
+    hits equal the oracle's, and the counters hold exactly one batch."""
     torch, dev = torch_dev
     ss, b = workloads.c4_stress_generation()
     reqs, arena = records.gen_c4(6_000, ss, seed=workloads.C4_STRESS_POOL_SEED + 9, plant_rate=0.3, stress=True)
@@ -337,3 +338,123 @@ def test_stress_first_batch_default_sizing(torch_dev):
         outs.append((d_out.cpu().numpy(), d_hits[:tot].cpu().numpy()))
     assert ovs[0] & (OV_CAND | OV_SURV), f"first batch did not overflow ({ovs[0]:#x}): the test lost its point"
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+def _set_shift_for(b, reqs, arena, slots_log2):
+    """The GM_CREATE_SET_SHIFT that puts the default set (2^slots_log2 slots) below the batch's keys
+    but within reach of the continuation's doubling."""
+    probe = engine.Engine(0)
+    probe.load(b, 5)
+    probe.match_host(reqs, arena)
+    st = probe.stats()
+    keys = st["last_pairs"] + st["last_jobs"]
+    probe.close()
+    shift = 1
+    while (1 << slots_log2) >> (shift + 1) >= keys // 2 and shift < 14:
+        shift += 1
+    return shift, keys
+
+
+def test_set_overflow_continuation_cost(torch_dev):
+    """The continuation's cost: a 200k-request stress batch whose set overflows completes in
+    gm_sync in under 2x the time of the same batch on a context whose set fits (the sub-batch holds
+    only the requests with a refused insert), with the same verdicts and hits, and one batch's
+    counters.  Both are a fresh stream's first batch of this traffic (so both grow their candidate
+    buffers on the device's continuation path), after a warm-up batch of the same shape without
+    hits (buffers allocated)."""
+    import time
+    torch, dev = torch_dev
+    ss, b = workloads.c4_stress_generation()
+    reqs, arena = records.gen_c4(200_000, ss, seed=workloads.C4_STRESS_POOL_SEED + 11, stress=True, pool_mb=8)
+    n = len(reqs)
+    d_reqs, d_arena = _to_dev(torch, dev, reqs, arena)
+    zero = torch.zeros_like(d_arena)
+    cap = 8 * n + (1 << 16)
+    # default set for 200k requests: 2 * (3 * 200k + 131072) -> 2^21 slots
+    shift, keys = _set_shift_for(b, reqs, arena, 21)
+
+    def first_batch(set_shift):
+        e = engine.Engine(0, set_shift=set_shift)
+        e.load(b, 5)
+        d_out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+        d_hits = torch.zeros(cap, dtype=torch.int32, device=dev)
+        e.match_ptr(d_reqs.data_ptr(), zero.data_ptr(), len(arena), n, d_out.data_ptr(), d_hits.data_ptr(), cap, 0)
+        e.sync(0)
+        base = e.counters()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), len(arena), n, d_out.data_ptr(), d_hits.data_ptr(), cap, 0)
+        e.sync(0)
+        t = time.perf_counter() - t0
+        st = e.stats()
+        v = d_out.cpu().numpy().view(records.VERDICT_DTYPE).copy()
+        h = d_hits[:st["last_hits"]].cpu().numpy().view(np.uint32).copy()
+        ctr = e.counters() - base
+        e.close()
+        return v, h, ctr, t, st
+
+    clean = [first_batch(0) for _ in range(3)]
+    ref_v, ref_h, ref_c = clean[0][0], clean[0][1], clean[0][2]
+    assert all(c[4]["n_set_reruns"] == 0 for c in clean)
+    ov = [first_batch(shift) for _ in range(3)]
+    for v, h, ctr, t, st in ov:
+        assert st["n_set_reruns"] >= 1, (shift, keys, st["n_set_reruns"])
+        assert_verdicts_equal(v, ref_v, h, ref_h, f"continuation vs clean (shift {shift})")
+        assert np.array_equal(ctr, ref_c)
+    t_clean, t_ov = min(c[3] for c in clean), min(o[3] for o in ov)
+    redo = [o[4]["last_redo"] for o in ov]
+    print(f"continuation: {t_ov * 1e3:.2f} ms vs clean {t_clean * 1e3:.2f} ms; keys {keys}, set shift {shift}, "
+          f"requests redone {redo} of {n}")
+    assert t_ov < 2 * t_clean, (t_ov, t_clean, shift, keys, redo)
+
+
+def test_two_batches_before_one_sync(torch_dev):
+    """several batches queued on one stream before gm_sync.  An earlier batch's overflow
+    is not lost when a later batch starts: its dedupe-set overflow is completed (re-run whole, its
+    scratch being reused), and its hit_cap overflow is reported by the sync, with its counters not
+    committed while the clean batch's are."""
+    torch, dev = torch_dev
+    ss, b = workloads.c4_stress_generation()
+    ra, aa = records.gen_c4(6_000, ss, seed=workloads.C4_STRESS_POOL_SEED + 9, plant_rate=0.3, stress=True)
+    rb, ab = records.gen_c4(4_000, ss, seed=workloads.C4_STRESS_POOL_SEED + 13, plant_rate=0.1, stress=True)
+    exp_a, eh_a = Oracle(b, 5).match(ra, aa)
+    exp_b, eh_b = Oracle(b, 5).match(rb, ab)
+    shift, _ = _set_shift_for(b, ra, aa, 19)
+
+    def enqueue(e, reqs, arena, cap):
+        d_reqs, d_arena = _to_dev(torch, dev, reqs, arena)
+        d_out = torch.empty(len(reqs) * 32, dtype=torch.uint8, device=dev)
+        d_hits = torch.zeros(max(cap, 1), dtype=torch.int32, device=dev)
+        e.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), len(arena), len(reqs), d_out.data_ptr(), d_hits.data_ptr(),
+                    cap, 0)
+        return d_reqs, d_arena, d_out, d_hits
+
+    def read(bufs, n_hits_total):
+        v = bufs[2].cpu().numpy().view(records.VERDICT_DTYPE)
+        return v, bufs[3][:n_hits_total].cpu().numpy().view(np.uint32)
+
+    # A overflows its set, B is clean: one sync completes both
+    e = engine.Engine(0, set_shift=shift)
+    e.load(b, 5)
+    A = enqueue(e, ra, aa, 8 * len(ra) + 1024)
+    B = enqueue(e, rb, ab, 8 * len(rb) + 1024)
+    e.sync(0)
+    assert e.stats()["n_set_reruns"] >= 1
+    got_a, gh_a = read(A, int(len(eh_a)))
+    got_b, gh_b = read(B, int(len(eh_b)))
+    assert_verdicts_equal(got_a, exp_a, gh_a, eh_a, "queued batch A (set overflow)")
+    assert_verdicts_equal(got_b, exp_b, gh_b, eh_b, "queued batch B")
+    assert np.array_equal(e.counters(), _one_batch_counters(e, got_a, gh_a) + _one_batch_counters(e, got_b, gh_b))
+    e.close()
+    # A overflows hit_cap, B is clean: the sync reports the overflow; only B is counted
+    e = engine.Engine(0)
+    e.load(b, 5)
+    A = enqueue(e, ra, aa, 10)
+    B = enqueue(e, rb, ab, 8 * len(rb) + 1024)
+    with pytest.raises(engine.GmError) as ei:
+        e.sync(0)
+    assert ei.value.code == engine.GM_E_OVERFLOW
+    got_b, gh_b = read(B, int(len(eh_b)))
+    assert_verdicts_equal(got_b, exp_b, gh_b, eh_b, "queued batch B after a void A")
+    assert np.array_equal(e.counters(), _one_batch_counters(e, got_b, gh_b))
+    e.close()

@@ -55,7 +55,7 @@ def test_gpu_parse_arena_overflow(env):
 
 def _fields(reqs, arena):
     out = {}
-    for f in records.FIELDS:
+    for f in records.WIRE_FIELDS:
         out[f] = b"".join(records.field_bytes(reqs, arena, i, f) for i in range(len(reqs)))
     return out
 
@@ -73,18 +73,18 @@ def test_gpu_parse_matches_oracle(env):
     alen = int(d_len.item())
     ga = d_a[:alen].cpu().numpy()
     exp, ea = parse_requests(W, M)
-    for f in ("flags", "pad0", "uri_len", "args_len", "hdr_len", "body_len", "host_len", "method_len", "ruri_len",
-              "raddr_len", "port", "remote_port", "rid"):
+    for f in ("flags", "pad0", "pad1", "uri_len", "args_len", "hdr_len", "body_len", "host_len", "method_len",
+              "ruri_len", "raddr_len", "port", "remote_port", "rid"):
         bad = np.nonzero((got[f] != exp[f]).reshape(n, -1).any(axis=1))[0]
         assert len(bad) == 0, (f, int(bad[0]), msgs[int(bad[0])][:120], got[int(bad[0])], exp[int(bad[0])])
     assert (got["base"] % 16 == 0).all() and (np.diff(got["base"].astype(np.int64)) >= 0).all()
     gf, ef = _fields(got, ga), _fields(exp, ea)
-    for f in records.FIELDS:
+    for f in records.WIRE_FIELDS:
         assert gf[f] == ef[f], f
     # the arena between and after the records is zero (slack is cleared: the WAF scan reads it all)
     used = np.zeros(alen, bool)
     for r in got:
-        tot = sum(int(r[records.LEN_FIELD[f]]) for f in records.FIELDS)
+        tot = sum(records.field_len(r, f) for f in records.WIRE_FIELDS)
         used[int(r["base"]):int(r["base"]) + tot] = True
     assert not ga[~used].any()
     assert (got["flags"] & records.REQ_INVALID).sum() > 100
@@ -129,3 +129,87 @@ def test_parse_then_match_chain(env, cfg):
         assert (exp["action"] == 6).sum() > 1000
     else:
         assert (exp["route_kind"] == 3).any() and (exp["match_idx"] != 0xFF).any()
+
+
+def test_gpu_proxy_protocol_parity(env):
+    """PROXY protocol on the GPU: the reference's `basic` VirtualServer fixture
+    (virtualserver_test.go:163-282, ProxyProtocol true) with examples/proxy-protocol's ConfigMap
+    (proxy-protocol True, real-ip-header proxy_protocol, set-real-ip-from 192.168.192.168), plus a
+    rules route on $remote_addr.  gm_parse_requests on PROXY v1 / v2 / broken / keep-alive
+    messages equals the oracle's parse (records, $proxy_protocol_addr bytes), and parse -> match
+    equals the oracle's chain: realip takes the PROXY source address on the trusted balancer's
+    connections only.  Parity unpinned (no nginx in the reference)."""
+    import torch
+    from helpers import golden
+    from gpumatch import blob, confgen
+    from semantics_cases import ADDRS, _rules_vs
+    torch_, dev, e = env
+    case = golden("reference_configs.json")["vs_configs"]["basic"]
+    p = confgen.default_config_params()
+    p.update(case["params"])
+    p = confgen.configmap_params({"proxy-protocol": "True", "real-ip-header": "proxy_protocol",
+                                  "set-real-ip-from": "192.168.192.168"}, p)
+    store = {"%s/%s" % (x["metadata"]["namespace"], x["metadata"]["name"]): x for x in case["vsrs"]}
+    files = confgen.virtual_server_files([case["vs"], _rules_vs("pp.example.com", {"variable": "$remote_addr"}, ADDRS)],
+                                         base=p, vsr_store=store, pem_name="",
+                                         endpoints_of=lambda ns, s_, port: case["endpoints"].get(f"{ns}/{s_}:{port}", []))
+    b = blob.make_blob(confgen.render_main(p), files)
+    orc = Oracle(b, 9)
+    assert sorted(orc.proxy_ports()) == [80, 443]
+    e.load(b, 9)
+    assert e.stats()["n_rejected_other"] == 0, e.rejects()
+    # the KAT messages, then a seeded mix: v1 / v2 headers with ADDRS and random sources, trusted
+    # (the balancer 192.168.192.168) and untrusted peers, keep-alive requests, TLS and plain
+    cases = wire.proxy_cases()
+    msgs, conn = [c[0] for c in cases], [c[1] for c in cases]
+    rng = np.random.Generator(np.random.PCG64(515))
+    for i in range(4000):
+        src = ADDRS[i % 4] if rng.random() < 0.5 else "%d.%d.%d.%d" % tuple(int(x) for x in rng.integers(0, 256, 4))
+        sport = int(rng.integers(0, 65536))
+        host = ["pp.example.com", "cafe.example.com"][int(rng.integers(0, 2))]
+        req = wire.serialize({"uri": ["/", "/tea", "/coffee", "/x"][int(rng.integers(0, 4))], "host": host})
+        https = bool(rng.random() < 0.5)
+        peer = "192.168.192.168" if rng.random() < 0.7 else "10.1.2.3"
+        k = int(rng.integers(0, 10))
+        if k < 4:
+            m = wire.proxy_v1(src, "10.0.0.1", sport, 443 if https else 80) + req
+            c = {}
+        elif k < 8:
+            m = wire.proxy_v2(src, "10.0.0.1", sport, 443 if https else 80) + req
+            c = {}
+        elif k == 8:
+            m = req
+            c = {"proxy_done": True, "paddr": src, "proxy_port": sport}
+        else:
+            m = bytes(wire.proxy_v1(src, "10.0.0.1", sport))[:int(rng.integers(1, 30))] + req   # broken
+            c = {}
+        c.update({"https": https, "port": 443 if https else 80, "raddr": peer})
+        msgs.append(m)
+        conn.append(c)
+    W, M = wire.build(msgs, conn, seed=7)
+    d_w, d_m, d_r, d_a, d_len, cap = _gpu_parse(torch_, dev, e, W, M)
+    n = len(M)
+    d_v = torch_.zeros(n * 32, dtype=torch_.uint8, device=dev)
+    d_h = torch_.zeros(4 * n + 1024, dtype=torch_.int32, device=dev)
+    e.match_ptr(d_r.data_ptr(), d_a.data_ptr(), cap, n, d_v.data_ptr(), d_h.data_ptr(), d_h.numel(), 0,
+                arena_len_dev=d_len.data_ptr())
+    e.sync(0)
+    got = d_r[:n * 64].cpu().numpy().view(records.REQ_DTYPE)
+    alen = int(d_len.item())
+    ga = d_a[:alen].cpu().numpy()
+    exp, ea = parse_requests(W, M, proxy_ports=orc.proxy_ports())
+    for f in ("flags", "pad0", "pad1", "uri_len", "args_len", "hdr_len", "body_len", "host_len", "method_len",
+              "ruri_len", "raddr_len", "port", "remote_port"):
+        bad = np.nonzero((got[f] != exp[f]).reshape(n, -1).any(axis=1))[0]
+        assert len(bad) == 0, (f, int(bad[0]), msgs[int(bad[0])][:120], got[int(bad[0])], exp[int(bad[0])])
+    gf, ef = _fields(got, ga), _fields(exp, ea)
+    for f in records.WIRE_FIELDS:
+        assert gf[f] == ef[f], f
+    st = (got["flags"] & records.REQ_INVALID) != 0
+    assert (got["pad0"][:, 0] > 0).sum() > 2000 and st.sum() > 300
+    ev, eh = orc.match(exp, ea)
+    gv = d_v.cpu().numpy().view(records.VERDICT_DTYPE)
+    assert_verdicts_equal(gv, ev, None, None, "PROXY protocol parse -> match")
+    # realip took effect: trusted connections route on the PROXY source
+    pp_rules = (gv["route_kind"] == 3) & (gv["match_idx"] != 0xFF)
+    assert pp_rules.sum() > 300

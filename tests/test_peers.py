@@ -385,3 +385,54 @@ def test_update_upstream_racing_a_load_is_refused(pblob):
         assert [a for a, _ in _addresses(e)].count("10.9.9.9:80") == 1
     finally:
         L.gm_debug_update_hook(None, None)
+
+
+def test_parse_sticky_service_kats():
+    """annotations_test.go:44-62 (parseStickyService): a valid and an invalid declaration."""
+    from gpumatch import confgen
+    assert confgen.parse_sticky_service("serviceName=coffee-svc srv_id expires=1h domain=.example.com path=/") == \
+        ("coffee-svc", "srv_id expires=1h domain=.example.com path=/")
+    with pytest.raises(ValueError):
+        confgen.parse_sticky_service("serviceNamecoffee-svc srv_id expires=1h domain=.example.com path=/")
+
+
+def test_sticky_cookie_compiles_and_oracle_picks():
+    """NGINX Plus `sticky cookie` (nginx-plus.ingress.tmpl:9-11): the compiler keeps the upstreams
+    (none deferred), and the oracle sends a request whose cookie is the hex MD5 (hashlib) of a live
+    peer's address to that peer; a down peer, a stale / uppercase / short value or another
+    upstream's cookie leaves the request to the balancing method.  Parity unpinned (no Plus)."""
+    import hashlib
+    from gpumatch import confgen
+    b = peers.sticky_blob()
+    ings, _ = peers.sticky_ingresses()
+    txt = confgen.ingress_files(ings[:1], endpoints={"svc-080": peers.sticky_endpoints(0)}, is_plus=True)
+    assert "sticky cookie srv_0 expires=1h path=/;" in "".join(txt.values())
+    e = engine.Engine(compile_only=True)
+    e.load(b, 1)
+    st = e.stats()
+    assert st["n_upstreams_deferred"] == 0 and st["n_rejected_other"] == 0, e.rejects()
+    o = Oracle(b, 1)
+    bal = Balancer(o)
+    reqs, arena = peers.sticky_requests(3000)
+    v, _ = o.match(reqs, arena)
+    state = bal.state
+    down = {int(x) for x in np.nonzero(np.arange(len(state)) % 7 == 3)[0]}
+    state["flags"][sorted(down)] = 1
+    picks = bal.select(reqs, arena, v)
+    names = [e.peer_address(j)[0] for j in range(len(state))]
+    hits = 0
+    for i in range(len(reqs)):
+        hd = records.field_bytes(reqs, arena, i, "hdrs").decode()
+        host = records.field_bytes(reqs, arena, i, "host").decode()
+        k = int(host[1])
+        uri = records.field_bytes(reqs, arena, i, "uri").decode()
+        ck = [c.split("=", 1)[1] for c in hd.replace("Cookie: ", "").replace("\r\n", "").split("; ")
+              if c.startswith(f"srv_{k}=")]
+        if uri != "/" or not ck:
+            continue
+        want = [j for j in range(len(state)) if names[j] in peers.sticky_endpoints(k) and
+                hashlib.md5(names[j].encode()).hexdigest() == ck[0] and j not in down]
+        if want:
+            assert picks[i] == want[0], (i, hd, picks[i], want)
+            hits += 1
+    assert hits > 400

@@ -86,3 +86,26 @@ def test_synthetic_mix_statuses():
     assert {400, 501, 505, 414} <= set(st.tolist())
     assert (reqs["body_len"] > 0).sum() > 500
     assert (np.diff(reqs["base"].astype(np.int64)) >= 0).all() and (reqs["base"] % 16 == 0).all()
+
+
+def test_oracle_proxy_protocol_known_answers():
+    """PROXY protocol intake (ngx_proxy_protocol_read, nginx 1.17.3; parity unpinned: nginx is not
+    in the reference) on a listener with proxy_protocol (ports 80, 443; 8080 without): the source
+    address and port of v1 / v2 headers, UNKNOWN / LOCAL / other transports without an address,
+    broken or missing headers closing the connection (444), keep-alive requests carrying the
+    connection's address."""
+    cases = wire.proxy_cases()
+    W, M = wire.build([c[0] for c in cases], [c[1] for c in cases])
+    reqs, arena = parse_requests(W, M, proxy_ports=(80, 443))
+    for i, (_, _, want) in enumerate(cases):
+        r = reqs[i]
+        if isinstance(want, int):
+            assert _status(r) == want, (i, _status(r))
+            assert records.field_bytes(reqs, arena, i, "paddr") == b""
+            continue
+        assert _status(r) == 0, (i, _status(r))
+        assert records.field_bytes(reqs, arena, i, "paddr") == want[0], (i, records.field_bytes(reqs, arena, i, "paddr"))
+        if want[0]:
+            assert records.proxy_port(r) == want[1], (i, records.proxy_port(r))
+        assert records.field_bytes(reqs, arena, i, "uri") == want[2]
+        assert records.field_bytes(reqs, arena, i, "raddr") == bytes(M[i]["raddr"][:M[i]["raddr_len"]])
