@@ -5,8 +5,13 @@ headers / <= 8 KB body), 10M requests per GPU, requests resident in HBM before t
 
 N > 1 is launched by torch.distributed.run (one rank per GPU); requests shard with no data-path
 collective (weak scaling: every rank classifies its own R requests); the per-location and
-per-rule hit counters are all-reduced with RCCL over xGMI once per step (gm_counters_allreduce).
-A "step" = one gm_match_batch + gm_sync over the rank's R requests.  Rank 0 prints one JSON line.
+per-rule hit counters are all-reduced with RCCL over xGMI once per timed interval
+(gm_counters_allreduce, after the last step).
+A "step" = one gm_match_batch + gm_sync over the rank's R requests.  --inflight D (default 2):
+batches are pipelined over D streams -- step k is enqueued on stream k % D and completed by its
+gm_sync when that stream comes round again -- so a batch's tail overlaps the next batch's scan, as
+a server handing the engine consecutive batches would run it; every step is still a whole batch
+with its own verdicts and hits.  Rank 0 prints one JSON line (config.inflight = D).
 """
 
 from __future__ import annotations
@@ -59,6 +64,10 @@ def main():
                          "over the ranks with the hit counters all-reduced (--stream, --batch)")
     ap.add_argument("--stream", type=int, default=100_000_000, help="c5: requests in the whole stream")
     ap.add_argument("--batch", type=int, default=10_000_000, help="c5: requests per gm_match_batch")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="batches in flight: step k runs on stream k %% inflight, and its gm_sync waits until the "
+                         "stream comes round again, so one batch's tail (context filter, exact check, hit "
+                         "emission) overlaps the next batch's route and scan (1: one batch at a time)")
     ap.add_argument("--allow-nondefault-build", action="store_true",
                     help="measure a library built with measurement / tuning macros (gm_stats build_flags != 0); "
                          "the line is then marked \"build\": \"nondefault\" and is not a headline number")
@@ -104,43 +113,68 @@ def main():
         d_arena[k * plen:k * plen + len(parena)].copy_(d_pool)
     del d_pool
     d_reqs = torch.from_numpy(reqs.view(np.uint8).reshape(-1)).to(dev)
-    d_out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    D = max(1, args.inflight)
+    outs = [torch.empty(n * 32, dtype=torch.uint8, device=dev) for _ in range(D)]
+    d_out = outs[0]
     hit_cap = n // 4 + (1 << 20)
-    d_hits = torch.empty(hit_cap, dtype=torch.int32, device=dev)
+    hitss = [torch.empty(hit_cap, dtype=torch.int32, device=dev) for _ in range(D)]
+    d_hits = hitss[0]
     zone_bytes = int(reqs["uri_len"].sum() + reqs["args_len"].sum() + reqs["hdr_len"].sum() + reqs["body_len"].sum())
     alg_bytes_req = workloads.algorithmic_bytes(reqs, "c4")
     torch.cuda.synchronize()
     log(f"[rank {rank}] resident in HBM: arena {arena_len / 1e9:.2f} GB, scanned zones {zone_bytes / 1e9:.2f} GB")
 
     stream = torch.cuda.current_stream()
+    # D streams, each with its own verdict / hit buffers (and, in the library, its own scratch):
+    # batch k goes to stream k % D; its gm_sync runs when the stream comes round again (or at the
+    # end), so the GPU always holds the next batch while one completes
+    streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(D - 1)]
     uid = None
     if world > 1:
         obj = [engine.Engine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(obj[0], world, rank)
+    pending = [False] * D
+    stage = {"scan": [], "route": [], "verify": [], "tail": []}
 
-    def step():
-        eng.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), arena_len, n, d_out.data_ptr(), d_hits.data_ptr(),
-                      hit_cap, stream.cuda_stream)
-        if world > 1:   # job-wide counter totals (out of place: local counters stay cumulative)
+    def complete(j, record):
+        if not pending[j]:
+            return
+        eng.sync(streams[j].cuda_stream)
+        pending[j] = False
+        if record:
+            s = eng.stats()
+            for key in stage:
+                stage[key].append(s["last_ms_" + key])
+
+    def step(k, record=False):
+        j = k % D
+        complete(j, record)
+        eng.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), arena_len, n, outs[j].data_ptr(), hitss[j].data_ptr(),
+                      hit_cap, streams[j].cuda_stream)
+        pending[j] = True
+
+    def drain(record=False):
+        for j in range(D):
+            complete(j, record)
+        if world > 1:   # job-wide counter totals, once per interval (out of place: local counters stay cumulative)
             eng.counters_allreduce(stream.cuda_stream)
-        eng.sync(stream.cuda_stream)
+            eng.sync(stream.cuda_stream)
 
     for w in range(args.warmup):
-        step()
+        step(w)
         log(f"[rank {rank}] warmup {w + 1}/{args.warmup}")
+    drain()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    scan_ms, route_ms, verify_ms, tail_ms = [], [], [], []
     t_start = time.perf_counter()
     for k in range(args.steps):
-        step()
-        s = eng.stats()
-        scan_ms.append(s["last_ms_scan"]); route_ms.append(s["last_ms_route"])
-        verify_ms.append(s["last_ms_verify"]); tail_ms.append(s["last_ms_tail"])
+        step(k, record=True)
+    drain(record=True)
     torch.cuda.synchronize()
+    scan_ms, route_ms, verify_ms, tail_ms = stage["scan"], stage["route"], stage["verify"], stage["tail"]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -180,7 +214,8 @@ def main():
         "data": "synthetic (numpy PCG64 seed 0xC0FFEE+3; 1M-request pool replicated in HBM)",
         "config": {"workload": "C4: 10k-rule WAF signature set (8000 literals + 2000 RE2-subset regexes) over "
                                "URI/args/headers/<=8KB body, cafe Ingress, wallarm_mode block",
-                   "requests_per_gpu": n, "rules": int(st["n_sigs"]), "parallelism": f"dp{world} (request shards)"},
+                   "requests_per_gpu": n, "rules": int(st["n_sigs"]), "parallelism": f"dp{world} (request shards)",
+                   "inflight": D},
         "scanned_GBps": (alg_bytes_req + 4 * int(s["last_hits"])) * world * args.steps / elapsed / 1e9,
         "hbm_frac_pipeline": (alg_bytes_req + 4 * int(s["last_hits"])) * world * args.steps / elapsed / 1e9
                              / HBM_PEAK_GBPS,

@@ -60,6 +60,9 @@ extern "C" {
 /* test hook: the WAF dedupe set at 2^-k of its default capacity too (bits 16..23), so a batch
  * overflows it (OV_SET) and gm_sync's re-run with the set doubled is exercised */
 #define GM_CREATE_SET_SHIFT(k) (((uint32_t)(k) & 0xFFu) << 16)
+/* test hook: the spill of the pairs a full set refuses at 2^-k of its capacity (bits 24..31), so that
+ * it overflows too and gm_sync's continuation redoes the requests it missed */
+#define GM_CREATE_SPILL_SHIFT(k) (((uint32_t)(k) & 0xFFu) << 24)
 
 /* ---------------------------------------------------------------- packed request record
  * One 64-byte header per request; payload bytes live in one byte arena.  The payload of a
@@ -234,9 +237,13 @@ typedef struct gm_stats_t {
     uint32_t set_shift;          /* GM_CREATE_SET_SHIFT in effect (0 normally) */
     /* always-run union members: one per distinct (pattern, nocase) among the always-run regexes */
     uint32_t n_alw_members;
-    /* the last dedupe-set continuation (gm_sync): requests redone, of the batch's */
+    /* the last dedupe-set continuation (gm_sync): requests redone (a sub-batch of their zones), and
+     * pairs the full set refused that the spill held (emitted from it with no stage re-run) */
     uint32_t last_redo;
-    uint32_t reserved_stats[1];
+    uint32_t last_spill;
+    /* of n_rsl_slices: anchored slices run only over the requests their head map admits (the
+     * first two $uri bytes) */
+    uint32_t n_rsl_heads;
 } gm_stats_t;
 
 /* gm_stats_t.build_flags: measurement / test variants compiled into the library.  bench.py refuses

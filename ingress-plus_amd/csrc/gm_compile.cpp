@@ -1355,6 +1355,27 @@ static void put_md5(std::vector<uint32_t> &v, const std::string &addr) {
     v.insert(v.end(), d, d + 4);
 }
 
+
+// The heads of an anchored DFA (state 1 = start, 0 = dead; acc bit0 match, bit1 match at the
+// subject's end): bit b1 << 8 | b2 of `bits` (RSL_HEAD_WORDS u32) for every two-byte start b1 b2 of
+// a subject it can match (b2 = 0 stands for a one-byte subject, and key 0 for the empty one: a
+// $uri with a NUL in its first two bytes joins every list, k_rloc_heads); a DFA that matches at its start state sets every bit.  A final '\n' may
+// satisfy a `$` (PCRE), so an end-accepting state after b1 also sets b1 '\n'.
+static void dfa_heads(const Dfa &d, std::vector<uint32_t> &bits) {
+    auto set = [&](uint32_t key) { bits[key >> 5] |= 1u << (key & 31); };
+    auto step = [&](uint32_t st, int b) { return (uint32_t)(d.trans[(size_t)st * d.n_classes + d.cls[b]] & DFA_TRANS_STATE_MASK); };
+    if (d.n_states < 2 || (d.acc[1] & 1)) { std::fill(bits.begin(), bits.end(), 0xFFFFFFFFu); return; }
+    if (d.acc[1] & 2) { set(0); set((uint32_t)'\n' << 8); }
+    for (int b1 = 1; b1 < 256; b1++) {
+        const uint32_t s1 = step(1, b1);
+        if (!s1) continue;
+        if (d.acc[s1] & 1) { for (int b2 = 0; b2 < 256; b2++) set((uint32_t)b1 << 8 | b2); continue; }
+        if (d.acc[s1] & 2) { set((uint32_t)b1 << 8); set((uint32_t)b1 << 8 | '\n'); }
+        for (int b2 = 1; b2 < 256; b2++)
+            if (step(s1, b2)) set((uint32_t)b1 << 8 | b2);
+    }
+}
+
 CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) {
     CompileResult R;
     gm_stats_t &st = R.stats;
@@ -1585,6 +1606,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     std::vector<DRegexLoc> rlocs;
     std::vector<std::vector<std::string>> rloc_factors;   // parallel to rlocs: >= 4-byte factors
     std::vector<uint8_t> rsl_pbit;   // parallel to rlocs (filled below): k_rloc_pref's mask bit, 0xFF none
+    std::vector<uint32_t> rsl_heads; // anchored slices' head maps (ALW_SLICE_HEADS), RSL_HEAD_WORDS each
+    std::vector<uint32_t> rsl_head_slice;   // and each map's slice
     // parallel to rlocs: the DFA of ^(\n)?rev(X) for an unanchored X$ (n_states 0: none) --
     // union-DFA slices of these run backwards from the URI's end (gm_regex.hpp
     // compile_regex_reversed) and die within a few bytes, where the forward search reads it all
@@ -2227,14 +2250,29 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             // matches they find let the costly ones skip requests; within a kind, config order
             std::vector<uint32_t> ord_a, ord_un, ord_uf, ord_r;
             std::vector<const Dfa *> rcomps(D.n_rloc, nullptr);
+            std::vector<std::vector<uint32_t>> heads(D.n_rloc);
             for (uint32_t k = 0; k < D.n_rloc; k++) {
                 const Dfa &rv = rloc_rev[D.first_rloc + k];
                 if (rv.n_states > 0) { rcomps[k] = &rv; ord_r.push_back(k); }
-                else if (comps[k]->anchored_start) ord_a.push_back(k);
+                else if (comps[k]->anchored_start) {
+                    ord_a.push_back(k);
+                    heads[k].assign(RSL_HEAD_WORDS, 0u);
+                    dfa_heads(*comps[k], heads[k]);
+                }
                 else if (rlocs[D.first_rloc + k].dfa != GM_NONE && !rloc_factors[D.first_rloc + k].empty())
                     ord_uf.push_back(k);
                 else ord_un.push_back(k);
             }
+            // anchored regexes by their lowest head (config order among equal ones): a group then
+            // holds regexes that start alike, so each anchored slice's head map is narrow and a
+            // $uri's first two bytes pick few slices (the first match in config order is the
+            // lowest index any slice finds, whatever the slices' order)
+            auto head0 = [&](uint32_t k) {
+                for (uint32_t w = 0; w < RSL_HEAD_WORDS; w++)
+                    if (heads[k][w]) return w * 32 + (uint32_t)__builtin_ctz(heads[k][w]);
+                return 0xFFFFFFFFu;
+            };
+            std::stable_sort(ord_a.begin(), ord_a.end(), [&](uint32_t a, uint32_t b) { return head0(a) < head0(b); });
             std::vector<std::vector<uint32_t>> gm_a, gm_un, gm_uf, gm_r;
             std::vector<MultiDfa> gd_a, gd_un, gd_uf, gd_r;
             std::vector<uint32_t> single;
@@ -2255,12 +2293,36 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 return (uint32_t)(alw_slices.size() - s0);
             };
             st.n_rsl_reversed += pack_kind(gm_r, gd_r, ALW_SLICE_REVERSED);
+            const size_t a0 = alw_slices.size();
             pack_kind(gm_a, gd_a, 0);
+            // each anchored slice's head map: the OR of its members'
+            for (size_t k = a0; k < alw_slices.size(); k++) {
+                const uint32_t slot = (uint32_t)(rsl_heads.size() / RSL_HEAD_WORDS);
+                if (slot >= RSL_HEADS_MAX) break;
+                rsl_heads.resize(rsl_heads.size() + RSL_HEAD_WORDS, 0u);
+                uint32_t *hb = rsl_heads.data() + (size_t)slot * RSL_HEAD_WORDS;
+                const DAlwSlice &sl = alw_slices[k];
+                for (uint32_t g = sl.first_group; g < sl.first_group + sl.n_groups; g++)
+                    for (uint32_t q = 0; q < (uint32_t)__builtin_popcount(alw[g].zone_mask[0]); q++) {
+                        const uint32_t m = alw_rule[alw[g].first + q] - fr;
+                        for (uint32_t w = 0; w < RSL_HEAD_WORDS; w++) hb[w] |= heads[m][w];
+                    }
+                alw_slices[k].flags |= ALW_SLICE_HEADS | slot << 16;
+                rsl_head_slice.push_back((uint32_t)k);
+            }
             pack_kind(gm_un, gd_un, 0);
             pack_kind(gm_uf, gd_uf, 0);
             D.rsl_n = (uint32_t)alw_slices.size() - D.rsl_first;
-            for (uint32_t k = D.rsl_first; k < D.rsl_first + D.rsl_n; k++)
-                alw_slices[k].min_member = alw_rule[alw[alw_slices[k].first_group].first];
+            // the lowest regex-location index a slice holds (members of a head-ordered anchored group
+            // are not in config order: the minimum over all of them)
+            for (uint32_t k = D.rsl_first; k < D.rsl_first + D.rsl_n; k++) {
+                const DAlwSlice &sl = alw_slices[k];
+                uint32_t mn = 0xFFFFFFFFu;
+                for (uint32_t g = sl.first_group; g < sl.first_group + sl.n_groups; g++)
+                    for (uint32_t q = 0; q < (uint32_t)__builtin_popcount(alw[g].zone_mask[0]); q++)
+                        mn = std::min(mn, alw_rule[alw[g].first + q]);
+                alw_slices[k].min_member = mn;
+            }
             st.n_rsl_slices += D.rsl_n;
             // forward slices of unanchored regexes that all have >= 4-byte factors run only for
             // the requests whose $uri holds a factor of one of them: k_rloc_pref sets bit
@@ -2316,6 +2378,12 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_lit_chk = I.put(dchk);
     rsl_pbit.resize((rsl_pbit.size() + 3) & ~size_t(3), 0xFF);
     h.off_rsl_pbit = I.put(rsl_pbit);
+    if (rsl_heads.empty()) rsl_heads.assign(1, 0u);
+    h.n_rsl_heads = (uint32_t)(rsl_heads.size() / RSL_HEAD_WORDS);
+    st.n_rsl_heads = (uint32_t)rsl_head_slice.size();
+    h.off_rsl_heads = I.put(rsl_heads);
+    rsl_head_slice.resize(std::max<size_t>(rsl_head_slice.size(), 1), 0u);
+    h.off_rsl_head_slice = I.put(rsl_head_slice);
     // (before the upstream section: gm_update_upstream copies everything before it unchanged)
     h.n_realip = (uint32_t)realips.size(); h.n_cidrs = (uint32_t)cidrs.size();
     st.n_realip = h.n_realip;
@@ -2504,6 +2572,9 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.alw_rl = (const uint32_t *)(b + h.off_alw_rl);
     t.lit_chk = (const DLitChk *)(b + h.off_lit_chk);
     t.rsl_pbit = b + h.off_rsl_pbit;
+    t.rsl_heads = (const uint32_t *)(b + h.off_rsl_heads);
+    t.n_rsl_heads = h.n_rsl_heads;
+    t.rsl_head_slice = (const uint32_t *)(b + h.off_rsl_head_slice);
     t.realip = (const DRealIp *)(b + h.off_realip);
     t.cidrs = (const DCidr *)(b + h.off_cidrs);
     t.n_always_lds = h.n_always_lds; t.n_alw_groups = h.n_alw_groups; t.n_alw_slices = h.n_alw_slices;

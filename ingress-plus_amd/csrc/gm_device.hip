@@ -1463,6 +1463,8 @@ struct Scratch {
     uint4 *d_rqu = nullptr; size_t cap_rqu = 0;          // and its $uri's first 32 bytes (+ a pad block)
     int32_t *d_rqb = nullptr; size_t cap_rqb = 0;        // and its longest prefix match (the tail pass)
     unsigned long long *d_rqm = nullptr; size_t cap_rqm = 0;   // and its prefiltered-slice mask
+    uint32_t *d_hlist = nullptr; size_t cap_hlist = 0;         // the anchored slices' candidate lists
+    uint32_t *d_hcnt = nullptr; size_t cap_hcnt = 0;           // and their lengths (k_rloc_heads)
     unsigned long long *d_bctr = nullptr; size_t cap_bctr = 0; // this batch's counters (k_ctr_commit)
     uint2 *d_slow = nullptr; size_t cap_slow = 0;              // requests for k_route's SLOW pass
     unsigned long long *d_agree = nullptr, *h_agree = nullptr;  // gm_counters_allreduce's agreement words
@@ -1476,6 +1478,8 @@ struct Scratch {
     gm_verdict *d_rsout = nullptr; size_t cap_rsout = 0;
     uint32_t *d_rsblk = nullptr; size_t cap_rsblk = 0;
     uint32_t *d_rscnt = nullptr; size_t cap_rscnt = 0;
+    // the pairs a full dedupe set refused (Dedup::spill) and their sorted copy
+    unsigned long long *d_spill = nullptr, *d_spill2 = nullptr; size_t cap_spill = 0, cap_spill2 = 0;
     // each pending batch's final overflow bits (k_ctr_commit), one word per batch since the last
     // gm_sync: later batches do not clear an earlier one's
     uint32_t *d_ovlog = nullptr, *h_ovlog = nullptr;
@@ -1499,7 +1503,8 @@ struct Scratch {
                         (void *)d_usize, (void *)d_utemp, (void *)d_sreqs, (void *)d_sarena, (void *)d_sblk,
                         (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm, (void *)d_rqu, (void *)d_bctr, (void *)d_slow,
                         (void *)d_redo, (void *)d_rlist, (void *)d_rsize, (void *)d_rbase, (void *)d_rtemp, (void *)d_rsreq,
-                        (void *)d_rsarena, (void *)d_rsout, (void *)d_rsblk, (void *)d_rscnt, (void *)d_ovlog, (void *)d_wmsg})
+                        (void *)d_rsarena, (void *)d_rsout, (void *)d_rsblk, (void *)d_rscnt, (void *)d_ovlog, (void *)d_wmsg, (void *)d_spill, (void *)d_spill2,
+                        (void *)d_hlist, (void *)d_hcnt})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
         if (h_ovlog) (void)hipHostFree(h_ovlog);
@@ -1520,8 +1525,10 @@ struct gm_ctx {
     int cu_count = 256;
     double cap_scale = 1.0;                   // GM_CREATE_SCRATCH_SHIFT (test hook): internal WAF capacities
     uint32_t set_shift = 0;                   // GM_CREATE_SET_SHIFT (test hook): the dedupe set
+    uint32_t spill_shift = 0;                 // GM_CREATE_SPILL_SHIFT (test hook): the refused pairs' spill
     std::atomic<uint32_t> n_set_reruns{0};    // gm_sync re-runs of OV_SET batches
     std::atomic<uint32_t> last_redo{0};       // requests the last continuation redid
+    std::atomic<uint32_t> last_spill{0};      // pairs the last spill continuation emitted from the spill
     std::shared_mutex gen_mu;                 // shared: enqueueing batches; exclusive: the swap
     Generation *gen = nullptr;
     uint64_t publish_seq = 0;                 // bumped under gen_mu (exclusive) by every publish
@@ -1654,6 +1661,7 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
     c->flags = flags;
     if (const uint32_t k = (flags >> 8) & 0xFFu) c->cap_scale = k < 32 ? 1.0 / (double)(1ull << k) : 1.0;
     if (const uint32_t k = (flags >> 16) & 0xFFu) c->set_shift = k < 24 ? k : 0;
+    if (const uint32_t k = (flags >> 24) & 0xFFu) c->spill_shift = k < 24 ? k : 0;
     if (!(flags & GM_CREATE_COMPILE_ONLY)) {
         if (hipSetDevice(hip_device) != hipSuccess) { t_err = "hipSetDevice failed"; delete c; return nullptr; }
         // the WAF scan's Bloom filter is dynamic LDS beyond the 64 KiB default
@@ -1677,6 +1685,10 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ALWAYS_LDS_BYTES) != hipSuccess) {
                 t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
             }
+        if (hipFuncSetAttribute((const void *)k_rloc_heads, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(HEADS_LDS_SLOTS * RSL_HEAD_WORDS * 4)) != hipSuccess) {
+            t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
+        }
         if (hipFuncSetAttribute((const void *)k_rloc_pref, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)RLOC_PREF_LDS) != hipSuccess) {
             t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
@@ -1821,6 +1833,7 @@ int gm_stats(gm_ctx *c, gm_stats_t *out) {
     out->scratch_scale = (float)c->cap_scale;
     out->n_set_reruns = c->n_set_reruns.load();
     out->last_redo = c->last_redo.load();
+    out->last_spill = c->last_spill.load();
     out->set_shift = c->set_shift;
     std::lock_guard<std::mutex> l2(c->last_mu);
     out->last_candidates = c->last_candidates;
@@ -1942,6 +1955,7 @@ static int waf_buffers(gm_ctx *c, Scratch *S, uint64_t alen, uint32_t n, WafCaps
     if ((e = grow(c, s, S->d_surv, S->cap_surv, std::min<size_t>(scaled((alen / 256 + 65536) * S->surv_mult, k.scan_blocks),
                                                                  0xFFFFFFFFu)))) return e;
     if ((e = grow_keep(c, s, S->d_pairs, S->cap_pairs, pcap, keep_pairs))) return e;
+    if ((e = grow(c, s, S->d_spill, S->cap_spill, pcap))) return e;
     if ((e = grow(c, s, S->d_jobs, S->cap_jobs, jcap))) return e;
     if ((e = grow(c, s, S->d_cnt, S->cap_cnt, (size_t)n + 1))) return e;
     if ((e = grow(c, s, S->d_start, S->cap_start, (size_t)n + 1))) return e;
@@ -2084,7 +2098,7 @@ static int waf_stages(gm_ctx *c, Scratch *S, const Generation *g, const WafCaps 
 // k_hits_scatter)
 static int emit_hits(gm_ctx *c, Scratch *S, const Generation *g, uint32_t n, gm_verdict *out, uint32_t *hit_ids,
                      size_t hit_cap, unsigned long long *ctr, const Dedup &dd, const uint32_t *redo, uint32_t np1,
-                     const uint32_t *remap) {
+                     const uint32_t *remap, const unsigned long long *spill = nullptr, uint32_t nspill = 0) {
     hipStream_t s = S->stream;
     size_t scan_tmp = 0;
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
@@ -2092,7 +2106,7 @@ static int emit_hits(gm_ctx *c, Scratch *S, const Generation *g, uint32_t n, gm_
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_temp, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
     k_hits_scatter<<<(uint32_t)c->cu_count * 4, 256, 0, s>>>(S->d_pairs, (uint32_t)S->cap_pairs, S->d_cnt, S->d_start,
                                                               hit_ids, hit_cap, ctr, g->tab.n_locs, S->d_status, dd,
-                                                              redo, np1, remap);
+                                                              redo, np1, remap, spill, nspill);
     HIPCHK(c, hipGetLastError());
     k_hits_finalize<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8)), 256, 0, s>>>(
         S->d_start, n, out, hit_ids, hit_cap, S->d_status);
@@ -2164,17 +2178,35 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
                 pm = S->d_rqm;
             }
             const DAlwSlice *sls = reinterpret_cast<const DAlwSlice *>(g->host_image.data() + g->hdr.off_alw_slices);
+            // the anchored slices' candidate lists (k_rloc_heads): each such slice runs over its list
+            const uint32_t nh = g->hdr.n_rsl_heads;
+            if (nh) {
+                int e5;
+                if ((e5 = grow(c, rs, S->d_hlist, S->cap_hlist, (size_t)nh * n)) ||
+                    (e5 = grow(c, rs, S->d_hcnt, S->cap_hcnt, (size_t)RSL_HEADS_MAX))) return e5;
+                HIPCHK(c, hipMemsetAsync(S->d_hcnt, 0, (size_t)nh * 4, rs));
+                for (uint32_t h0 = 0; h0 < nh; h0 += HEADS_LDS_SLOTS) {
+                    const uint32_t k = std::min<uint32_t>(HEADS_LDS_SLOTS, nh - h0);
+                    k_rloc_heads<<<(uint32_t)c->cu_count, 1024, k * RSL_HEAD_WORDS * 4, rs>>>(
+                        t, q.st, q.u, q.count, t.rsl_head_slice, h0, k, S->d_hlist, n, S->d_hcnt);
+                    HIPCHK(c, hipGetLastError());
+                }
+            }
             for (uint32_t k = t.n_alw_slices; k < t.n_alw_slices + t.n_rsl; k++) {
                 const dim3 grid((uint32_t)c->cu_count), blk(1024);
+                const bool hl = nh && (sls[k].flags & ALW_SLICE_HEADS);
+                const uint32_t slot = (sls[k].flags >> 16) & 0xFFu;
+                const uint32_t *L = hl ? S->d_hlist + (size_t)slot * n : nullptr;
+                const uint32_t *LC = hl ? S->d_hcnt + slot : nullptr;
                 switch (sls[k].n_groups) {
-                case 1: k_rloc_multi<1><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
-                case 2: k_rloc_multi<2><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
-                case 3: k_rloc_multi<3><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
-                case 4: k_rloc_multi<4><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
-                case 5: k_rloc_multi<5><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
-                case 6: k_rloc_multi<6><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
-                case 7: k_rloc_multi<7><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
-                default: k_rloc_multi<8><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm); break;
+                case 1: k_rloc_multi<1><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm, L, LC); break;
+                case 2: k_rloc_multi<2><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm, L, LC); break;
+                case 3: k_rloc_multi<3><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm, L, LC); break;
+                case 4: k_rloc_multi<4><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm, L, LC); break;
+                case 5: k_rloc_multi<5><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm, L, LC); break;
+                case 6: k_rloc_multi<6><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm, L, LC); break;
+                case 7: k_rloc_multi<7><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm, L, LC); break;
+                default: k_rloc_multi<8><<<grid, blk, sls[k].len, rs>>>(A, alen, t, q.st, q.u, q.count, q.loc, dlen, k, pm, L, LC); break;
                 }
                 HIPCHK(c, hipGetLastError());
             }
@@ -2212,7 +2244,9 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     HIPCHK(c, hipMemsetAsync(S->d_redo, 0, (((size_t)n + 31) / 32) * 4, s));
     // one epoch per batch (two with decoders: the decoded pass's jobs take epoch + 1)
     if ((e = next_epoch(c, S, t))) return e;
-    Dedup dd{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, out, S->d_cnt, S->d_status, S->d_redo};
+    const size_t spill_cap = c->spill_shift ? std::max<size_t>(S->cap_spill >> c->spill_shift, 16) : S->cap_spill;
+    Dedup dd{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, out, S->d_cnt, S->d_status, S->d_redo,
+             S->d_spill, (uint32_t)std::min<size_t>(spill_cap, 0xFFFFFFFFu)};
 
     // ---- fork: k_route on the side stream, beside the WAF scan (independent inputs; its waves
     // fit beside the scan's one workgroup per CU; issued after the scan so the scan claims the
@@ -2319,8 +2353,63 @@ static int rerun_whole(gm_ctx *c, Scratch *S, const Scratch::Replay &rp0, uint32
         lk.unlock();
         if ((e = read_status(c, S))) return e;
         ov = S->h_ovlog[0];
-        if (!(ov & OV_SET)) return GM_OK;
+        if (!ov_held(ov)) return GM_OK;
     }
+}
+
+// the first nspill spilled pairs sorted into d_spill2 and each distinct one counted for its request
+// (those of a redone request, redo's bits, skipped): out = the sorted array
+static int sort_spill(gm_ctx *c, Scratch *S, uint32_t nspill, const uint32_t *redo, unsigned long long *&out) {
+    hipStream_t s = S->stream;
+    int e;
+    if ((e = grow(c, s, S->d_spill2, S->cap_spill2, (size_t)nspill))) return e;
+    size_t tmp = 0;
+    HIPCHK(c, hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, S->d_spill, S->d_spill2, (int)nspill, 0, 64, s));
+    if ((e = grow(c, s, S->d_rtemp, S->cap_rtemp, tmp))) return e;
+    HIPCHK(c, hipcub::DeviceRadixSort::SortKeys(S->d_rtemp, tmp, S->d_spill, S->d_spill2, (int)nspill, 0, 64, s));
+    k_spill_count<<<std::min<uint32_t>((nspill + 255) / 256, (uint32_t)c->cu_count * 4), 256, 0, s>>>(S->d_spill2, nspill,
+                                                                                                        redo, S->d_cnt);
+    HIPCHK(c, hipGetLastError());
+    out = S->d_spill2;
+    return GM_OK;
+}
+
+// The dedupe set of the stream's last batch refused pairs, and the spill took them all (OV_SET
+// without OV_SPILL; no refused job lost to an overflowing job list): the batch's answer is exact
+// with the spill's distinct pairs added -- sorted, counted, emitted after the pair list.  No WAF
+// stage runs again.
+static int spill_continuation(gm_ctx *c, Scratch *S, const Scratch::Replay &rp, uint32_t &ov, bool &done) {
+    done = false;
+    hipStream_t s = S->stream;
+    std::shared_lock<std::shared_mutex> lk(c->gen_mu);
+    if (c->gen != rp.gen || c->publish_seq != rp.seq)
+        return fail(c, GM_E_OVERFLOW, "WAF dedupe set full and the generation changed before the batch could be "
+                                      "completed: retry it");
+    const Generation *g = c->gen;
+    const uint32_t nspill = (uint32_t)std::min<size_t>(S->h_status[SPILL_WORD], S->cap_spill);
+    int e;
+    DoneGuard G(S);
+    unsigned long long *sp = nullptr;
+    if (nspill && (e = sort_spill(c, S, nspill, nullptr, sp))) return e;
+    k_clear_held<<<1, 64, 0, s>>>(S->d_status);
+    HIPCHK(c, hipGetLastError());
+    const Dedup dd0{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, rp.out, S->d_cnt, S->d_status, nullptr,
+                    nullptr, 0u};
+    if ((e = emit_hits(c, S, g, rp.n, rp.out, rp.hits, rp.hit_cap, S->d_bctr, dd0, nullptr, 0, nullptr, sp, nspill)))
+        return e;
+    const size_t nctr = std::max<size_t>(g->n_counters, 1);
+    k_ctr_commit<<<std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)((nctr + 255) / 256), (uint32_t)c->cu_count)), 256, 0, s>>>(
+        S->d_bctr, g->d_counters, (uint32_t)g->n_counters, S->d_status, S->d_ovlog + rp.slot);
+    HIPCHK(c, hipGetLastError());
+    if ((e = copy_back(c, S, rp))) return e;
+    if ((e = G.done(c))) return e;
+    lk.unlock();
+    if ((e = read_status(c, S))) return e;
+    trace("spill continuation: emitted");
+    c->last_spill = nspill;
+    ov = S->h_ovlog[rp.slot];
+    done = true;
+    return GM_OK;
 }
 
 // The dedupe set of the stream's last batch overflowed (OV_SET): only the requests with a refused
@@ -2341,6 +2430,7 @@ static int set_continuation(gm_ctx *c, Scratch *S, const Scratch::Replay &rp, ui
     const GTab &t = g->tab;
     const uint32_t n = rp.n;
     const uint32_t np1 = S->h_status[1];
+    const uint32_t nspill = (uint32_t)std::min<size_t>(S->h_status[SPILL_WORD], S->cap_spill);
     int e;
     DoneGuard G(S);
     // the requests to redo
@@ -2393,20 +2483,27 @@ static int set_continuation(gm_ctx *c, Scratch *S, const Scratch::Replay &rp, ui
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemsetAsync(S->d_rscnt, 0, ((size_t)m + 1) * 4, s));
         c->n_set_reruns++;
-        const Dedup dd{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, S->d_rsout, S->d_rscnt, S->d_status, nullptr};
+        // (no spill in a redo pass: a refusal there is an overflow, and the pass re-runs larger)
+        const Dedup dd{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, S->d_rsout, S->d_rscnt, S->d_status, nullptr,
+                       nullptr, 0u};
         trace("continuation: sub-batch enqueued");
         if ((e = waf_stages(c, S, g, k, io, dd, std::function<int()>(), false, nomark))) return e;
         if ((e = read_status(c, S))) return e;
         trace("continuation: sub-batch done");
-        const uint32_t ov2 = S->h_status[3];
+        const uint32_t ov2 = S->h_status[3] | S->h_status[PASS1_OV_WORD];
         if (ov2 & (OV_PAIRS | OV_DEC)) { G.armed = false; return mark_done(c, S); }   // whole re-run instead
-        if (!(ov2 & OV_SET)) break;
+        if (!ov_held(ov2)) break;
     }
     // merge: the sub-requests' counts, then the emission over the whole batch and the commit
     k_redo_merge<<<(m + 255) / 256, 256, 0, s>>>(S->d_rlist, m, S->d_rscnt, S->d_cnt);
     HIPCHK(c, hipGetLastError());
-    const Dedup dd0{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, rp.out, S->d_cnt, S->d_status, nullptr};
-    if ((e = emit_hits(c, S, g, n, rp.out, rp.hits, rp.hit_cap, S->d_bctr, dd0, S->d_redo, np1, S->d_rlist))) return e;
+    const Dedup dd0{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, rp.out, S->d_cnt, S->d_status, nullptr,
+                    nullptr, 0u};
+    // the first pass's spilled pairs of the requests not redone
+    unsigned long long *sp = nullptr;
+    if (nspill && (e = sort_spill(c, S, nspill, S->d_redo, sp))) return e;
+    if ((e = emit_hits(c, S, g, n, rp.out, rp.hits, rp.hit_cap, S->d_bctr, dd0, S->d_redo, np1, S->d_rlist, sp,
+                       nspill))) return e;
     const size_t nctr = std::max<size_t>(g->n_counters, 1);
     k_ctr_commit<<<std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)((nctr + 255) / 256), (uint32_t)c->cu_count)), 256, 0, s>>>(
         S->d_bctr, g->d_counters, (uint32_t)g->n_counters, S->d_status, S->d_ovlog + rp.slot);
@@ -2463,9 +2560,15 @@ static int sync_pending(gm_ctx *c, Scratch *S) {
     // the last batch first: its scratch (pairs, counts, redo bits) is still in place
     for (size_t i = pend.size(); i-- > 0;) {
         uint32_t ov = ovs[i];
-        if (ov & OV_SET) {
+        if (ov_held(ov)) {
             bool done = false;
-            if (i + 1 == pend.size() && last_in_place && (e = set_continuation(c, S, pend[i], ov, ov, done))) return e;
+            if (i + 1 == pend.size() && last_in_place) {
+                // refused pairs all in the spill: emitted from it; else the requests whose pairs the
+                // spill missed, or whose refused jobs a full job list lost, are redone
+                const bool redo = (ov & OV_SPILL) || ((ov & OV_JSET) && (ov & OV_JOBS));
+                e = redo ? set_continuation(c, S, pend[i], ov, ov, done) : spill_continuation(c, S, pend[i], ov, done);
+                if (e) return e;
+            }
             if (!done && (e = rerun_whole(c, S, pend[i], ov))) return e;
             if (i + 1 == pend.size()) {
                 std::lock_guard<std::mutex> lk(c->last_mu);
@@ -2479,7 +2582,7 @@ static int sync_pending(gm_ctx *c, Scratch *S) {
     if (err & OV_HITS) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded (the batch's counters were not committed)");
     // candidate / survivor / pair / job overflows were completed on the device (k_waf_direct, the
     // set-based scatter and regex runs): the batch is whole, the buffers grow for speed
-    if (err & OV_SET) return fail(c, GM_E_OVERFLOW, "WAF dedupe set full at its largest size (64x: > ~380 unique hits + "
+    if (ov_held(err)) return fail(c, GM_E_OVERFLOW, "WAF dedupe set full at its largest size (64x: > ~380 unique hits + "
                                                     "regex jobs per request); the batch's counters were not committed");
     if (err & OV_DEC) return fail(c, GM_E_OVERFLOW, "decoded-view arena capacity exceeded");
     return GM_OK;

@@ -334,6 +334,12 @@ constexpr uint32_t ALW_SLICE_REVERSED = 1;
 // a forward slice of unanchored regexes that all have factors: it runs only for requests whose
 // k_rloc_pref mask has bit (flags >> 8) & 63
 constexpr uint32_t ALW_SLICE_PREF = 2;
+// an anchored regex-location slice with a head map (flags >> 16: its slot in rsl_heads): bit
+// b1 << 8 | b2 is set if a member can match a $uri whose first two bytes are b1 b2 (b2 = 0: a
+// one-byte $uri); k_rloc_heads lists each slice's candidate requests, the slice runs only those
+constexpr uint32_t ALW_SLICE_HEADS = 4;
+constexpr uint32_t RSL_HEAD_WORDS = 65536 / 32;
+constexpr uint32_t RSL_HEADS_MAX = 64;
 
 struct TabHeader {
     uint32_t magic, version;
@@ -369,6 +375,9 @@ struct TabHeader {
     uint32_t n_rk_prefilter, pad_rkp;   // rk_on servers left to the factor prefilter (rsl_n 0)
     uint64_t off_alw, off_alw_slices, off_alw_pack, off_alw_rule;
     uint64_t off_rsl_pbit;         // u8 per regex location: its prefiltered slice's mask bit (0xFF none)
+    uint64_t off_rsl_heads;        // anchored regex-location slices: a 65536-bit head map each (RSL_HEAD_WORDS u32)
+    uint64_t off_rsl_head_slice;   // and each map's slice index (u32)
+    uint32_t n_rsl_heads, pad_heads;
     uint32_t n_rk_ents_n, pad_rke; // DRlocEnt entries (k_rloc_pref stages them in LDS)
     uint32_t n_realip, n_cidrs;    // realip configurations and their set_real_ip_from entries
     uint64_t off_realip, off_cidrs;
@@ -402,6 +411,7 @@ struct GTab {                // device pointers, built on host from the image ba
     uint32_t decoders;
     const DAlwGroup *alw; const DAlwSlice *alw_slices; const uint8_t *alw_pack; const uint32_t *alw_rule;
     const uint8_t *rsl_pbit;
+    const uint32_t *rsl_heads; uint32_t n_rsl_heads; const uint32_t *rsl_head_slice;
     const DRealIp *realip; const DCidr *cidrs;
     const uint32_t *alw_rl;
     const DLitChk *lit_chk;

@@ -50,6 +50,10 @@ def GM_CREATE_SET_SHIFT(k: int) -> int:
     return (k & 0xFF) << 16
 
 
+def GM_CREATE_SPILL_SHIFT(k: int) -> int:
+    return (k & 0xFF) << 24
+
+
 def GM_CREATE_SCRATCH_SHIFT(k: int) -> int:
     """Test hook: the internal WAF buffers at 2^-k of their default capacity (include/gpumatch.h)."""
     return (k & 0xFF) << 8
@@ -61,7 +65,8 @@ class GmStats(ctypes.Structure):
                 [(f, ctypes.c_uint32) for f in STATS_FIELDS_WAF] +
                 [("scratch_scale", ctypes.c_float), ("n_set_reruns", ctypes.c_uint32),
                  ("set_shift", ctypes.c_uint32), ("n_alw_members", ctypes.c_uint32),
-                 ("last_redo", ctypes.c_uint32), ("reserved_stats", ctypes.c_uint32 * 1)])
+                 ("last_redo", ctypes.c_uint32), ("last_spill", ctypes.c_uint32),
+                 ("n_rsl_heads", ctypes.c_uint32)])
 
 
 class GmBatch(ctypes.Structure):
@@ -142,11 +147,11 @@ class Engine:
     """One context per HIP device (one process per GPU)."""
 
     def __init__(self, device: int = 0, compile_only: bool = False, profile: bool = False, serial: bool = False,
-                 scratch_shift: int = 0, set_shift: int = 0):
+                 scratch_shift: int = 0, set_shift: int = 0, spill_shift: int = 0):
         L = lib()
         fl = (GM_CREATE_COMPILE_ONLY if compile_only else 0) | (GM_CREATE_PROFILE if profile else 0) | \
              (GM_CREATE_SERIAL if serial else 0) | GM_CREATE_SCRATCH_SHIFT(scratch_shift) | \
-             GM_CREATE_SET_SHIFT(set_shift)
+             GM_CREATE_SET_SHIFT(set_shift) | GM_CREATE_SPILL_SHIFT(spill_shift)
         self.h = L.gm_create(device, fl)
         if not self.h:
             raise GmError(-1, L.gm_last_error(None).decode())
@@ -178,6 +183,8 @@ class Engine:
         d["scratch_scale"] = s.scratch_scale
         d["n_set_reruns"] = s.n_set_reruns
         d["last_redo"] = s.last_redo
+        d["last_spill"] = s.last_spill
+        d["n_rsl_heads"] = s.n_rsl_heads
         d["set_shift"] = s.set_shift
         d["n_alw_members"] = s.n_alw_members
         return d

@@ -96,9 +96,15 @@ def main():
             print("exp counters (steps+warmup)", list(ex), flush=True)
         except (AttributeError, OSError):
             pass
+        # the per-config roofline: SURVEY §8(d)'s algorithmic bytes per request
+        # (workloads.algorithmic_bytes) over the step's wall time and over the route kernel's
+        alg = workloads.algorithmic_bytes(reqs, cfg)
+        roof = {"algorithmic_bytes_per_step": alg, "algorithmic_GBps_step": alg * args.steps / dt / 1e9,
+                "hbm_frac_step": alg * args.steps / dt / 1e9 / 8000.0,
+                "algorithmic_GBps_route": alg / (rt * 1e-3) / 1e9, "hbm_frac_route": alg / (rt * 1e-3) / 1e9 / 8000.0}
         if args.no_cpu:
             print(json.dumps({"config": cfg, "requests": n, "ms_per_step": dt / args.steps * 1e3,
-                              "route_kernel_ms": rt, "value": n * args.steps / dt}), flush=True)
+                              "route_kernel_ms": rt, "value": n * args.steps / dt, **roof}), flush=True)
             del d_arena, d_reqs, d_out, d_hits, d_pool, eng
             continue
         # CPU oracle on a bounded sample of the pool
@@ -108,13 +114,10 @@ def main():
         rate = 500 / (time.perf_counter() - t)
         m = int(min(pool_n, max(500, rate * args.cpu_seconds)))
         t = time.perf_counter(); o.match(preqs[:m], parena, nthreads=cores); cdt = time.perf_counter() - t
-        alg = workloads.algorithmic_bytes(reqs, cfg)
-        rt = float(np.mean(ms))
         print(json.dumps({
             "metric": f"requests/sec ({cfg.upper()})", "value": n * args.steps / dt, "unit": "requests/s",
             "n_gpus": 1, "steps": args.steps, "ms_per_step": dt / args.steps * 1e3,
-            "route_kernel_ms": rt, "config": {"workload": desc, "requests": n, "pool": pool_n},
-            "algorithmic_GBps_route": alg / (rt * 1e-3) / 1e9,
+            "route_kernel_ms": rt, "config": {"workload": desc, "requests": n, "pool": pool_n}, **roof,
             "cpu_baseline": {"value": m / cdt, "unit": "requests/s", "cores": cores, "kind": "port",
                              "sample": f"first {m} requests of the pool ({cdt:.1f}s)"}}), flush=True)
         del d_arena, d_reqs, d_out, d_hits, d_pool, eng

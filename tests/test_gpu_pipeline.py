@@ -220,13 +220,15 @@ def test_void_batch_commits_no_counters(torch_dev):
     assert_verdicts_equal(got, exp, gh, eh, "retry after a void batch")
 
 
-@pytest.mark.parametrize("host", [True, False])
-def test_set_overflow_continuation(torch_dev, host):
+@pytest.mark.parametrize("host,spill", [(True, True), (False, True), (True, False), (False, False)])
+def test_set_overflow_continuation(torch_dev, host, spill):
     """a dedupe-set overflow (OV_SET: more unique hits + regex jobs than the set holds
     -- an attack burst) neither voids the batch nor re-runs it whole.  With the set shrunk
-    (GM_CREATE_SET_SHIFT) the first pass overflows it; gm_sync redoes only the requests whose
-    inserts were refused, as a sub-batch with a set twice as large, and returns GM_OK: verdicts and
-    hits equal the oracle's, and the counters hold exactly one batch."""
+    (GM_CREATE_SET_SHIFT) the first pass overflows it: the pairs it refuses go to the spill, and
+    gm_sync emits each distinct one (spill); with the spill shrunk too (GM_CREATE_SPILL_SHIFT) it
+    overflows as well, and gm_sync redoes the requests it
+    missed as a sub-batch with a set twice as large.  Either way GM_OK: verdicts and hits equal the
+    oracle's, and the counters hold exactly one batch."""
     torch, dev = torch_dev
     ss, b = workloads.c4_stress_generation()
     reqs, arena = records.gen_c4(6_000, ss, seed=workloads.C4_STRESS_POOL_SEED + 9, plant_rate=0.3, stress=True)
@@ -242,7 +244,7 @@ def test_set_overflow_continuation(torch_dev, host):
     shift = 1
     while (1 << 19) >> (shift + 1) >= keys // 2 and shift < 12:
         shift += 1
-    e = engine.Engine(0, set_shift=shift)
+    e = engine.Engine(0, set_shift=shift, spill_shift=0 if spill else 8)
     e.load(b, 5)
     if host:
         got, gh = e.match_host(reqs, arena)   # no GmError
@@ -257,9 +259,13 @@ def test_set_overflow_continuation(torch_dev, host):
         got = d_out.cpu().numpy().view(records.VERDICT_DTYPE)
         gh = d_hits[:e.stats()["last_hits"]].cpu().numpy().view(np.uint32)
     st = e.stats()
-    assert st["n_set_reruns"] >= 1 and st["set_shift"] == shift, st
+    assert st["set_shift"] == shift, st
+    if spill:
+        assert st["last_spill"] > 0 and st["n_set_reruns"] == 0, st
+    else:
+        assert st["last_redo"] > 0 and st["n_set_reruns"] >= 1, st
     exp, eh = Oracle(b, 5).match(reqs, arena)
-    assert_verdicts_equal(got, exp, gh, eh, f"set overflow re-run (shift {shift})")
+    assert_verdicts_equal(got, exp, gh, eh, f"set overflow continuation (shift {shift}, spill {spill})")
     assert np.array_equal(e.counters(), _one_batch_counters(e, got, gh))
 
 
@@ -398,13 +404,13 @@ def test_set_overflow_continuation_cost(torch_dev):
     assert all(c[4]["n_set_reruns"] == 0 for c in clean)
     ov = [first_batch(shift) for _ in range(3)]
     for v, h, ctr, t, st in ov:
-        assert st["n_set_reruns"] >= 1, (shift, keys, st["n_set_reruns"])
+        assert st["last_spill"] > 0, (shift, keys, st)
         assert_verdicts_equal(v, ref_v, h, ref_h, f"continuation vs clean (shift {shift})")
         assert np.array_equal(ctr, ref_c)
     t_clean, t_ov = min(c[3] for c in clean), min(o[3] for o in ov)
-    redo = [o[4]["last_redo"] for o in ov]
+    redo = [o[4]["last_spill"] for o in ov]
     print(f"continuation: {t_ov * 1e3:.2f} ms vs clean {t_clean * 1e3:.2f} ms; keys {keys}, set shift {shift}, "
-          f"requests redone {redo} of {n}")
+          f"pairs spilled {redo} for {n} requests")
     assert t_ov < 2 * t_clean, (t_ov, t_clean, shift, keys, redo)
 
 
@@ -439,7 +445,7 @@ def test_two_batches_before_one_sync(torch_dev):
     A = enqueue(e, ra, aa, 8 * len(ra) + 1024)
     B = enqueue(e, rb, ab, 8 * len(rb) + 1024)
     e.sync(0)
-    assert e.stats()["n_set_reruns"] >= 1
+    assert e.stats()["n_set_reruns"] >= 1   # A (not the stream's last batch) re-ran whole
     got_a, gh_a = read(A, int(len(eh_a)))
     got_b, gh_b = read(B, int(len(eh_b)))
     assert_verdicts_equal(got_a, exp_a, gh_a, eh_a, "queued batch A (set overflow)")
