@@ -2114,6 +2114,13 @@ static int emit_hits(gm_ctx *c, Scratch *S, const Generation *g, uint32_t n, gm_
     return GM_OK;
 }
 
+// the entries of the spill a batch may fill (the whole buffer, or 2^-k of it under the
+// GM_CREATE_SPILL_SHIFT(k) test hook): the count word can run past it, the entries cannot
+static size_t spill_cap_of(const gm_ctx *c, const Scratch *S) {
+    return c->spill_shift ? std::min<size_t>(std::max<size_t>(S->cap_spill >> c->spill_shift, 16), S->cap_spill)
+                          : S->cap_spill;
+}
+
 static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *reqs, const uint8_t *A, uint64_t alen,
                      uint32_t n, gm_verdict *out, uint32_t *hit_ids, size_t hit_cap, const uint64_t *dlen, uint32_t slot) {
     hipStream_t s = S->stream;
@@ -2244,7 +2251,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     HIPCHK(c, hipMemsetAsync(S->d_redo, 0, (((size_t)n + 31) / 32) * 4, s));
     // one epoch per batch (two with decoders: the decoded pass's jobs take epoch + 1)
     if ((e = next_epoch(c, S, t))) return e;
-    const size_t spill_cap = c->spill_shift ? std::max<size_t>(S->cap_spill >> c->spill_shift, 16) : S->cap_spill;
+    const size_t spill_cap = spill_cap_of(c, S);
     Dedup dd{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, out, S->d_cnt, S->d_status, S->d_redo,
              S->d_spill, (uint32_t)std::min<size_t>(spill_cap, 0xFFFFFFFFu)};
 
@@ -2359,7 +2366,8 @@ static int rerun_whole(gm_ctx *c, Scratch *S, const Scratch::Replay &rp0, uint32
 
 // the first nspill spilled pairs sorted into d_spill2 and each distinct one counted for its request
 // (those of a redone request, redo's bits, skipped): out = the sorted array
-static int sort_spill(gm_ctx *c, Scratch *S, uint32_t nspill, const uint32_t *redo, unsigned long long *&out) {
+static int sort_spill(gm_ctx *c, Scratch *S, uint32_t nspill, const uint32_t *redo, const Dedup &dd,
+                      unsigned long long *&out) {
     hipStream_t s = S->stream;
     int e;
     if ((e = grow(c, s, S->d_spill2, S->cap_spill2, (size_t)nspill))) return e;
@@ -2368,7 +2376,7 @@ static int sort_spill(gm_ctx *c, Scratch *S, uint32_t nspill, const uint32_t *re
     if ((e = grow(c, s, S->d_rtemp, S->cap_rtemp, tmp))) return e;
     HIPCHK(c, hipcub::DeviceRadixSort::SortKeys(S->d_rtemp, tmp, S->d_spill, S->d_spill2, (int)nspill, 0, 64, s));
     k_spill_count<<<std::min<uint32_t>((nspill + 255) / 256, (uint32_t)c->cu_count * 4), 256, 0, s>>>(S->d_spill2, nspill,
-                                                                                                        redo, S->d_cnt);
+                                                                                                        redo, S->d_cnt, dd);
     HIPCHK(c, hipGetLastError());
     out = S->d_spill2;
     return GM_OK;
@@ -2386,15 +2394,15 @@ static int spill_continuation(gm_ctx *c, Scratch *S, const Scratch::Replay &rp, 
         return fail(c, GM_E_OVERFLOW, "WAF dedupe set full and the generation changed before the batch could be "
                                       "completed: retry it");
     const Generation *g = c->gen;
-    const uint32_t nspill = (uint32_t)std::min<size_t>(S->h_status[SPILL_WORD], S->cap_spill);
+    const uint32_t nspill = (uint32_t)std::min<size_t>(S->h_status[SPILL_WORD], spill_cap_of(c, S));
     int e;
     DoneGuard G(S);
     unsigned long long *sp = nullptr;
-    if (nspill && (e = sort_spill(c, S, nspill, nullptr, sp))) return e;
+    const Dedup dd0{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch + 1, rp.out, S->d_cnt, S->d_status, nullptr,
+                    nullptr, 0u};
+    if (nspill && (e = sort_spill(c, S, nspill, nullptr, dd0, sp))) return e;
     k_clear_held<<<1, 64, 0, s>>>(S->d_status);
     HIPCHK(c, hipGetLastError());
-    const Dedup dd0{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, rp.out, S->d_cnt, S->d_status, nullptr,
-                    nullptr, 0u};
     if ((e = emit_hits(c, S, g, rp.n, rp.out, rp.hits, rp.hit_cap, S->d_bctr, dd0, nullptr, 0, nullptr, sp, nspill)))
         return e;
     const size_t nctr = std::max<size_t>(g->n_counters, 1);
@@ -2430,7 +2438,7 @@ static int set_continuation(gm_ctx *c, Scratch *S, const Scratch::Replay &rp, ui
     const GTab &t = g->tab;
     const uint32_t n = rp.n;
     const uint32_t np1 = S->h_status[1];
-    const uint32_t nspill = (uint32_t)std::min<size_t>(S->h_status[SPILL_WORD], S->cap_spill);
+    const uint32_t nspill = (uint32_t)std::min<size_t>(S->h_status[SPILL_WORD], spill_cap_of(c, S));
     int e;
     DoneGuard G(S);
     // the requests to redo
@@ -2466,6 +2474,15 @@ static int set_continuation(gm_ctx *c, Scratch *S, const Scratch::Replay &rp, ui
     k_redo_emit<<<(m + 255) / 256, 256, 0, s>>>(rp.reqs, rp.A, rp.out, S->d_rlist, m, S->d_rbase, sub_len, S->d_rsreq,
                                                 S->d_rsarena, S->d_rsout, S->d_rsblk, snblk);
     HIPCHK(c, hipGetLastError());
+    // the first pass's spilled pairs of the requests not redone, sorted and counted now: the
+    // sub-batch's buffers may reallocate the spill (waf_buffers), not its sorted copy
+    unsigned long long *sp = nullptr;
+    if (nspill) {
+        // (the first pass's set: the pair epoch, its jobs' epochs taken as in use)
+        const Dedup dd1{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch + 1, rp.out, S->d_cnt, S->d_status,
+                        nullptr, nullptr, 0u};
+        if ((e = sort_spill(c, S, nspill, S->d_redo, dd1, sp))) return e;
+    }
     const WafIO io{S->d_rsarena, sub_len, nullptr, S->d_rsreq, m, S->d_rsout, S->d_rsblk, snblk};
     const std::function<int(int)> nomark = [](int) { return GM_OK; };
     for (;;) {
@@ -2499,9 +2516,6 @@ static int set_continuation(gm_ctx *c, Scratch *S, const Scratch::Replay &rp, ui
     HIPCHK(c, hipGetLastError());
     const Dedup dd0{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, rp.out, S->d_cnt, S->d_status, nullptr,
                     nullptr, 0u};
-    // the first pass's spilled pairs of the requests not redone
-    unsigned long long *sp = nullptr;
-    if (nspill && (e = sort_spill(c, S, nspill, S->d_redo, sp))) return e;
     if ((e = emit_hits(c, S, g, n, rp.out, rp.hits, rp.hit_cap, S->d_bctr, dd0, S->d_redo, np1, S->d_rlist, sp,
                        nspill))) return e;
     const size_t nctr = std::max<size_t>(g->n_counters, 1);
