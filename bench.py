@@ -7,11 +7,13 @@ N > 1 is launched by torch.distributed.run (one rank per GPU); requests shard wi
 collective (weak scaling: every rank classifies its own R requests); the per-location and
 per-rule hit counters are all-reduced with RCCL over xGMI once per timed interval
 (gm_counters_allreduce, after the last step).
-A "step" = one gm_match_batch + gm_sync over the rank's R requests.  --inflight D (default 2):
-batches are pipelined over D streams -- step k is enqueued on stream k % D and completed by its
-gm_sync when that stream comes round again -- so a batch's tail overlaps the next batch's scan, as
-a server handing the engine consecutive batches would run it; every step is still a whole batch
-with its own verdicts and hits.  Rank 0 prints one JSON line (config.inflight = D).
+A "step" = one gm_match_batch + gm_sync over the rank's R requests.  --inflight D (default 1):
+with D > 1 batches are pipelined over D streams -- step k is enqueued on stream k % D and completed
+by its gm_sync when that stream comes round again -- so a batch's tail overlaps the next batch's
+scan, as a server handing the engine consecutive batches would run it; every step is still a whole
+batch with its own verdicts and hits.  The default stays 1: overlapped launches stretch each
+kernel's duration, and the roofline fraction is read from the scan's launch duration (DESIGN.md §6
+has the D = 2 numbers).  Rank 0 prints one JSON line (config.inflight = D).
 """
 
 from __future__ import annotations
@@ -64,7 +66,7 @@ def main():
                          "over the ranks with the hit counters all-reduced (--stream, --batch)")
     ap.add_argument("--stream", type=int, default=100_000_000, help="c5: requests in the whole stream")
     ap.add_argument("--batch", type=int, default=10_000_000, help="c5: requests per gm_match_batch")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=1,
                     help="batches in flight: step k runs on stream k %% inflight, and its gm_sync waits until the "
                          "stream comes round again, so one batch's tail (context filter, exact check, hit "
                          "emission) overlaps the next batch's route and scan (1: one batch at a time)")
