@@ -2053,7 +2053,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     // and zone sets share it (the location slices keep one value per member in alw_rule)
     std::vector<uint32_t> alw_rl;
     auto tab_bytes = [](const MultiDfa &m) {   // the group's rows (gm_tables.hpp DAlwGroup)
-        return (size_t)m.n_states * ((size_t)m.n_classes + (m.n_classes & 1) + 4) * 2;
+        return (size_t)m.n_states * ((size_t)alw_row_cols((uint32_t)m.n_classes) + 4) * 2;
     };
     // greedy: in `order`, a component joins the open group while joinable(first member, it), the
     // group has < ALW_GROUP_MAX members and the minimised union's rows stay within
@@ -2089,32 +2089,44 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     };
     // slices: consecutive groups, <= ALW_SLICE_GROUPS of them within ALWAYS_LDS_BYTES; member k of
     // group g stores val(g, k) in alw_rule and scans the zones zones(g, k)
+    bool alw_layout_err = false;   // (an internal invariant: the class table's offsets are the rows')
     auto pack_slices = [&](const std::vector<std::vector<uint32_t>> &gmem, const std::vector<MultiDfa> &gdfa,
                            auto val, auto zones, uint32_t server, const std::vector<std::vector<uint32_t>> *mrules = nullptr) {
         auto pad16 = [&]() { alw_pack.resize((alw_pack.size() + 15) & ~size_t(15), 0); };
         for (size_t g0 = 0; g0 < gmem.size();) {
-            size_t g1 = g0, bytes = 2048;
-            while (g1 < gmem.size() && g1 - g0 < ALW_SLICE_GROUPS && bytes + tab_bytes(gdfa[g1]) + 16 <= ALWAYS_LDS_BYTES)
-                bytes += tab_bytes(gdfa[g1++]) + 16;
+            // the class table's size grows at the fifth group (alw_cls_bytes)
+            size_t g1 = g0, rows_bytes = 0;
+            while (g1 < gmem.size() && g1 - g0 < ALW_SLICE_GROUPS &&
+                   alw_cls_bytes((uint32_t)(g1 - g0 + 1)) + rows_bytes + tab_bytes(gdfa[g1]) + 16 <= ALWAYS_LDS_BYTES)
+                rows_bytes += ((tab_bytes(gdfa[g1++]) + 15) & ~size_t(15));
             DAlwSlice sl{};
             sl.off = (uint32_t)alw_pack.size();
             sl.first_group = (uint32_t)alw.size();
             sl.n_groups = (uint32_t)(g1 - g0);
             sl.server = server;
-            // clsq[b]: byte b's class in groups 0..3 (a byte each), times 2 -- the class's byte offset
-            // in a row of u16 transitions, added to the row by one byte-select add (add_cls);
-            // clsq[256 + b]: groups 4..7
-            std::vector<uint32_t> clsq(512, 0);
-            for (size_t j = g0; j < g1; j++)
+            // clsa[b * NGP + j] = group j's row 0 offset in the slice + 2 x byte b's class in group j:
+            // the byte offset of b's transition column, so a step adds it to the chain's row and
+            // reads (alw_cls_bytes; NGP = 4 or 8 u32 per byte, one or two 16-byte LDS reads)
+            const uint32_t ngp = alw_cls_ngp(sl.n_groups), hdr = alw_cls_bytes(sl.n_groups);
+            std::vector<uint32_t> tro(g1 - g0, 0);
+            {
+                uint32_t o = hdr;
+                for (size_t j = g0; j < g1; j++) { tro[j - g0] = o; o += (uint32_t)((tab_bytes(gdfa[j]) + 15) & ~size_t(15)); }
+            }
+            std::vector<uint32_t> clsa((size_t)(ALW_CLS_IDENTITY + 1) * ngp, 0);
+            for (size_t j = g0; j < g1; j++) {
                 for (int b = 0; b < 256; b++)
-                    clsq[((j - g0) >= 4 ? 256 : 0) + b] |= (2u * gdfa[j].cls[b]) << (8 * ((j - g0) & 3));
-            const uint8_t *cb = reinterpret_cast<const uint8_t *>(clsq.data());
-            alw_pack.insert(alw_pack.end(), cb, cb + 2048);
+                    clsa[(size_t)b * ngp + (j - g0)] = tro[j - g0] + 2u * gdfa[j].cls[b];
+                clsa[(size_t)ALW_CLS_IDENTITY * ngp + (j - g0)] = tro[j - g0] + 2u * (uint32_t)gdfa[j].n_classes;
+            }
+            const uint8_t *cb = reinterpret_cast<const uint8_t *>(clsa.data());
+            alw_pack.insert(alw_pack.end(), cb, cb + hdr);
             for (size_t j = g0; j < g1; j++) {
                 const MultiDfa &m = gdfa[j];
-                const size_t S = (size_t)m.n_states, Cn = (size_t)m.n_classes, Cp = Cn + (Cn & 1), R = Cp + 4;
+                const size_t S = (size_t)m.n_states, Cn = (size_t)m.n_classes, Cp = alw_row_cols((uint32_t)Cn), R = Cp + 4;
                 DAlwGroup g{};
                 g.tr_off = (uint32_t)(alw_pack.size() - sl.off);
+                if (g.tr_off != tro[j - g0]) alw_layout_err = true;
                 g.mask_off = (uint32_t)(2 * Cp);
                 // states renumbered: the dead state 0, the others, then the emitting ones (an emit
                 // mask, or the target of a transition flagged MDFA_EMIT) from row emit_row on
@@ -2136,6 +2148,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                     const size_t o = (size_t)perm[q] * R;
                     for (size_t c = 0; c < Cn; c++)
                         rows[o + c] = (uint16_t)(2 * R * perm[m.trans[q * Cn + c] & 0x3FFF]);
+                    rows[o + Cn] = (uint16_t)(2 * R * perm[q]);   // the identity column
                     rows[o + Cp] = (uint16_t)m.emit[q]; rows[o + Cp + 1] = (uint16_t)(m.emit[q] >> 16);
                     rows[o + Cp + 2] = (uint16_t)m.endm[q]; rows[o + Cp + 3] = (uint16_t)(m.endm[q] >> 16);
                 }
@@ -2380,6 +2393,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.off_rsl_pbit = I.put(rsl_pbit);
     if (rsl_heads.empty()) rsl_heads.assign(1, 0u);
     h.n_rsl_heads = (uint32_t)(rsl_heads.size() / RSL_HEAD_WORDS);
+    if (alw_layout_err) { R.code = GM_E_INVAL; R.err = "internal: union-DFA slice layout"; return R; }
     st.n_rsl_heads = (uint32_t)rsl_head_slice.size();
     h.off_rsl_heads = I.put(rsl_heads);
     rsl_head_slice.resize(std::max<size_t>(rsl_head_slice.size(), 1), 0u);

@@ -1464,6 +1464,7 @@ struct Scratch {
     int32_t *d_rqb = nullptr; size_t cap_rqb = 0;        // and its longest prefix match (the tail pass)
     unsigned long long *d_rqm = nullptr; size_t cap_rqm = 0;   // and its prefiltered-slice mask
     uint32_t *d_hlist = nullptr; size_t cap_hlist = 0;         // the anchored slices' candidate lists
+    uint32_t *d_along = nullptr; size_t cap_along = 0;         // the always-run slices' long zones + count
     uint32_t *d_hcnt = nullptr; size_t cap_hcnt = 0;           // and their lengths (k_rloc_heads)
     unsigned long long *d_bctr = nullptr; size_t cap_bctr = 0; // this batch's counters (k_ctr_commit)
     uint2 *d_slow = nullptr; size_t cap_slow = 0;              // requests for k_route's SLOW pass
@@ -1504,7 +1505,7 @@ struct Scratch {
                         (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm, (void *)d_rqu, (void *)d_bctr, (void *)d_slow,
                         (void *)d_redo, (void *)d_rlist, (void *)d_rsize, (void *)d_rbase, (void *)d_rtemp, (void *)d_rsreq,
                         (void *)d_rsarena, (void *)d_rsout, (void *)d_rsblk, (void *)d_rscnt, (void *)d_ovlog, (void *)d_wmsg, (void *)d_spill, (void *)d_spill2,
-                        (void *)d_hlist, (void *)d_hcnt})
+                        (void *)d_hlist, (void *)d_hcnt, (void *)d_along})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
         if (h_ovlog) (void)hipHostFree(h_ovlog);
@@ -1869,18 +1870,32 @@ static int launch_always(gm_ctx *c, hipStream_t s, const Generation *g, const ui
                          const uint64_t *dlen) {
     const GTab &t = g->tab;
     const DAlwSlice *sls = reinterpret_cast<const DAlwSlice *>(g->host_image.data() + g->hdr.off_alw_slices);
+    // the long zones first (k_alw_long): one list per WAF pass, one entry per request's long zone at
+    // most on average (a longer list is not used)
+    uint32_t n_slices = 0;
+    for (uint32_t k = 0; k < t.n_alw_slices; k++) n_slices += sls[k].server == GM_NONE;
+    const uint32_t lcap = std::max<uint32_t>(n, 1024);
+    if (n_slices) {
+        int e;
+        if ((e = grow(c, s, S->d_along, S->cap_along, (size_t)lcap + 1))) return e;
+        HIPCHK(c, hipMemsetAsync(S->d_along + lcap, 0, 4, s));
+        k_alw_long<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8)), 256, 0, s>>>(
+            reqs, n, dd.out, S->d_along, lcap, S->d_along + lcap);
+        HIPCHK(c, hipGetLastError());
+    }
+    const uint32_t *LL = S->d_along, *LC = S->d_along + lcap;
     for (uint32_t k = 0; k < t.n_alw_slices; k++) {
         const DAlwSlice &sl = sls[k];
         const dim3 grid((uint32_t)c->cu_count), blk(1024);
         switch (sl.n_groups) {
-        case 1: k_waf_always_multi<1><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
-        case 2: k_waf_always_multi<2><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
-        case 3: k_waf_always_multi<3><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
-        case 4: k_waf_always_multi<4><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
-        case 5: k_waf_always_multi<5><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
-        case 6: k_waf_always_multi<6><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
-        case 7: k_waf_always_multi<7><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
-        default: k_waf_always_multi<8><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k); break;
+        case 1: k_waf_always_multi<1><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 2: k_waf_always_multi<2><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 3: k_waf_always_multi<3><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 4: k_waf_always_multi<4><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 5: k_waf_always_multi<5><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 6: k_waf_always_multi<6><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 7: k_waf_always_multi<7><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
+        default: k_waf_always_multi<8><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
         }
         HIPCHK(c, hipGetLastError());
     }
@@ -2805,7 +2820,8 @@ extern "C" int gm_debug_alw_profile(gm_ctx *c, const gm_req *reqs, const uint8_t
         const DAlwSlice &sl = sls[si];
         if (sl.server != GM_NONE) continue;
         const uint8_t *P = img + h.off_alw_pack + sl.off;
-        const uint32_t *clsq = reinterpret_cast<const uint32_t *>(P);
+        const uint32_t *clsa = reinterpret_cast<const uint32_t *>(P);
+        const uint32_t ngp = alw_cls_ngp(sl.n_groups);
         for (uint32_t j = 0; j < sl.n_groups; j++) {
             const DAlwGroup &gr = grs[sl.first_group + j];
             const uint8_t *G = P + gr.tr_off;
@@ -2819,9 +2835,8 @@ extern "C" int gm_debug_alw_profile(gm_ctx *c, const gm_req *reqs, const uint8_t
                         uint32_t row = gr.start_row;
                         for (uint32_t i = 0; i < lens[z] && row; i++) {
                             const uint32_t b = arena[o + i];
-                            const uint32_t cl = (clsq[(j >= 4 ? 256u : 0u) + b] >> (8 * (j & 3))) & 0xFF;
                             uint16_t nx;
-                            memcpy(&nx, G + row + cl, 2);   // (clsq holds 2 * class)
+                            memcpy(&nx, P + row + clsa[b * ngp + j], 2);   // (the column includes tr_off)
                             tot++;
                             if (row == gr.start_row) { at++; if (nx == gr.start_row) stay++; }
                             row = nx;

@@ -295,9 +295,12 @@ __host__ __device__ inline uint32_t peer_draw(uint64_t lo, uint64_t hi, uint32_t
 // pass over a zone answers a whole group.  Groups are packed into slices of <= ALW_SLICE_GROUPS
 // groups that fit ALWAYS_LDS_BYTES together; k_waf_always_multi stages one slice in LDS and runs a
 // transition chain per group of the slice.
-// Slice pack (16-B aligned): clsq u32[256] (byte b's class in group j of the slice = byte j of
-// clsq[b]) | per group, its rows.  A row (state) is Cp + 4 u16: the transitions of the C classes
-// (Cp = C rounded up to even), then the state's emit mask and end mask (u32 each).  A transition
+// Slice pack (16-B aligned): clsa u32[257 * NGP] (NGP = 4 for up to four groups, else 8; entry
+// b * NGP + j = group j's tr_off + 2 x byte b's class in group j: the offset of b's column in the
+// group's row 0, so a chain's step is one add to its row and one u16 read, and a byte's entries for
+// four groups are one 16-byte LDS read; entry 256 the identity columns) | per group, its rows.  A
+// row (state) is Cp + 4 u16: the transitions of the C classes, the identity column (the row's own
+// offset), padded to Cp = alw_row_cols(C), then the state's emit mask and end mask (u32 each).  A transition
 // is the target row's byte offset in the group: the step needs no multiply, and row 0 (the dead
 // state) is all zeros.  The emitting states are numbered last, from row emit_row on: a chain
 // entered one within a chunk iff the largest row it took there is >= emit_row (one max per step,
@@ -305,7 +308,15 @@ __host__ __device__ inline uint32_t peer_draw(uint64_t lo, uint64_t hi, uint32_t
 constexpr uint32_t ALWAYS_LDS_BYTES = 160 * 1024;
 constexpr uint32_t ALW_GROUP_BYTES = 64 * 1024 - 64;   // row byte offsets fit a u16 with the flag bit
 constexpr uint32_t ALW_GROUP_MAX = 32;
-constexpr uint32_t ALW_CLASSES_MAX = 127;   // clsq holds 2 * class in a byte
+constexpr uint32_t ALW_CLASSES_MAX = 127;
+__host__ __device__ constexpr uint32_t alw_cls_ngp(uint32_t n_groups) { return n_groups <= 4 ? 4u : 8u; }
+// entries 0..255: the bytes; entry 256: every group's identity column (a row's own offset: a step
+// that changes nothing, for the bytes past a chunk's end)
+constexpr uint32_t ALW_CLS_IDENTITY = 256;
+__host__ __device__ constexpr uint32_t alw_cls_bytes(uint32_t n_groups) { return 257u * 4u * alw_cls_ngp(n_groups); }
+// a group's row: its classes, the identity column (class n_classes), padded to even, then the emit
+// and end masks (u32 each)
+__host__ __device__ constexpr uint32_t alw_row_cols(uint32_t n_classes) { return (n_classes + 2) & ~1u; }
 #ifndef GM_ALW_SLICE_GROUPS
 #define GM_ALW_SLICE_GROUPS 8
 #endif
