@@ -1465,6 +1465,7 @@ struct Scratch {
     unsigned long long *d_rqm = nullptr; size_t cap_rqm = 0;   // and its prefiltered-slice mask
     uint32_t *d_hlist = nullptr; size_t cap_hlist = 0;         // the anchored slices' candidate lists
     uint32_t *d_along = nullptr; size_t cap_along = 0;         // the always-run slices' long zones + count
+    AlwEmit *d_alwemit = nullptr; size_t cap_alwemit = 0;      // and their emission state
     uint32_t *d_hcnt = nullptr; size_t cap_hcnt = 0;           // and their lengths (k_rloc_heads)
     unsigned long long *d_bctr = nullptr; size_t cap_bctr = 0; // this batch's counters (k_ctr_commit)
     uint2 *d_slow = nullptr; size_t cap_slow = 0;              // requests for k_route's SLOW pass
@@ -1505,7 +1506,7 @@ struct Scratch {
                         (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm, (void *)d_rqu, (void *)d_bctr, (void *)d_slow,
                         (void *)d_redo, (void *)d_rlist, (void *)d_rsize, (void *)d_rbase, (void *)d_rtemp, (void *)d_rsreq,
                         (void *)d_rsarena, (void *)d_rsout, (void *)d_rsblk, (void *)d_rscnt, (void *)d_ovlog, (void *)d_wmsg, (void *)d_spill, (void *)d_spill2,
-                        (void *)d_hlist, (void *)d_hcnt, (void *)d_along})
+                        (void *)d_hlist, (void *)d_hcnt, (void *)d_along, (void *)d_alwemit})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
         if (h_ovlog) (void)hipHostFree(h_ovlog);
@@ -1879,23 +1880,32 @@ static int launch_always(gm_ctx *c, hipStream_t s, const Generation *g, const ui
         int e;
         if ((e = grow(c, s, S->d_along, S->cap_along, (size_t)lcap + 1))) return e;
         HIPCHK(c, hipMemsetAsync(S->d_along + lcap, 0, 4, s));
-        k_alw_long<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8)), 256, 0, s>>>(
+        k_alw_long<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 1023) / 1024, (uint32_t)c->cu_count * 4)), 1024, 0, s>>>(
             reqs, n, dd.out, S->d_along, lcap, S->d_along + lcap);
         HIPCHK(c, hipGetLastError());
     }
     const uint32_t *LL = S->d_along, *LC = S->d_along + lcap;
+    // the slices' emission state, in device memory (AlwEmit; stream-ordered by a one-lane kernel)
+    AlwEmit *EM = nullptr;
+    if (t.n_alw_slices) {
+        int e;
+        if ((e = grow(c, s, S->d_alwemit, S->cap_alwemit, 1))) return e;
+        EM = S->d_alwemit;
+        k_put_emit<<<1, 64, 0, s>>>(EM, AlwEmit{dd, S->d_pairs, (uint32_t)S->cap_pairs, t.alw_rule, t.alw_rl});
+        HIPCHK(c, hipGetLastError());
+    }
     for (uint32_t k = 0; k < t.n_alw_slices; k++) {
         const DAlwSlice &sl = sls[k];
         const dim3 grid((uint32_t)c->cu_count), blk(1024);
         switch (sl.n_groups) {
-        case 1: k_waf_always_multi<1><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
-        case 2: k_waf_always_multi<2><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
-        case 3: k_waf_always_multi<3><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
-        case 4: k_waf_always_multi<4><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
-        case 5: k_waf_always_multi<5><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
-        case 6: k_waf_always_multi<6><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
-        case 7: k_waf_always_multi<7><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
-        default: k_waf_always_multi<8><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, S->d_pairs, (uint32_t)S->cap_pairs, dd, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 1: k_waf_always_multi<1><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 2: k_waf_always_multi<2><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 3: k_waf_always_multi<3><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 4: k_waf_always_multi<4><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 5: k_waf_always_multi<5><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 6: k_waf_always_multi<6><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 7: k_waf_always_multi<7><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
+        default: k_waf_always_multi<8><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
         }
         HIPCHK(c, hipGetLastError());
     }
@@ -3353,7 +3363,8 @@ extern "C" int gm_upstream_uris(gm_ctx *c, const gm_batch *in, const gm_verdict 
 // tuning macros count when they differ from the shipped values.
 static constexpr uint32_t kBuildFlags =
 #if defined(GM_EXP_COUNT) || defined(GM_EXP_CMASK) || defined(GM_EXP_ROUTE_AFTER) || defined(GM_EXP_ROUTE_FIRST) || \
-    defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_SCAN_NOBRANCH) || defined(GM_SCAN_VMASK)
+    defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_SCAN_NOBRANCH) || defined(GM_SCAN_VMASK) || \
+    defined(GM_EXP_ALW_NOEMIT) || defined(GM_EXP_ALW_COUNT)
     GM_BUILD_EXPERIMENT |
 #endif
 #if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != 32 || \
