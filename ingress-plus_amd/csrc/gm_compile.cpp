@@ -1357,22 +1357,40 @@ static void put_md5(std::vector<uint32_t> &v, const std::string &addr) {
 
 
 // The heads of an anchored DFA (state 1 = start, 0 = dead; acc bit0 match, bit1 match at the
-// subject's end): bit b1 << 8 | b2 of `bits` (RSL_HEAD_WORDS u32) for every two-byte start b1 b2 of
-// a subject it can match (b2 = 0 stands for a one-byte subject, and key 0 for the empty one: a
-// $uri with a NUL in its first two bytes joins every list, k_rloc_heads); a DFA that matches at its start state sets every bit.  A final '\n' may
-// satisfy a `$` (PCRE), so an end-accepting state after b1 also sets b1 '\n'.
+// subject's end): bit rsl_head_key(b0, b1, b2) of `bits` (RSL_HEAD_WORDS u32) for every three-byte
+// start b0 b1 b2 of a subject it can match (a 0 stands for "no byte": rsl_head_key(b0, b1, 0) is
+// the two-byte subject b0 b1, and so on; a $uri with a NUL in its first three bytes joins every
+// list, k_rloc_heads); a DFA that matches at its start state sets every bit.  A final '\n' may
+// satisfy a `$` (PCRE), so an end-accepting state also sets its subject + '\n'.  Past
+// RSL_HEAD_PAIRS live two-byte starts the map is full (a superset: the slice runs on every request).
 static void dfa_heads(const Dfa &d, std::vector<uint32_t> &bits) {
     auto set = [&](uint32_t key) { bits[key >> 5] |= 1u << (key & 31); };
     auto step = [&](uint32_t st, int b) { return (uint32_t)(d.trans[(size_t)st * d.n_classes + d.cls[b]] & DFA_TRANS_STATE_MASK); };
-    if (d.n_states < 2 || (d.acc[1] & 1)) { std::fill(bits.begin(), bits.end(), 0xFFFFFFFFu); return; }
-    if (d.acc[1] & 2) { set(0); set((uint32_t)'\n' << 8); }
-    for (int b1 = 1; b1 < 256; b1++) {
-        const uint32_t s1 = step(1, b1);
+    auto fill = [&]() { std::fill(bits.begin(), bits.end(), 0xFFFFFFFFu); };
+    if (d.n_states < 2 || (d.acc[1] & 1)) { fill(); return; }
+    if (d.acc[1] & 2) { set(rsl_head_key(0, 0, 0)); set(rsl_head_key('\n', 0, 0)); }
+    uint32_t pairs = 0;
+    for (uint32_t b0 = 1; b0 < 256; b0++) {
+        const uint32_t s1 = step(1, (int)b0);
         if (!s1) continue;
-        if (d.acc[s1] & 1) { for (int b2 = 0; b2 < 256; b2++) set((uint32_t)b1 << 8 | b2); continue; }
-        if (d.acc[s1] & 2) { set((uint32_t)b1 << 8); set((uint32_t)b1 << 8 | '\n'); }
-        for (int b2 = 1; b2 < 256; b2++)
-            if (step(s1, b2)) set((uint32_t)b1 << 8 | b2);
+        if (d.acc[s1] & 1) {
+            for (uint32_t b1 = 0; b1 < 256; b1++)
+                for (uint32_t b2 = 0; b2 < 256; b2++) set(rsl_head_key(b0, b1, b2));
+            continue;
+        }
+        if (d.acc[s1] & 2) { set(rsl_head_key(b0, 0, 0)); set(rsl_head_key(b0, '\n', 0)); }
+        for (uint32_t b1 = 1; b1 < 256; b1++) {
+            const uint32_t s2 = step(s1, (int)b1);
+            if (!s2) continue;
+            if (++pairs > RSL_HEAD_PAIRS) { fill(); return; }
+            if (d.acc[s2] & 1) {
+                for (uint32_t b2 = 0; b2 < 256; b2++) set(rsl_head_key(b0, b1, b2));
+                continue;
+            }
+            if (d.acc[s2] & 2) { set(rsl_head_key(b0, b1, 0)); set(rsl_head_key(b0, b1, '\n')); }
+            for (uint32_t b2 = 1; b2 < 256; b2++)
+                if (step(s2, (int)b2)) set(rsl_head_key(b0, b1, b2));
+        }
     }
 }
 
@@ -2285,7 +2303,18 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                     if (heads[k][w]) return w * 32 + (uint32_t)__builtin_ctz(heads[k][w]);
                 return 0xFFFFFFFFu;
             };
-            std::stable_sort(ord_a.begin(), ord_a.end(), [&](uint32_t a, uint32_t b) { return head0(a) < head0(b); });
+            // (narrow maps first -- a few starts each, grouped by their lowest -- then the broader
+            // ones, which select most requests wherever they go)
+            auto breadth = [&](uint32_t k) {
+                uint32_t c = 0;
+                for (uint32_t w = 0; w < RSL_HEAD_WORDS; w++) c += (uint32_t)__builtin_popcount(heads[k][w]);
+                return c <= 16 ? 0u : c <= 1024 ? 1u : 2u;
+            };
+            std::vector<uint32_t> hb(rcomps.size(), 0), h0(rcomps.size(), 0);
+            for (uint32_t k : ord_a) { hb[k] = breadth(k); h0[k] = head0(k); }
+            std::stable_sort(ord_a.begin(), ord_a.end(), [&](uint32_t a, uint32_t b) {
+                return hb[a] != hb[b] ? hb[a] < hb[b] : h0[a] < h0[b];
+            });
             std::vector<std::vector<uint32_t>> gm_a, gm_un, gm_uf, gm_r;
             std::vector<MultiDfa> gd_a, gd_un, gd_uf, gd_r;
             std::vector<uint32_t> single;

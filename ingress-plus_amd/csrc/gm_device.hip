@@ -2223,6 +2223,15 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
                         t, q.st, q.u, q.count, t.rsl_head_slice, h0, k, S->d_hlist, n, S->d_hcnt);
                     HIPCHK(c, hipGetLastError());
                 }
+                static const bool trace_heads = getenv("GM_TRACE_HEADS") != nullptr;
+                if (trace_heads) {   // (diagnostics, GM_TRACE_HEADS=1: the candidate lists' lengths)
+                    std::vector<uint32_t> hc(nh);
+                    HIPCHK(c, hipMemcpyAsync(hc.data(), S->d_hcnt, nh * 4, hipMemcpyDeviceToHost, rs));
+                    HIPCHK(c, hipStreamSynchronize(rs));
+                    fprintf(stderr, "[heads] n=%u:", n);
+                    for (uint32_t h = 0; h < nh; h++) fprintf(stderr, " %u", hc[h]);
+                    fprintf(stderr, "\n");
+                }
             }
             for (uint32_t k = t.n_alw_slices; k < t.n_alw_slices + t.n_rsl; k++) {
                 const dim3 grid((uint32_t)c->cu_count), blk(1024);

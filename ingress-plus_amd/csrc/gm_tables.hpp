@@ -346,10 +346,17 @@ constexpr uint32_t ALW_SLICE_REVERSED = 1;
 // k_rloc_pref mask has bit (flags >> 8) & 63
 constexpr uint32_t ALW_SLICE_PREF = 2;
 // an anchored regex-location slice with a head map (flags >> 16: its slot in rsl_heads): bit
-// b1 << 8 | b2 is set if a member can match a $uri whose first two bytes are b1 b2 (b2 = 0: a
-// one-byte $uri); k_rloc_heads lists each slice's candidate requests, the slice runs only those
+// rsl_head_key(b0, b1, b2) is set if a member can match a $uri whose first three bytes are b0 b1
+// b2 (0: no byte -- a shorter $uri); k_rloc_heads lists each slice's candidate requests, the slice
+// runs only those
 constexpr uint32_t ALW_SLICE_HEADS = 4;
 constexpr uint32_t RSL_HEAD_WORDS = 65536 / 32;
+// the key of a $uri's first three bytes in a head map: the second and third bytes, XOR-ed with a
+// hash of the first (nearly always '/': a $uri's first byte says little)
+__host__ __device__ constexpr uint32_t rsl_head_key(uint32_t b0, uint32_t b1, uint32_t b2) {
+    return ((b1 << 8) | b2) ^ ((b0 * 0x9E37u) & 0xFFFFu);
+}
+constexpr uint32_t RSL_HEAD_PAIRS = 4096;   // live two-byte starts past which a head map is full
 constexpr uint32_t RSL_HEADS_MAX = 64;
 
 struct TabHeader {
