@@ -28,6 +28,9 @@ int gm_debug_status(struct gm_ctx *ctx, uint32_t *out, size_t n);
 int gm_debug_wire_sizes(struct gm_ctx *ctx, void *stream, uint64_t *out, size_t n);
 /* DServer words of server `sid`, then its (dfa, loc) regex-location pairs; returns words written. */
 int gm_debug_server(struct gm_ctx *ctx, uint32_t sid, uint32_t *out, size_t cap);
+/* The union-DFA slices: 8 u32 each (len, n_groups, zones, server, min_member, flags, states,
+ * classes); returns the u32 count. */
+int gm_debug_alw_slices(struct gm_ctx *ctx, uint32_t *out, size_t cap);
 int gm_debug_waf_keys(struct gm_ctx *ctx, uint32_t *out, size_t cap);
 /* The prefilter's literal table: one row of 4 x uint32 per (key window, pattern) entry --
  * {key, rule id or regex index, (uint16)key_off | len << 16, flags | zones << 8}; returns the

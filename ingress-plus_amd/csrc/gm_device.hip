@@ -2986,6 +2986,26 @@ extern "C" int64_t gm_debug_waf_prefilter2(gm_ctx *c, const uint8_t *A, size_t l
 
 // Server `sid` of the current generation as u32 words (DServer), followed by its regex
 // locations (dfa, loc) pairs; returns the number of words written.
+// The union-DFA slices (always-run, then regex-location): per slice 8 u32 (len, n_groups, zones,
+// server, min_member, flags, states, classes summed over its groups) -- diagnostics
+extern "C" int gm_debug_alw_slices(gm_ctx *c, uint32_t *out, size_t cap) {
+    if (!c || !c->gen || !out) return -1;
+    const TabHeader &h = c->gen->hdr;
+    const uint8_t *b = c->gen->host_image.data();
+    const DAlwSlice *sls = reinterpret_cast<const DAlwSlice *>(b + h.off_alw_slices);
+    const DAlwGroup *grs = reinterpret_cast<const DAlwGroup *>(b + h.off_alw);
+    const uint32_t ns = h.n_alw_slices + h.n_rsl;
+    size_t k = 0;
+    for (uint32_t i = 0; i < ns && k + 8 <= cap; i++) {
+        const DAlwSlice &sl = sls[i];
+        uint32_t st = 0, cl = 0;
+        for (uint32_t g = sl.first_group; g < sl.first_group + sl.n_groups; g++) { st += grs[g].n_states; cl += grs[g].n_classes; }
+        const uint32_t v[8] = {sl.len, sl.n_groups, sl.zones, sl.server, sl.min_member, sl.flags, st, cl};
+        for (uint32_t q = 0; q < 8; q++) out[k++] = v[q];
+    }
+    return (int)k;
+}
+
 extern "C" int gm_debug_server(gm_ctx *c, uint32_t sid, uint32_t *out, size_t cap) {
     if (!c || !c->gen || !out) return -1;
     const TabHeader &h = c->gen->hdr;
