@@ -1465,7 +1465,8 @@ struct Scratch {
     unsigned long long *d_rqm = nullptr; size_t cap_rqm = 0;   // and its prefiltered-slice mask
     uint32_t *d_hlist = nullptr; size_t cap_hlist = 0;         // the anchored slices' candidate lists
     uint32_t *d_along = nullptr; size_t cap_along = 0;         // the always-run slices' long zones + count
-    AlwEmit *d_alwemit = nullptr; size_t cap_alwemit = 0;      // and their emission state
+    uint4 *d_amlist = nullptr; size_t cap_amlist = 0;          // and their match list (AlwMatch)
+    uint32_t *d_amcnt = nullptr; size_t cap_amcnt = 0;         // with a count per slice
     uint32_t *d_hcnt = nullptr; size_t cap_hcnt = 0;           // and their lengths (k_rloc_heads)
     unsigned long long *d_bctr = nullptr; size_t cap_bctr = 0; // this batch's counters (k_ctr_commit)
     uint2 *d_slow = nullptr; size_t cap_slow = 0;              // requests for k_route's SLOW pass
@@ -1506,7 +1507,7 @@ struct Scratch {
                         (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm, (void *)d_rqu, (void *)d_bctr, (void *)d_slow,
                         (void *)d_redo, (void *)d_rlist, (void *)d_rsize, (void *)d_rbase, (void *)d_rtemp, (void *)d_rsreq,
                         (void *)d_rsarena, (void *)d_rsout, (void *)d_rsblk, (void *)d_rscnt, (void *)d_ovlog, (void *)d_wmsg, (void *)d_spill, (void *)d_spill2,
-                        (void *)d_hlist, (void *)d_hcnt, (void *)d_along, (void *)d_alwemit})
+                        (void *)d_hlist, (void *)d_hcnt, (void *)d_along, (void *)d_amlist, (void *)d_amcnt})
             if (p) (void)hipFree(p);
         if (h_status) (void)hipHostFree(h_status);
         if (h_ovlog) (void)hipHostFree(h_ovlog);
@@ -1885,28 +1886,35 @@ static int launch_always(gm_ctx *c, hipStream_t s, const Generation *g, const ui
         HIPCHK(c, hipGetLastError());
     }
     const uint32_t *LL = S->d_along, *LC = S->d_along + lcap;
-    // the slices' emission state, in device memory (AlwEmit; stream-ordered by a one-lane kernel)
-    AlwEmit *EM = nullptr;
+    // the slices' match lists (AlwMatch): one region reused slice after slice, a count per slice;
+    // k_alw_emit turns each slice's matches into pairs right after it
+    AlwMatch am{};
     if (t.n_alw_slices) {
         int e;
-        if ((e = grow(c, s, S->d_alwemit, S->cap_alwemit, 1))) return e;
-        EM = S->d_alwemit;
-        k_put_emit<<<1, 64, 0, s>>>(EM, AlwEmit{dd, S->d_pairs, (uint32_t)S->cap_pairs, t.alw_rule, t.alw_rl});
-        HIPCHK(c, hipGetLastError());
+        const size_t mcap = ((size_t)n / 4 + 65536) * S->list_mult;
+        if ((e = grow(c, s, S->d_amlist, S->cap_amlist, mcap)) ||
+            (e = grow(c, s, S->d_amcnt, S->cap_amcnt, (size_t)t.n_alw_slices)))
+            return e;
+        HIPCHK(c, hipMemsetAsync(S->d_amcnt, 0, (size_t)t.n_alw_slices * 4, s));
+        am = AlwMatch{S->d_amlist, S->d_amcnt, (uint32_t)std::min<size_t>(S->cap_amlist, 0xFFFFFFFFu), dd.redo, dd.status};
     }
     for (uint32_t k = 0; k < t.n_alw_slices; k++) {
         const DAlwSlice &sl = sls[k];
         const dim3 grid((uint32_t)c->cu_count), blk(1024);
+        AlwMatch amk = am;
+        amk.count = am.count + k;
         switch (sl.n_groups) {
-        case 1: k_waf_always_multi<1><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
-        case 2: k_waf_always_multi<2><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
-        case 3: k_waf_always_multi<3><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
-        case 4: k_waf_always_multi<4><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
-        case 5: k_waf_always_multi<5><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
-        case 6: k_waf_always_multi<6><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
-        case 7: k_waf_always_multi<7><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
-        default: k_waf_always_multi<8><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, EM, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 1: k_waf_always_multi<1><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, amk, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 2: k_waf_always_multi<2><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, amk, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 3: k_waf_always_multi<3><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, amk, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 4: k_waf_always_multi<4><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, amk, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 5: k_waf_always_multi<5><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, amk, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 6: k_waf_always_multi<6><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, amk, skip_empty, dlen, k, LL, LC, lcap); break;
+        case 7: k_waf_always_multi<7><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, amk, skip_empty, dlen, k, LL, LC, lcap); break;
+        default: k_waf_always_multi<8><<<grid, blk, sl.len, s>>>(A, alen, reqs, n, t, dd.out, amk, skip_empty, dlen, k, LL, LC, lcap); break;
         }
+        HIPCHK(c, hipGetLastError());
+        k_alw_emit<<<(uint32_t)c->cu_count * 2, 256, 0, s>>>(t, am.list, amk.count, am.cap, S->d_pairs, (uint32_t)S->cap_pairs, dd);
         HIPCHK(c, hipGetLastError());
     }
     if (t.n_always > t.n_always_lds) {
