@@ -58,10 +58,11 @@ extern "C" {
  * the oracle; reported in gm_stats_t.scratch_scale */
 #define GM_CREATE_SCRATCH_SHIFT(k) (((uint32_t)(k) & 0xFFu) << 8)
 /* test hook: the WAF dedupe set at 2^-k of its default capacity too (bits 16..23), so a batch
- * overflows it (OV_SET) and gm_sync's re-run with the set doubled is exercised */
+ * overflows it (OV_SET) and gm_sync's continuation is exercised */
 #define GM_CREATE_SET_SHIFT(k) (((uint32_t)(k) & 0xFFu) << 16)
-/* test hook: the spill of the pairs a full set refuses at 2^-k of its capacity (bits 24..31), so that
- * it overflows too and gm_sync's continuation redoes the requests it missed */
+/* test hook: the spill of the pairs a full set refuses, and the always-run slices' match list, at
+ * 2^-k of their capacity (bits 24..31), so that they overflow and gm_sync's continuation redoes the
+ * requests they missed */
 #define GM_CREATE_SPILL_SHIFT(k) (((uint32_t)(k) & 0xFFu) << 24)
 
 /* ---------------------------------------------------------------- packed request record

@@ -1891,12 +1891,16 @@ static int launch_always(gm_ctx *c, hipStream_t s, const Generation *g, const ui
     AlwMatch am{};
     if (t.n_alw_slices) {
         int e;
-        const size_t mcap = ((size_t)n / 4 + 65536) * S->list_mult;
+        // (GM_CREATE_SCRATCH_SHIFT scales it, GM_CREATE_SPILL_SHIFT shrinks it: the test hooks of
+        // the lists whose overflow gm_sync completes)
+        const size_t mcap = std::max<size_t>(
+            (size_t)((double)(((size_t)n / 4 + 65536) * S->list_mult) * c->cap_scale) >> c->spill_shift, 16);
         if ((e = grow(c, s, S->d_amlist, S->cap_amlist, mcap)) ||
             (e = grow(c, s, S->d_amcnt, S->cap_amcnt, (size_t)t.n_alw_slices)))
             return e;
         HIPCHK(c, hipMemsetAsync(S->d_amcnt, 0, (size_t)t.n_alw_slices * 4, s));
-        am = AlwMatch{S->d_amlist, S->d_amcnt, (uint32_t)std::min<size_t>(S->cap_amlist, 0xFFFFFFFFu), dd.redo, dd.status};
+        am = AlwMatch{S->d_amlist, S->d_amcnt, (uint32_t)std::min<size_t>(std::min(mcap, S->cap_amlist), 0xFFFFFFFFu), dd.redo,
+                      dd.status};
     }
     for (uint32_t k = 0; k < t.n_alw_slices; k++) {
         const DAlwSlice &sl = sls[k];

@@ -299,6 +299,21 @@ def test_internal_overflow_completes_on_device(torch_dev, scale, want):
     assert_verdicts_equal(got, exp, gh, eh, f"overflow continuation (scale {scale})")
 
 
+def test_always_match_list_overflow_redoes_requests(torch_dev):
+    """The always-run slices' match list (k_waf_always_multi -> k_alw_emit) shrunk to 16 entries
+    (GM_CREATE_SPILL_SHIFT(12)): the matches past it mark their requests, gm_sync redoes them as a
+    sub-batch, and the batch -- GM_OK -- equals the oracle."""
+    ss, b = workloads.c4_stress_generation()
+    reqs, arena = records.gen_c4(6_000, ss, seed=workloads.C4_STRESS_POOL_SEED + 11, plant_rate=0.3, stress=True)
+    e = engine.Engine(0, spill_shift=12)
+    e.load(b, 5)
+    got, gh = e.match_host(reqs, arena)          # no GmError
+    st = e.stats()
+    assert st["last_redo"] > 0, st               # the overflow was taken by the redo continuation
+    exp, eh = Oracle(b, 5).match(reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, "always-run match list overflow")
+
+
 def test_job_list_overflow_runs_jobs_from_set(torch_dev):
     """Factor regexes that are not prefix-mode (k_waf_regex jobs) with a shrunken job list: the
     jobs run from the dedupe set and every hit equals the oracle's."""
