@@ -242,8 +242,8 @@ typedef struct gm_stats_t {
      * pairs the full set refused that the spill held (emitted from it with no stage re-run) */
     uint32_t last_redo;
     uint32_t last_spill;
-    /* of n_rsl_slices: anchored slices run only over the requests their head map admits (the
-     * first two $uri bytes) */
+    /* of n_rsl_slices: anchored and reversed slices run only over the requests their head map
+     * admits (the first, or for a reversed slice the last, three $uri bytes) */
     uint32_t n_rsl_heads;
 } gm_stats_t;
 

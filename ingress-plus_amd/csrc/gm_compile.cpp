@@ -2284,7 +2284,13 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             std::vector<std::vector<uint32_t>> heads(D.n_rloc);
             for (uint32_t k = 0; k < D.n_rloc; k++) {
                 const Dfa &rv = rloc_rev[D.first_rloc + k];
-                if (rv.n_states > 0) { rcomps[k] = &rv; ord_r.push_back(k); }
+                if (rv.n_states > 0) {
+                    rcomps[k] = &rv;
+                    ord_r.push_back(k);
+                    // (a reversed DFA reads the $uri from its end: its heads are the last bytes)
+                    heads[k].assign(RSL_HEAD_WORDS, 0u);
+                    dfa_heads(rv, heads[k]);
+                }
                 else if (comps[k]->anchored_start) {
                     ord_a.push_back(k);
                     heads[k].assign(RSL_HEAD_WORDS, 0u);
@@ -2312,9 +2318,10 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             };
             std::vector<uint32_t> hb(rcomps.size(), 0), h0(rcomps.size(), 0);
             for (uint32_t k : ord_a) { hb[k] = breadth(k); h0[k] = head0(k); }
-            std::stable_sort(ord_a.begin(), ord_a.end(), [&](uint32_t a, uint32_t b) {
-                return hb[a] != hb[b] ? hb[a] < hb[b] : h0[a] < h0[b];
-            });
+            for (uint32_t k : ord_r) { hb[k] = breadth(k); h0[k] = head0(k); }
+            auto by_heads = [&](uint32_t a, uint32_t b) { return hb[a] != hb[b] ? hb[a] < hb[b] : h0[a] < h0[b]; };
+            std::stable_sort(ord_a.begin(), ord_a.end(), by_heads);
+            std::stable_sort(ord_r.begin(), ord_r.end(), by_heads);
             std::vector<std::vector<uint32_t>> gm_a, gm_un, gm_uf, gm_r;
             std::vector<MultiDfa> gd_a, gd_un, gd_uf, gd_r;
             std::vector<uint32_t> single;
@@ -2334,10 +2341,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 for (size_t k = s0; k < alw_slices.size(); k++) alw_slices[k].flags |= flags;
                 return (uint32_t)(alw_slices.size() - s0);
             };
-            st.n_rsl_reversed += pack_kind(gm_r, gd_r, ALW_SLICE_REVERSED);
-            const size_t a0 = alw_slices.size();
-            pack_kind(gm_a, gd_a, 0);
-            // each anchored slice's head map: the OR of its members'
+            // each anchored or reversed slice's head map: the OR of its members'
+            auto assign_heads = [&](size_t a0) {
             for (size_t k = a0; k < alw_slices.size(); k++) {
                 const uint32_t slot = (uint32_t)(rsl_heads.size() / RSL_HEAD_WORDS);
                 if (slot >= RSL_HEADS_MAX) break;
@@ -2352,6 +2357,13 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 alw_slices[k].flags |= ALW_SLICE_HEADS | slot << 16;
                 rsl_head_slice.push_back((uint32_t)k);
             }
+            };
+            const size_t r0 = alw_slices.size();
+            st.n_rsl_reversed += pack_kind(gm_r, gd_r, ALW_SLICE_REVERSED);
+            assign_heads(r0);
+            const size_t a0 = alw_slices.size();
+            pack_kind(gm_a, gd_a, 0);
+            assign_heads(a0);
             pack_kind(gm_un, gd_un, 0);
             pack_kind(gm_uf, gd_uf, 0);
             D.rsl_n = (uint32_t)alw_slices.size() - D.rsl_first;

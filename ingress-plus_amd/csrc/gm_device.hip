@@ -2232,7 +2232,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
                 for (uint32_t h0 = 0; h0 < nh; h0 += HEADS_LDS_SLOTS) {
                     const uint32_t k = std::min<uint32_t>(HEADS_LDS_SLOTS, nh - h0);
                     k_rloc_heads<<<(uint32_t)c->cu_count, 1024, k * RSL_HEAD_WORDS * 4, rs>>>(
-                        t, q.st, q.u, q.count, t.rsl_head_slice, h0, k, S->d_hlist, n, S->d_hcnt);
+                        A, t, q.st, q.u, q.count, t.rsl_head_slice, h0, k, S->d_hlist, n, S->d_hcnt);
                     HIPCHK(c, hipGetLastError());
                 }
                 static const bool trace_heads = getenv("GM_TRACE_HEADS") != nullptr;
