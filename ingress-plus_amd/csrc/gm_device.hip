@@ -2961,7 +2961,7 @@ extern "C" int64_t gm_debug_waf_prefilter(gm_ctx *c, const uint8_t *A, size_t le
     for (size_t p = 0; p + 4 <= len; p += 2) {   // even offsets only (stride-2 scan)
         uint32_t w;
         memcpy(&w, A + p, 4);
-        const BloomProbe b = bloom_probe(fold4(w), h.bloom_mul, h.bloom_pk);
+        const BloomProbe b = scan_probe(fold4(w), h.bloom_mul, h.bloom_pk);
         if ((bloom[b.block] & b.mask) == b.mask) { if ((size_t)k < cap && out) out[k] = p; k++; }
     }
     return k;
@@ -2980,7 +2980,7 @@ extern "C" int64_t gm_debug_waf_prefilter2(gm_ctx *c, const uint8_t *A, size_t l
         uint32_t w;
         memcpy(&w, A + p, 4);
         w = fold4(w);
-        const BloomProbe b = bloom_probe(w, h.bloom_mul, h.bloom_pk);
+        const BloomProbe b = scan_probe(w, h.bloom_mul, h.bloom_pk);
         if ((bloom[b.block] & b.mask) != b.mask) continue;
         const int64_t q = (int64_t)p;
         const uint32_t l2 = fb(q - 2) | fb(q - 1) << 8, r2 = fb(q + 4) | fb(q + 5) << 8;

@@ -481,6 +481,14 @@ __host__ __device__ inline BloomProbe bloom_probe(uint32_t w, uint32_t mul, uint
     else for (uint32_t q = 0; q < pk; q++) m |= pk_bits(hi >> (4 * q));
     return BloomProbe{lo >> (32 - BLOOM_LOG2), m};
 }
+// The scan filter's probe (waf_a, k_waf_scan).  Measured, not kept: the block from bits 2 .. 16
+// of hi (its LDS byte address one v_and, 8 fewer VALU ops per KiB chunk) with the bit positions
+// from hi ^ lo -- 15 % more scan candidates, C4 step 4.79 vs 4.65 ms; and K = 8 bits as two per
+// byte (perm_bits of hi and of hi rotated by 3): as many candidates as K = 4 (most are windows
+// that are keys, not filter collisions).
+__host__ __device__ inline BloomProbe scan_probe(uint32_t w, uint32_t mul, uint32_t pk) {
+    return bloom_probe(w, mul, pk);
+}
 // Stage-2 context filter (waf_b, same size as the scan Bloom filter; staged into LDS by
 // k_waf_ctx).  A scan candidate window w at arena offset p survives only if waf_b holds w
 // together with the folded bytes around it that its pattern fixes: up to two on the left
