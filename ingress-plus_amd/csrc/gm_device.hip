@@ -3403,12 +3403,11 @@ extern "C" int gm_upstream_uris(gm_ctx *c, const gm_batch *in, const gm_verdict 
 // came from the product build.  Every GM_EXP_* macro is a measurement (timing) variant; the
 // tuning macros count when they differ from the shipped values.
 static constexpr uint32_t kBuildFlags =
-#if defined(GM_EXP_COUNT) || defined(GM_EXP_CMASK) || defined(GM_EXP_ROUTE_AFTER) || defined(GM_EXP_ROUTE_FIRST) || \
-    defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_SCAN_NOBRANCH) || defined(GM_SCAN_VMASK) || \
-    defined(GM_EXP_ALW_NOEMIT) || defined(GM_EXP_ALW_COUNT)
+#if defined(GM_EXP_COUNT) || defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_EXP_ALW_NOEMIT) || \
+    defined(GM_EXP_ALW_COUNT)
     GM_BUILD_EXPERIMENT |
 #endif
-#if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_PIPE != 1 || GM_SCAN_STG != 32 || \
+#if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_STG != 32 || \
     GM_ROUTE_BPC != 1 || GM_ROUTE_PRIO != 0 || GM_ROUTE_WPE != GM_ROUTE_WPE_SHIPPED || GM_EXP_GRIDMUL != 8 || \
     GM_EXP_WPE != 3 || GM_RLOC_CTX != 1 || GM_RLOC_PREF != 0 || GM_ALW_SLICE_GROUPS != 8 || GM_WIRE_WPE != 8 || \
     GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1 || GM_EXACT_BPC != 6 || !defined(GM_DFA_INL_SHIPPED)
