@@ -420,7 +420,7 @@ def stress_leg(torch, engine, records, workloads, args, local):
 # --kernel-trace --stats run and the PMC passes of scripts/pmc.sh on the same tree), stamped with
 # the hash of the kernel sources.  Selected by name, and used only when that hash matches the tree
 # being benched: a new kernel never pairs with an old profile (VERDICT r2 "Next round" 1).
-SCAN_PROFILE = "profiles/r5c_scan_profile.json"
+SCAN_PROFILE = "profiles/r5f_scan_profile.json"
 
 
 def profiled(zone_bytes: int) -> dict:
