@@ -189,6 +189,9 @@ def main():
     dbg = eng.debug_status()
     log(f"[rank {rank}] status words: records {dbg[5]}, anchored-DFA bytes {dbg[8]} (max/lane {dbg[9]}), "
         f"full literal matches {dbg[10]}")
+    if dbg[40:48].any():   # GM_EXP_EXACT_CNT builds (measurement): the exact check's probe counts
+        log(f"[rank {rank}] exact-check counts: survivors {dbg[45]}, bucket probes {dbg[40]} (max {dbg[41]}), "
+            f"buckets hit {dbg[47]}, check-word rounds {dbg[42]} (max bucket {dbg[43]}), literal compares {dbg[44]}")
     log(f"[rank {rank}] {args.steps} steps in {elapsed:.3f}s; candidates {s['last_candidates']}, ctx-pass {s['last_ctx_pass']}, jobs {s['last_jobs']}, pairs "
         f"{s['last_pairs']}, hits {s['last_hits']}; ms route {np.mean(route_ms):.3f} scan {np.mean(scan_ms):.3f} "
         f"verify {np.mean(verify_ms):.3f} tail {np.mean(tail_ms):.3f}")
@@ -227,7 +230,7 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
                      "algorithmic_bytes_per_launch": zone_bytes},
     }
-    result["roofline"].update(profiled(zone_bytes))
+    result["roofline"].update(profiled(zone_bytes, st["csrc_hash"]))
     if st["build_flags"]:
         result["build"] = f"nondefault (build_flags {st['build_flags']:#x})"
     if world == 1 and not args.serial and not args.no_alone:
@@ -423,17 +426,24 @@ def stress_leg(torch, engine, records, workloads, args, local):
 SCAN_PROFILE = "profiles/r5f_scan_profile.json"
 
 
-def profiled(zone_bytes: int) -> dict:
+def profiled(zone_bytes: int, lib_hash: str) -> dict:
     """roofline fields from the committed same-tree profile: `traffic` (HBM read bytes per
     k_waf_scan launch, 2 x FETCH_SIZE x 1024 per the gfx950 correction in MI355X_MICROARCH.md),
     the LDS bank-conflict rate of the Bloom probes (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE), and
     `frac_profiled` = zone bytes / the rocprofv3 average k_waf_scan duration / HBM peak.  Counters
-    cannot be read inside the timed run, so these come from the profile, named with its source."""
+    cannot be read inside the timed run, so these come from the profile, named with its source.
+    The profile pairs with the LIBRARY benched: `lib_hash` is the source hash libgpumatch.so was
+    built from (gm_stats_t.csrc_hash), so a stale prebuilt library never pairs with a profile of
+    newer sources; `tree_hash` (the sources beside it) is reported for comparison."""
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     from scan_profile import csrc_hash
-    here = csrc_hash(ROOT)
+    here = lib_hash
+    tree = csrc_hash(ROOT)
     path = os.path.join(ROOT, SCAN_PROFILE)
-    out = {"traffic": None, "frac_profiled": None, "csrc_hash": here}
+    out = {"traffic": None, "frac_profiled": None, "csrc_hash": here, "tree_hash": tree,
+           "anchor": "frac_profiled (rocprofv3 average of k_waf_scan; `frac` is the HIP-event time on this run)"}
+    if here != tree:
+        out["lib_status"] = f"library built from {here}, sources beside it hash {tree}"
     if not os.path.exists(path):
         out["profile_status"] = f"no profile ({SCAN_PROFILE} missing)"
         return out

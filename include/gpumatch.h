@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 8u   /* 8: PROXY protocol (gm_wire_msg 128 B, $proxy_protocol_addr in gm_req), last_redo;
+#define GM_ABI_VERSION 9u   /* 9: gm_stats_t.csrc_hash, gm_build_hash; 8: PROXY protocol (gm_wire_msg 128 B, $proxy_protocol_addr in gm_req), last_redo;
                                7: GM_ACT_TOO_LARGE, GM_REQ_CHUNKED, gm_rejects, build flags; 6: n_rsl_reversed;
                                5: gm_update_upstream / gm_peers_migrate; 4: union-DFA stats */
 
@@ -165,6 +165,12 @@ enum {
 };
 
 enum { GM_ROUTE_NONE = 0, GM_ROUTE_PLAIN = 1, GM_ROUTE_SPLIT = 2, GM_ROUTE_RULES = 3 };
+/* route_kind bit, only between gm_match_batch and gm_sync: the batch's WAF dedupe set overflowed and
+ * whether this wallarm_mode-block request is blocked is known only once gm_sync completes the batch
+ * (its action reads PROXY meanwhile).  gm_select_peers / gm_upstream_uris enqueued before gm_sync
+ * answer GM_PEER_DEFER for it (no balancer state moves); gm_sync clears the bit.  Every other action
+ * is final when the batch's kernels end, so the match -> peers -> URI chain needs no gm_sync. */
+#define GM_ROUTE_HELD 0x80u
 enum { GM_WAF_OFF = 0, GM_WAF_MONITORING = 1, GM_WAF_SAFE_BLOCKING = 2, GM_WAF_BLOCK = 3 };
 
 /* ---------------------------------------------------------------- generation blob (GMB1)
@@ -245,6 +251,11 @@ typedef struct gm_stats_t {
     /* of n_rsl_slices: anchored and reversed slices run only over the requests their head map
      * admits (the first, or for a reversed slice the last, three $uri bytes) */
     uint32_t n_rsl_heads;
+    uint32_t reserved0;
+    /* the source hash the library was built from (scripts/scan_profile.py csrc_hash: sha256 over
+     * the files of ingress-plus_amd/csrc and include/gpumatch.h, first 16 hex digits as a number; 0 = unknown):
+     * a profile or bench line names the build it measured, not the tree beside it */
+    uint64_t csrc_hash;
 } gm_stats_t;
 
 /* gm_stats_t.build_flags: measurement / test variants compiled into the library.  bench.py refuses
@@ -453,6 +464,9 @@ int         gm_stats(gm_ctx *ctx, gm_stats_t *out);
  * counted and logged, never a Reload error).  Returns the text's length (written up to cap - 1
  * bytes, NUL-terminated), or a negative GM_E_*. */
 int         gm_rejects(gm_ctx *ctx, char *buf, size_t cap);
+/* The source hash the library was built from, 16 lowercase hex digits ("unknown" if the build had
+ * none): the same value as gm_stats_t.csrc_hash, readable without a context or a generation. */
+const char *gm_build_hash(void);
 /* Message of the calling thread's last failing call (thread-local; ctx is not consulted). */
 const char *gm_last_error(gm_ctx *ctx);
 

@@ -1654,9 +1654,21 @@ extern "C" int gm_exp_read(unsigned long long *out) {
     return 0;
 }
 #endif
+extern "C" const char gm_csrc_hash_text[];   // gm_buildid.cpp (the Makefile's source hash)
+static uint64_t csrc_hash_u64() {
+    uint64_t v = 0;
+    for (int k = 0; k < 16; k++) {
+        const char ch = gm_csrc_hash_text[k];
+        const int d = ch >= '0' && ch <= '9' ? ch - '0' : ch >= 'a' && ch <= 'f' ? ch - 'a' + 10 : -1;
+        if (d < 0) return 0;
+        v = v << 4 | (uint64_t)d;
+    }
+    return v;
+}
 extern "C" {
 
 uint32_t gm_abi_version(void) { return GM_ABI_VERSION; }
+const char *gm_build_hash(void) { return gm_csrc_hash_text; }
 
 gm_ctx *gm_create(int hip_device, uint32_t flags) {
     gm_ctx *c = new gm_ctx();
@@ -1833,6 +1845,7 @@ int gm_stats(gm_ctx *c, gm_stats_t *out) {
     if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
     *out = c->gen->stats;
     out->build_flags = build_flags();
+    out->csrc_hash = csrc_hash_u64();
     out->scratch_scale = (float)c->cap_scale;
     out->n_set_reruns = c->n_set_reruns.load();
     out->last_redo = c->last_redo.load();
@@ -2133,9 +2146,12 @@ static int waf_stages(gm_ctx *c, Scratch *S, const Generation *g, const WafCaps 
 // hit emission: offsets by an exclusive scan of the per-request counts (request order), the
 // pairs into their slots, each request's ids sorted (continuation: remap / redo / np1, see
 // k_hits_scatter)
+// the stream's per-request bitmaps: redo bits, then hold bits (Dedup::redo, Dedup::hold)
+static size_t redo_words(uint32_t n) { return ((size_t)n + 31) / 32; }
 static int emit_hits(gm_ctx *c, Scratch *S, const Generation *g, uint32_t n, gm_verdict *out, uint32_t *hit_ids,
                      size_t hit_cap, unsigned long long *ctr, const Dedup &dd, const uint32_t *redo, uint32_t np1,
-                     const uint32_t *remap, const unsigned long long *spill = nullptr, uint32_t nspill = 0) {
+                     const uint32_t *remap, const unsigned long long *spill = nullptr, uint32_t nspill = 0,
+                     bool cont = false) {
     hipStream_t s = S->stream;
     size_t scan_tmp = 0;
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, scan_tmp, S->d_cnt, S->d_start, (int)n + 1, s));
@@ -2146,7 +2162,7 @@ static int emit_hits(gm_ctx *c, Scratch *S, const Generation *g, uint32_t n, gm_
                                                               redo, np1, remap, spill, nspill);
     HIPCHK(c, hipGetLastError());
     k_hits_finalize<<<std::max<uint32_t>(1, std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8)), 256, 0, s>>>(
-        S->d_start, n, out, hit_ids, hit_cap, S->d_status);
+        S->d_start, n, out, hit_ids, hit_cap, S->d_status, S->d_redo, S->d_redo + redo_words(n), cont ? 1u : 0u);
     HIPCHK(c, hipGetLastError());
     return GM_OK;
 }
@@ -2293,13 +2309,13 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     WafCaps k{};
     if ((e = waf_buffers(c, S, alen, n, k))) return e;
     if ((e = grow(c, s, S->d_blk2rec, S->cap_blk, nblk))) return e;
-    if ((e = grow(c, s, S->d_redo, S->cap_redo, ((size_t)n + 31) / 32))) return e;
-    HIPCHK(c, hipMemsetAsync(S->d_redo, 0, (((size_t)n + 31) / 32) * 4, s));
+    if ((e = grow(c, s, S->d_redo, S->cap_redo, 2 * redo_words(n)))) return e;
+    HIPCHK(c, hipMemsetAsync(S->d_redo, 0, 2 * redo_words(n) * 4, s));
     // one epoch per batch (two with decoders: the decoded pass's jobs take epoch + 1)
     if ((e = next_epoch(c, S, t))) return e;
     const size_t spill_cap = spill_cap_of(c, S);
     Dedup dd{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, out, S->d_cnt, S->d_status, S->d_redo,
-             S->d_spill, (uint32_t)std::min<size_t>(spill_cap, 0xFFFFFFFFu)};
+             S->d_spill, (uint32_t)std::min<size_t>(spill_cap, 0xFFFFFFFFu), S->d_redo + redo_words(n)};
 
     // ---- fork: k_route on the side stream, beside the WAF scan (independent inputs; its waves
     // fit beside the scan's one workgroup per CU; issued after the scan so the scan claims the
@@ -2449,7 +2465,7 @@ static int spill_continuation(gm_ctx *c, Scratch *S, const Scratch::Replay &rp, 
     if (nspill && (e = sort_spill(c, S, nspill, nullptr, dd0, sp))) return e;
     k_clear_held<<<1, 64, 0, s>>>(S->d_status);
     HIPCHK(c, hipGetLastError());
-    if ((e = emit_hits(c, S, g, rp.n, rp.out, rp.hits, rp.hit_cap, S->d_bctr, dd0, nullptr, 0, nullptr, sp, nspill)))
+    if ((e = emit_hits(c, S, g, rp.n, rp.out, rp.hits, rp.hit_cap, S->d_bctr, dd0, nullptr, 0, nullptr, sp, nspill, true)))
         return e;
     const size_t nctr = std::max<size_t>(g->n_counters, 1);
     k_ctr_commit<<<std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)((nctr + 255) / 256), (uint32_t)c->cu_count)), 256, 0, s>>>(
@@ -2563,7 +2579,7 @@ static int set_continuation(gm_ctx *c, Scratch *S, const Scratch::Replay &rp, ui
     const Dedup dd0{S->d_set, (uint32_t)(S->cap_set - 1), S->epoch, S->epoch, rp.out, S->d_cnt, S->d_status, nullptr,
                     nullptr, 0u};
     if ((e = emit_hits(c, S, g, n, rp.out, rp.hits, rp.hit_cap, S->d_bctr, dd0, S->d_redo, np1, S->d_rlist, sp,
-                       nspill))) return e;
+                       nspill, true))) return e;
     const size_t nctr = std::max<size_t>(g->n_counters, 1);
     k_ctr_commit<<<std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)((nctr + 255) / 256), (uint32_t)c->cu_count)), 256, 0, s>>>(
         S->d_bctr, g->d_counters, (uint32_t)g->n_counters, S->d_status, S->d_ovlog + rp.slot);
@@ -3404,7 +3420,7 @@ extern "C" int gm_upstream_uris(gm_ctx *c, const gm_batch *in, const gm_verdict 
 // tuning macros count when they differ from the shipped values.
 static constexpr uint32_t kBuildFlags =
 #if defined(GM_EXP_COUNT) || defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_EXP_ALW_NOEMIT) || \
-    defined(GM_EXP_ALW_COUNT)
+    defined(GM_EXP_ALW_COUNT) || GM_EXP_EXACT || defined(GM_EXP_EXACT_CNT)
     GM_BUILD_EXPERIMENT |
 #endif
 #if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_STG != 32 || \

@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GM_LIB") or os.path.join(os.path.dirname(HERE), "libgpumatch.so")
 
 GM_OK = 0
-GM_ABI_VERSION = 8   # include/gpumatch.h
+GM_ABI_VERSION = 9   # include/gpumatch.h
 GM_E_OVERFLOW = -4
 GM_E_STALE = -9
 GM_E_COMM = -7
@@ -66,7 +66,8 @@ class GmStats(ctypes.Structure):
                 [("scratch_scale", ctypes.c_float), ("n_set_reruns", ctypes.c_uint32),
                  ("set_shift", ctypes.c_uint32), ("n_alw_members", ctypes.c_uint32),
                  ("last_redo", ctypes.c_uint32), ("last_spill", ctypes.c_uint32),
-                 ("n_rsl_heads", ctypes.c_uint32)])
+                 ("n_rsl_heads", ctypes.c_uint32), ("reserved0", ctypes.c_uint32),
+                 ("csrc_hash", ctypes.c_uint64)])
 
 
 class GmBatch(ctypes.Structure):
@@ -78,7 +79,7 @@ EXPORTS = ["gm_create", "gm_destroy", "gm_abi_version", "gm_load_generation", "g
            "gm_counters", "gm_counters_reset", "gm_comm_unique_id", "gm_comm_init", "gm_counters_allreduce",
            "gm_stats", "gm_last_error", "gm_normalize_uris", "gm_counters_global", "gm_parse_requests",
            "gm_peers_init", "gm_select_peers", "gm_release_peers", "gm_peer_address", "gm_upstream_uris",
-           "gm_update_upstream", "gm_peers_migrate", "gm_rejects"]
+           "gm_update_upstream", "gm_peers_migrate", "gm_rejects", "gm_build_hash"]
 
 # gm_peer_state (include/gpumatch.h)
 PEER_STATE_DTYPE = np.dtype([("conns", "<u4"), ("current_weight", "<i4"), ("flags", "<u4"), ("reserved", "<u4")])
@@ -131,10 +132,17 @@ def lib():
         L.gm_upstream_uris.argtypes = [ctypes.c_void_p, ctypes.POINTER(GmBatch), ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.gm_rejects.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
+        L.gm_build_hash.restype = ctypes.c_char_p
+        L.gm_build_hash.argtypes = []
         L.gm_last_error.restype = ctypes.c_char_p
         L.gm_last_error.argtypes = [ctypes.c_void_p]
         _lib = L
     return _lib
+
+
+def build_hash() -> str:
+    """gm_build_hash: the source hash the loaded library was built from (16 hex digits)."""
+    return lib().gm_build_hash().decode()
 
 
 class GmError(RuntimeError):
@@ -187,6 +195,7 @@ class Engine:
         d["n_rsl_heads"] = s.n_rsl_heads
         d["set_shift"] = s.set_shift
         d["n_alw_members"] = s.n_alw_members
+        d["csrc_hash"] = f"{s.csrc_hash:016x}" if s.csrc_hash else "unknown"
         return d
 
     def rejects(self) -> list:

@@ -43,6 +43,9 @@ def scan_stats(path: str) -> dict:
 
 
 def main():
+    if sys.argv[1:] == ["--hash"]:   # the Makefile's stamp (gm_buildid.cpp)
+        print(csrc_hash())
+        return
     tag, stats = sys.argv[1], sys.argv[2]
     rec = {"tag": tag, "csrc_hash": csrc_hash(), "kernel_stats": os.path.basename(stats)}
     rec.update(scan_stats(stats))

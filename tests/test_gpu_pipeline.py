@@ -479,3 +479,62 @@ def test_two_batches_before_one_sync(torch_dev):
     assert_verdicts_equal(got_b, exp_b, gh_b, eh_b, "queued batch B after a void A")
     assert np.array_equal(e.counters(), _one_batch_counters(e, got_b, gh_b))
     e.close()
+
+
+GM_ROUTE_HELD = 0x80
+
+
+@pytest.mark.parametrize("set_shift,spill_shift", [(None, 0), (0, 12), (None, 12)])
+def test_held_verdicts_before_sync(torch_dev, set_shift, spill_shift):
+    """a batch whose dedupe set (or spill, or always-run match list) overflowed is
+    completed by gm_sync, but the documented chain match -> gm_select_peers -> gm_upstream_uris runs
+    on the stream BEFORE gm_sync.  Every action the first pass can settle is final when its kernels
+    end (a refused true hit blocks at once); a wallarm-block request whose hits only the continuation
+    knows is marked GM_ROUTE_HELD with action PROXY, and the peer selection enqueued before gm_sync
+    answers GM_PEER_DEFER for exactly those.  After gm_sync every verdict equals the oracle's and no
+    HELD mark remains."""
+    torch, dev = torch_dev
+    ss, b = workloads.c4_stress_generation()
+    reqs, arena = records.gen_c4(6_000, ss, seed=workloads.C4_STRESS_POOL_SEED + 9, plant_rate=0.3, stress=True)
+    n = len(reqs)
+    if set_shift is None:   # a set below the batch's unique keys (as test_set_overflow_continuation)
+        probe = engine.Engine(0)
+        probe.load(b, 5)
+        probe.match_host(reqs, arena)
+        st = probe.stats()
+        keys = st["last_pairs"] + st["last_jobs"]
+        probe.close()
+        set_shift = 1
+        while (1 << 19) >> (set_shift + 1) >= keys // 2 and set_shift < 12:
+            set_shift += 1
+    e = engine.Engine(0, set_shift=set_shift, spill_shift=spill_shift)
+    e.load(b, 5)
+    n_peers = e.stats()["n_peers"]
+    state = torch.zeros(max(n_peers, 1) * 16, dtype=torch.uint8, device=dev)
+    e.peers_init_ptr(state.data_ptr(), n_peers, 0)
+    d_reqs, d_arena = _to_dev(torch, dev, reqs, arena)
+    d_out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    d_hits = torch.zeros(8 * n + 1024, dtype=torch.int32, device=dev)
+    d_peer = torch.zeros(n, dtype=torch.int32, device=dev)
+    e.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), len(arena), n, d_out.data_ptr(), d_hits.data_ptr(),
+                d_hits.numel(), 0)
+    e.select_peers_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), len(arena), n, d_out.data_ptr(), state.data_ptr(),
+                       n_peers, d_peer.data_ptr(), 0)
+    torch.cuda.synchronize()   # the kernels are done; gm_sync has not run
+    pre = d_out.cpu().numpy().view(records.VERDICT_DTYPE).copy()
+    peer = d_peer.cpu().numpy().view(np.uint32).copy()
+    assert int(e.debug_status()[3]) & (16 | 512 | 1024), "no set / spill overflow: the test exercises nothing"
+    e.sync(0)
+    got = d_out.cpu().numpy().view(records.VERDICT_DTYPE)
+    gh = d_hits[:e.stats()["last_hits"]].cpu().numpy().view(np.uint32)
+    exp, eh = Oracle(b, 5).match(reqs, arena)
+    assert_verdicts_equal(got, exp, gh, eh, f"held batch (set shift {set_shift}, spill shift {spill_shift})")
+    assert not (got["route_kind"] & GM_ROUTE_HELD).any(), "gm_sync left a HELD mark"
+    held = (pre["route_kind"] & GM_ROUTE_HELD) != 0
+    assert (pre["action"][held] == 0).all() and (pre["waf_mode"][held] == 3).all()
+    assert (peer[held] == engine.GM_PEER_DEFER).all(), "a held request got a peer before gm_sync"
+    # every other action was already final before gm_sync
+    bad = np.nonzero(~held & (pre["action"] != exp["action"]))[0]
+    assert len(bad) == 0, f"{len(bad)} requests changed action at gm_sync without a HELD mark, e.g. {bad[:5]}"
+    if spill_shift == 12:
+        assert held.any(), "the always-run list overflow marked no request HELD"

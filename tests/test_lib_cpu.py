@@ -4,6 +4,7 @@ generation compiler (host code) behaves -- no classification calls without a GPU
 import ctypes
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -267,3 +268,12 @@ def test_no_kernel_has_a_dynamic_stack(tmp_path):
     assert not dyn, f"kernels with a dynamic stack: {dyn}"
     big = [(n, p) for n, _, p in md if p > PRIVATE_SEGMENT_MAX]
     assert not big, f"kernels over {PRIVATE_SEGMENT_MAX} B of private segment: {big}"
+
+
+def test_library_names_its_sources():
+    """Evidence hygiene: libgpumatch.so carries the hash of the sources it was built
+    from (gm_build_hash, gm_stats_t.csrc_hash); the shipped library must be built from this tree,
+    so a profile stamped with the tree's hash describes the library that runs."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from scan_profile import csrc_hash
+    assert engine.build_hash() == csrc_hash(ROOT)
