@@ -321,8 +321,12 @@ int         gm_comm_init(gm_ctx *ctx, const void *nccl_unique_id, int nranks, in
 /* Sum of every rank's cumulative counters (RCCL all-reduce over xGMI, enqueued on `stream`),
  * OUT OF PLACE: the local counters are untouched, so any number of calls give the true job
  * totals.  gm_counters_global() reads the result of the last call.  Collective: every rank calls
- * it.  The ranks first agree on (gen, n_counters) with one 4-word MAX reduction (synchronous on
- * `stream`); if any rank differs, every rank returns GM_E_COMM and no sum is issued. */
+ * it, the same number of times.  The ranks' agreement on (gen, n_counters) travels inside the sum
+ * (a 10-word block beside the counters), so a call is one collective with no host synchronisation;
+ * the first call, and the call after one whose block showed the ranks apart, agree synchronously
+ * first.  Ranks on different generations or counter spaces: that call's totals are void --
+ * gm_counters_global returns GM_E_COMM on every rank -- and the next call re-agrees (GM_E_COMM on
+ * every rank while they still differ; no collective of mismatched size is ever issued). */
 int         gm_counters_allreduce(gm_ctx *ctx, void *stream);
 int         gm_counters_global(gm_ctx *ctx, uint64_t *out, size_t n);
 
@@ -376,7 +380,8 @@ typedef struct gm_wire_msg {
  * *arena_len_dev (device) receives the arena's length -- hand it to gm_match_batch through
  * gm_batch.arena_len_dev, with arena_cap as gm_batch.arena_len.  A request nginx would reject
  * gets GM_REQ_INVALID and its status (400 / 501 / 505).  arena_cap >= the sum over requests of
- * align16(2 * len + raddr_len) always suffices; gm_sync reports GM_E_OVERFLOW if it is exceeded. */
+ * align16(2 * len + raddr_len + 46) always suffices (46: the record's $proxy_protocol_addr after
+ * raddr); gm_sync reports GM_E_OVERFLOW if it is exceeded. */
 int         gm_parse_requests(gm_ctx *ctx, const uint8_t *wire, const gm_wire_msg *msgs, uint32_t n,
                               gm_req *reqs, uint8_t *arena, uint64_t arena_cap, uint64_t *arena_len_dev,
                               void *stream);

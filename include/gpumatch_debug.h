@@ -49,11 +49,18 @@ int64_t gm_debug_waf_prefilter2(struct gm_ctx *ctx, const uint8_t *A, size_t len
  * out[1] transitions taken in a group's start state that stay there, out[2] transitions taken in
  * the start state, out[3] (group, request, zone) tasks. */
 int gm_debug_alw_profile(gm_ctx *ctx, const gm_req *reqs, const uint8_t *arena, uint32_t n, uint64_t *out4);
-/* gm_counters_allreduce's generation agreement: the 4 words a rank contributes to the MAX
- * reduction (gen, n_counters and their complements to 0xFFFFFFFF), and the verdict on the reduced
- * words (GM_OK: every rank had the same gen and n_counters; GM_E_COMM otherwise). */
-void gm_debug_agree_pack(uint64_t gen, uint64_t n_counters, uint64_t *words4);
-int  gm_debug_agree_check(const uint64_t *max_words4);
+/* gm_counters_allreduce's protocol (RedProto, gm_device.hip) with the caller as the transport:
+ * the block of gm_debug_red_words() u64 words a rank contributes to the SUM, and one state machine
+ * per rank.  begin: 1 = agree first (a block-only collective, then gm_debug_red_agree with its sum),
+ * 0 = issue the combined collective of red_words + *count words at once; finish: the combined
+ * collective's summed block -> GM_OK (valid totals) or GM_E_COMM. */
+void     gm_debug_red_pack(uint64_t gen, uint64_t n_counters, uint64_t *words);
+uint32_t gm_debug_red_words(void);
+void    *gm_debug_red_new(void);
+void     gm_debug_red_free(void *proto);
+int      gm_debug_red_begin(void *proto, uint64_t *count);
+int      gm_debug_red_agree(void *proto, const uint64_t *sum_words);
+int      gm_debug_red_finish(void *proto, const uint64_t *sum_words);
 /* Tests: fn(arg) runs inside every later gm_update_upstream between its read of the live tables and
  * its publish, with no lock held (a gm_load_generation there must make the update fail GM_E_STALE).
  * fn = NULL clears it. */

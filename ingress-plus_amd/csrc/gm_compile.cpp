@@ -1129,7 +1129,11 @@ struct KeyModel {
         const double prior = std::exp2(window_score_w(w));
         if (n == 0) return prior;
         auto it = cnt.find(w);
-        return (it == cnt.end() ? 0.0 : (double)it->second) + n * prior * std::exp2(-28.0);
+        // the model's term is squashed into (0, 1): it ranks the windows the sample does not hold
+        // and never outweighs one observed occurrence (round 6: unsquashed, an unseen window could
+        // score ~350 and lose to one the sample held ~1800 times once the context penalty applied)
+        const double m = n * prior * std::exp2(-28.0);
+        return (it == cnt.end() ? 0.0 : (double)it->second) + m / (1.0 + m);
     }
 };
 
@@ -1153,45 +1157,92 @@ uint16_t prefix_entry(const Dfa &d, const std::string &f, bool nocase) {
 }
 
 // The scan probes only even arena offsets (k_waf_scan), so every pattern is keyed on a set of
-// windows that catches an occurrence at either parity:
-//   >= 5 bytes: two ADJACENT windows (o, o + 1), the pair of least summed cost;
-//   4 bytes:    the pattern itself plus, for odd occurrences, the window one byte to the left
-//               ("Zabc", key_off -1) or to the right ("bcdY", key_off +1) for each of the 128
-//               folded bytes Z / Y -- whichever family is cheaper.
+// windows that catches an occurrence at either parity: an occurrence at an even arena offset is
+// probed at the pattern's even offsets, one at an odd arena offset at its odd offsets, so the keys
+// are one EVEN-offset choice plus one ODD-offset choice, each either
+//   a window inside the pattern (o, o + 4 <= L), or
+//   a family: the window one byte past either end, for each of the 128 folded values of that byte
+//   ("Zabc", key_off -1: odd; "xyzY", key_off L - 3) -- the only choice of a 4-byte pattern's odd
+//   class, and what a 5- or 6-byte pattern takes when its few inside windows are frequent text.
+// Round 6: the two choices are independent (they were an adjacent pair (o, o + 1)): a 5-byte
+// pattern "hipp?" had to key on "hipp", 15 % of the C4 pool's key-window hits.
 struct KeyChoice { std::vector<std::pair<uint32_t, int16_t>> keys; };
-// follow: the bytes that can come right after a 4-byte pattern (regex prefix / factor strings;
-// nullptr = any byte) -- the right-hand family then only needs those
-// use: how many patterns already key on a window.  A >= 5-byte pattern's pair cost is, per
-// window, (benign cost + a floor for attack traffic) x (1 + patterns sharing the key: each is one
-// more literal compare per hit in k_waf_exact) x 8 per missing byte of stage-2 context (the
-// k_waf_ctx filter checks up to two pattern bytes either side of the window).
+// follow: the bytes that can come right after the pattern (regex prefix / factor strings;
+// nullptr = any byte) -- a right-hand family then only needs those
+// use: how many patterns already key on a window.  A window's cost is (benign cost + a floor for
+// attack traffic) x (1 + patterns sharing the key: each is one more literal compare per hit in
+// k_waf_exact) x 8 per missing byte of stage-2 context (the k_waf_ctx filter checks up to two
+// pattern bytes either side of the window); a family adds, per key, the Bloom fill it costs every
+// probed window (kKeyLoad, in the same units).
 KeyChoice choose_keys(const std::string &pat, const KeyModel &M, std::unordered_map<uint32_t, uint32_t> &use,
                       const std::bitset<256> *follow = nullptr) {
     KeyChoice r;
-    if (pat.size() >= 5) {
-        const int L = (int)pat.size();
-        auto wcost = [&](int o) {
-            const uint32_t w = fold4(load4(pat, (size_t)o));
-            auto it = use.find(w);
-            const double share = 1.0 + (it == use.end() ? 0.0 : (double)it->second);
-            const int miss = (2 - std::min(2, o)) + (2 - std::max(0, std::min(2, L - o - 4)));
-            return (M.cost(w) + std::exp2(-30.0)) * share * std::exp2(3.0 * miss);
-        };
-        double best = 1e300; int bo = 0;
-        for (int o = 0; o + 5 <= L; o++) {
-            const double c = wcost(o) + wcost(o + 1);
-            if (c < best * (1 - 1e-12)) { best = c; bo = o; }
+    const int L = (int)pat.size();
+    // one key's share of the Bloom false positives per probed window (4 bits of a 2^20-bit filter
+    // at ~17 % fill: d(f^4)/dn = 16 f^3 / m), scaled like M.cost (sample counts, or a probability)
+    const double kKeyLoad = 3.5e-8 * (M.n > 0 ? M.n : 1.0);
+    auto share = [&](uint32_t w) {
+        auto it = use.find(w);
+        return 1.0 + (it == use.end() ? 0.0 : (double)it->second);
+    };
+    auto ctx_miss = [&](int o) {   // stage-2 context bytes the pattern lacks around window o
+        return (2 - std::max(0, std::min(2, o))) + (2 - std::max(0, std::min(2, L - o - 4)));
+    };
+    auto wcost = [&](int o) {
+        const uint32_t w = fold4(load4(pat, (size_t)o));
+        return (M.cost(w) + std::exp2(-30.0)) * share(w) * std::exp2(3.0 * ctx_miss(o));
+    };
+    std::bitset<256> ys;   // folded right-hand bytes
+    for (uint32_t z = 0; z < 256; z++) if (!follow || (*follow)[z]) ys[z | 0x20u] = true;
+    ys[0x20] = true;   // a pattern that ends the arena: the scan reads the byte past it as 0, folded ' '
+                       // (k_waf_scan probes windows of >= 3 arena bytes)
+    // the family of window o (o = -1: the byte before the pattern varies; o = L - 3: the byte after):
+    // its keys, and its expected candidates -- benign occurrences of its windows plus the Bloom
+    // load of its keys (kKeyLoad each)
+    auto family = [&](int o, std::vector<uint32_t> *out) {
+        double c = 0;
+        const bool left = o < 0;
+        for (uint32_t z = 0; z < 256; z++) {
+            if ((z | 0x20u) != z || (!left && !ys[z])) continue;
+            const uint32_t w = left ? (z | (fold4(load4(pat, 0)) << 8)) : ((fold4(load4(pat, (size_t)L - 4)) >> 8) | (z << 24));
+            if (out) out->push_back(w);
+            else c += M.cost(w) + kKeyLoad;
         }
-        for (int o = bo; o <= bo + 1; o++) {
-            const uint32_t w = fold4(load4(pat, (size_t)o));
-            r.keys.push_back({w, (int16_t)o});
-            use[w]++;
+        return c;
+    };
+    if (L >= 5) {
+        double best[2] = {1e300, 1e300};
+        int bo[2] = {0, 1};
+        for (int o = 0; o + 4 <= L; o++) {
+            const double c = wcost(o);
+            if (c < best[o & 1] * (1 - 1e-12)) { best[o & 1] = c; bo[o & 1] = o; }
+        }
+        // a class whose best inside window is frequent benign text (more expected candidates than a
+        // whole family's Bloom load) takes a family instead when that family expects 4x fewer
+        // candidates: the left one serves the odd class, the right one the class of L - 3
+        int fam[2] = {0, 0};   // 0: inside window; -1: left family; 1: right family
+        for (int cls = 0; cls < 2; cls++) {
+            const double cin = M.cost(fold4(load4(pat, (size_t)bo[cls])));
+            if (cin <= 128 * kKeyLoad) continue;
+            double fb = 1e300;
+            if (cls == 1) { const double f = family(-1, nullptr); if (4 * f < cin && f < fb) { fb = f; fam[cls] = -1; } }
+            if (((L - 3) & 1) == cls) { const double f = family(L - 3, nullptr); if (4 * f < cin && f < fb) { fb = f; fam[cls] = 1; } }
+        }
+        for (int cls = 0; cls < 2; cls++) {
+            if (fam[cls]) {
+                const int o = fam[cls] < 0 ? -1 : L - 3;
+                std::vector<uint32_t> ws;
+                family(o, &ws);
+                for (uint32_t w : ws) { r.keys.push_back({w, (int16_t)o}); use[w]++; }
+            } else {
+                const uint32_t w = fold4(load4(pat, (size_t)bo[cls]));
+                r.keys.push_back({w, (int16_t)bo[cls]});
+                use[w]++;
+            }
         }
         return r;
     }
     const uint32_t w = fold4(load4(pat, 0));
-    std::bitset<256> ys;   // folded right-hand bytes
-    for (uint32_t z = 0; z < 256; z++) if (!follow || (*follow)[z]) ys[z | 0x20u] = true;
     double cl = 0, cr = 0;
     for (uint32_t z = 0; z < 256; z++) {
         if ((z | 0x20u) != z) continue;
@@ -2079,6 +2130,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.n_srcs = (uint32_t)C.srcs.size(); h.n_conds = (uint32_t)C.conds.size(); h.n_chain_heads = (uint32_t)C.chain_heads.size();
     h.n_rules = (uint32_t)C.rules.size(); h.n_splits = (uint32_t)C.splits.size(); h.n_parts = (uint32_t)C.parts.size();
     h.n_dfas = (uint32_t)C.dfas.size();
+    // k_waf_exact's rings carry a literal index in 24 bits (gm_waf.inc XPOS_MASK)
+    if (dlits.size() >= (1u << 24)) { R.code = GM_E_INVAL; R.err = "signature set too large: >= 2^24 prefilter literal rows"; return R; }
     h.n_lit_buckets_cap = lcap; h.n_lits = (uint32_t)dlits.size(); h.n_sig_regex = (uint32_t)sregex.size();
     h.n_always = (uint32_t)always.size(); h.n_sigs = st.n_sigs;
     // ---- union-DFA groups (gm_regex.hpp MultiDfa) packed into LDS slices (gm_tables.hpp

@@ -1427,7 +1427,7 @@ struct Scratch {
     uint32_t *d_status = nullptr, *h_status = nullptr;
     uint32_t *d_blk2rec = nullptr; size_t cap_blk = 0;
     unsigned long long *d_cand = nullptr; size_t cap_cand = 0;
-    unsigned long long *d_surv = nullptr; size_t cap_surv = 0;   // stage-2 survivors (arena offsets)
+    uint4 *d_surv = nullptr; size_t cap_surv = 0;   // stage-2 survivors (gm_waf.inc surv_entry, 16 B)
     unsigned long long *d_pairs = nullptr; size_t cap_pairs = 0; // unique active (request, rule) pairs
     unsigned long long *d_jobs = nullptr; size_t cap_jobs = 0;   // unique (request, regex, zone) jobs
     unsigned long long *d_set = nullptr; size_t cap_set = 0;     // dedupe set (power of two)
@@ -1522,6 +1522,78 @@ struct Scratch {
     }
 };
 
+// ---- gm_counters_allreduce's protocol: the agreement rides in the counter sum.
+// Each rank contributes, beside its counters, a block of RED_WORDS u64 words {1, v, v^2 for the four
+// 16-bit halves v of (gen, n_counters), 0} to one SUM: with N = the summed first word, the ranks
+// hold one value v iff N * sum(v^2) == sum(v)^2 (Cauchy-Schwarz; exact in u64 for N < 2^20).  The
+// collective's count is RED_WORDS + the agreed n on every rank (agreed by the same test, once,
+// synchronously).  A call whose block shows the ranks apart, or on another n, has no valid totals,
+// and the next call re-agrees synchronously; every rank reads the same block, so every rank takes
+// the same branch at the same call and no collective of mismatched size is ever issued.
+constexpr uint32_t RED_WORDS = 10;
+struct RedBlock { unsigned long long w[RED_WORDS]; };
+struct RedProto {
+    bool agreed = false;      // (gen, n) agreed: the combined collective carries RED_WORDS + n words
+    uint32_t gen = 0;
+    uint64_t n = 0;
+    bool last_valid = true;   // the last call's totals are every rank's counters of one space
+    static void pack(uint32_t g, uint64_t cnt, unsigned long long *w) {
+        const uint32_t v[4] = {g & 0xFFFFu, g >> 16, (uint32_t)(cnt & 0xFFFFu), (uint32_t)((cnt >> 16) & 0xFFFFu)};
+        w[0] = 1;
+        for (int i = 0; i < 4; i++) { w[1 + 2 * i] = v[i]; w[2 + 2 * i] = (unsigned long long)v[i] * v[i]; }
+        w[9] = 0;
+    }
+    __host__ __device__ static bool all_equal(const unsigned long long *s, uint32_t &g, uint64_t &cnt) {
+        const unsigned long long N = s[0];
+        if (N == 0) return false;
+        uint32_t v[4];
+        for (int i = 0; i < 4; i++) {
+            if (N * s[2 + 2 * i] != s[1 + 2 * i] * s[1 + 2 * i]) return false;
+            v[i] = (uint32_t)(s[1 + 2 * i] / N);
+        }
+        g = v[0] | v[1] << 16;
+        cnt = (uint64_t)v[2] | (uint64_t)v[3] << 16;
+        return true;
+    }
+    // the block-only collective of a synchronous agreement
+    bool agree(const unsigned long long *s) {
+        uint32_t g; uint64_t m;
+        agreed = all_equal(s, g, m);
+        if (agreed) { gen = g; n = m; } else last_valid = false;
+        return agreed;
+    }
+    // the summed block of a combined collective
+    void finish(const unsigned long long *s) {
+        uint32_t g; uint64_t m;
+        last_valid = all_equal(s, g, m) && m == n;
+        if (last_valid) gen = g; else agreed = false;
+    }
+};
+// [block | the first na counters, zero-padded] -- the rank's contribution (n: its own count)
+__global__ void k_red_stage(const unsigned long long *__restrict__ ctr, uint64_t n, uint64_t na, RedBlock b,
+                            unsigned long long *__restrict__ out) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < RED_WORDS + na; i += (uint64_t)gridDim.x * blockDim.x) {
+        unsigned long long v = 0;
+        if (i < RED_WORDS) {
+#pragma unroll
+            for (uint32_t k = 0; k < RED_WORDS; k++) if (i == k) v = b.w[k];
+        } else if (i - RED_WORDS < n) {
+            v = ctr[i - RED_WORDS];
+        }
+        out[i] = v;
+    }
+}
+// the totals to the generation's reduced buffer, only when the block shows every rank on this
+// count (the same test the host applies to the block afterwards)
+__global__ void k_red_finish(const unsigned long long *__restrict__ sum, uint64_t na, unsigned long long *__restrict__ dst,
+                             uint64_t n) {
+    uint32_t g;
+    uint64_t m;
+    if (!RedProto::all_equal(sum, g, m) || m != na || n != na) return;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < na; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = sum[RED_WORDS + i];
+}
+
 struct gm_ctx {
     int dev = 0;
     uint32_t flags = 0;
@@ -1538,6 +1610,14 @@ struct gm_ctx {
     std::mutex scr_mu;                        // the stream -> scratch map only
     std::map<hipStream_t, std::unique_ptr<Scratch>> scratch;
     ncclComm_t comm = nullptr;
+    // gm_counters_allreduce's protocol state (RedProto) and buffers: [agreement block | counters] in
+    // and out, the last call's summed block (pinned) and its completion event
+    std::mutex red_mu;
+    RedProto red;
+    unsigned long long *d_red = nullptr; size_t cap_red = 0;
+    unsigned long long *h_red = nullptr;
+    hipEvent_t ev_red = nullptr;
+    bool red_pending = false;
     // last completed batch (gm_sync), for gm_stats / gm_debug_status
     std::mutex last_mu;
     uint64_t last_candidates = 0, last_pairs = 0, last_hits = 0, last_ctx_pass = 0, last_jobs = 0;
@@ -1730,6 +1810,9 @@ void gm_destroy(gm_ctx *c) {
         (void)hipDeviceSynchronize();
         c->scratch.clear();
         if (c->comm) ncclCommDestroy(c->comm);
+        if (c->d_red) (void)hipFree(c->d_red);
+        if (c->h_red) (void)hipHostFree(c->h_red);
+        if (c->ev_red) (void)hipEventDestroy(c->ev_red);
     }
     delete c->gen;
     delete c;
@@ -2684,6 +2767,7 @@ int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit
     if (in->n == 0) { HIPCHK(c, hipMemsetAsync(S->d_status, 0, BATCH_STATUS_WORDS * 4, s)); S->ev_pending = false; return GM_OK; }
     if (((uintptr_t)in->arena & 15) || ((uintptr_t)in->reqs & 15) || ((uintptr_t)out & 15))
         return fail(c, GM_E_INVAL, "reqs / arena / out must be 16-byte aligned");
+    if (in->arena_len >> SURV_POS_BITS) return fail(c, GM_E_INVAL, "arena_len must be below 512 GiB");
     if (hit_cap > 0xFFFFFFFFull) hit_cap = 0xFFFFFFFFull;   // hit offsets are u32
     DoneGuard G(S);
     Scratch::Replay rp;
@@ -2756,6 +2840,17 @@ int gm_counters_global(gm_ctx *c, uint64_t *out, size_t n) {
     if (!c->gen) return fail(c, GM_E_NOGEN, "no generation loaded");
     HIPCHK(c, hipSetDevice(c->dev));
     if (int e = wait_done(c)) return e;
+    {
+        std::lock_guard<std::mutex> rl(c->red_mu);
+        if (c->red_pending) {
+            HIPCHK(c, hipEventSynchronize(c->ev_red));
+            c->red_pending = false;
+            c->red.finish(c->h_red);
+        }
+        if (!c->red.last_valid)
+            return fail(c, GM_E_COMM, "the last gm_counters_allreduce found the ranks on different generations or "
+                                      "counter spaces: no totals (the next call re-agrees)");
+    }
     HIPCHK(c, hipMemcpy(out, c->gen->d_counters_sum, std::min(n, c->gen->n_counters) * 8, hipMemcpyDeviceToHost));
     return GM_OK;
 }
@@ -2790,23 +2885,15 @@ int gm_comm_init(gm_ctx *c, const void *uid, int nranks, int rank) {
     return GM_OK;
 }
 
-// The ranks' agreement on the counter space before the sum: every rank contributes
-// {gen, n, 0xFFFFFFFF - gen, 0xFFFFFFFF - n} to one MAX reduction, which yields the largest and
-// (by complement) the smallest gen and n over the ranks; they agree iff the two are equal.  All
-// ranks see the same reduced words, so all take the same branch: on a disagreement none issues
-// the sum (mismatched element counts would hang or corrupt the collective).
-static void agree_pack(uint64_t gen, uint64_t n, unsigned long long w[4]) {
-    w[0] = gen & 0xFFFFFFFFu; w[1] = n & 0xFFFFFFFFu;
-    w[2] = 0xFFFFFFFFull - w[0]; w[3] = 0xFFFFFFFFull - w[1];
-}
-static bool agree_check(const unsigned long long m[4]) {
-    return m[0] == 0xFFFFFFFFull - m[2] && m[1] == 0xFFFFFFFFull - m[3];
-}
-
 // Out of place: the cumulative local counters stay this device's own; their sum over the ranks
 // goes to the generation's reduced buffer (gm_counters_global).  Any number of calls give the
 // true totals (an in-place reduction of cumulative counters would add them up again each time).
-// First the ranks agree on (gen, n_counters) -- GM_E_COMM when one rank runs another generation.
+// The ranks' agreement on (gen, n_counters) rides in the same collective (RedProto): in steady
+// state a call enqueues one staging kernel, ONE ncclAllReduce and one check kernel, with no host
+// synchronisation (the 4-word agreement was a host round trip in front of every sum).
+// The call evaluates the previous call's agreement first (its event, normally long complete); a
+// failed one makes this call re-agree synchronously, and GM_E_COMM reaches every rank at the same
+// call, since every rank reads the same summed block.
 int gm_counters_allreduce(gm_ctx *c, void *stream) {
     if (!c || !c->comm) return fail(c, GM_E_COMM, "gm_comm_init not called");
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
@@ -2815,25 +2902,50 @@ int gm_counters_allreduce(gm_ctx *c, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     Scratch *S = scratch_for(c, s);
     if (!S) return fail(c, GM_E_NOMEM, t_err);
-    DoneGuard G(S);
-    if (!S->d_agree) {
-        HIPCHK(c, hipMalloc((void **)&S->d_agree, 4 * 8));
-        HIPCHK(c, hipHostMalloc((void **)&S->h_agree, 4 * 8, hipHostMallocDefault));
+    std::lock_guard<std::mutex> rl(c->red_mu);
+    if (!c->h_red) {
+        HIPCHK(c, hipHostMalloc((void **)&c->h_red, RED_WORDS * 8, hipHostMallocDefault));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_red, hipEventDisableTiming));
     }
-    agree_pack(c->gen->stats.gen, c->gen->n_counters, S->h_agree);
-    HIPCHK(c, hipMemcpyAsync(S->d_agree, S->h_agree, 4 * 8, hipMemcpyHostToDevice, s));
-    ncclResult_t r = ncclAllReduce(S->d_agree, S->d_agree, 4, ncclUint64, ncclMax, c->comm, s);
-    if (r != ncclSuccess) return fail(c, GM_E_COMM, std::string("ncclAllReduce (agreement): ") + ncclGetErrorString(r));
-    HIPCHK(c, hipMemcpyAsync(S->h_agree, S->d_agree, 4 * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    if (!agree_check(S->h_agree))
-        return fail(c, GM_E_COMM, "ranks disagree on the generation or its counter space (gen " +
-                                      std::to_string(0xFFFFFFFFull - S->h_agree[2]) + ".." + std::to_string(S->h_agree[0]) +
-                                      ", counters " + std::to_string(0xFFFFFFFFull - S->h_agree[3]) + ".." +
-                                      std::to_string(S->h_agree[1]) + "): no reduction issued");
-    r = ncclAllReduce(c->gen->d_counters, c->gen->d_counters_sum, std::max<size_t>(c->gen->n_counters, 1),
-                      ncclUint64, ncclSum, c->comm, s);
+    // the previous call's verdict, before anything of this call is issued (lockstep over the ranks)
+    if (c->red_pending) {
+        HIPCHK(c, hipEventSynchronize(c->ev_red));
+        c->red_pending = false;
+        c->red.finish(c->h_red);
+    }
+    DoneGuard G(S);
+    const uint32_t gen = c->gen->stats.gen;
+    const uint64_t n = c->gen->n_counters;
+    unsigned long long blk[RED_WORDS];
+    RedProto::pack(gen, n, blk);
+    if (!c->red.agreed) {
+        // synchronous: the agreement block alone (count RED_WORDS on every rank)
+        if (int e = grow(c, s, c->d_red, c->cap_red, 2 * RED_WORDS)) return e;
+        memcpy(c->h_red, blk, sizeof blk);
+        HIPCHK(c, hipMemcpyAsync(c->d_red, c->h_red, RED_WORDS * 8, hipMemcpyHostToDevice, s));
+        ncclResult_t r = ncclAllReduce(c->d_red, c->d_red + RED_WORDS, RED_WORDS, ncclUint64, ncclSum, c->comm, s);
+        if (r != ncclSuccess) return fail(c, GM_E_COMM, std::string("ncclAllReduce (agreement): ") + ncclGetErrorString(r));
+        HIPCHK(c, hipMemcpyAsync(c->h_red, c->d_red + RED_WORDS, RED_WORDS * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        if (!c->red.agree(c->h_red))
+            return fail(c, GM_E_COMM, "ranks disagree on the generation or its counter space: no reduction issued");
+    }
+    // the block and the counters in one collective of RED_WORDS + the agreed count on every rank
+    const uint64_t na = c->red.n;
+    if (int e = grow(c, s, c->d_red, c->cap_red, 2 * (RED_WORDS + na))) return e;
+    unsigned long long *din = c->d_red, *dout = c->d_red + RED_WORDS + na;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((RED_WORDS + na + 255) / 256, (uint64_t)c->cu_count * 4);
+    RedBlock rb;
+    memcpy(rb.w, blk, sizeof blk);
+    k_red_stage<<<blocks, 256, 0, s>>>(c->gen->d_counters, n, na, rb, din);
+    HIPCHK(c, hipGetLastError());
+    ncclResult_t r = ncclAllReduce(din, dout, RED_WORDS + na, ncclUint64, ncclSum, c->comm, s);
     if (r != ncclSuccess) return fail(c, GM_E_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    k_red_finish<<<blocks, 256, 0, s>>>(dout, na, c->gen->d_counters_sum, n);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(c->h_red, dout, RED_WORDS * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipEventRecord(c->ev_red, s));
+    c->red_pending = true;
     return G.done(c);
 }
 
@@ -2899,14 +3011,36 @@ extern "C" int gm_debug_alw_profile(gm_ctx *c, const gm_req *reqs, const uint8_t
 }
 
 // gm_counters_allreduce's agreement protocol, exposed for the world-size-2 gloo test
-extern "C" void gm_debug_agree_pack(uint64_t gen, uint64_t n, uint64_t *w4) {
-    unsigned long long w[4];
-    agree_pack(gen, n, w);
-    for (int k = 0; k < 4; k++) w4[k] = w[k];
+// gm_counters_allreduce's protocol (RedProto) with the caller as the transport: pack the block a
+// rank contributes, and drive one state machine per rank (new / begin / agree / finish)
+extern "C" void gm_debug_red_pack(uint64_t gen, uint64_t n, uint64_t *words) {
+    unsigned long long w[RED_WORDS];
+    RedProto::pack((uint32_t)gen, n, w);
+    for (uint32_t k = 0; k < RED_WORDS; k++) words[k] = w[k];
 }
-extern "C" int gm_debug_agree_check(const uint64_t *max4) {
-    const unsigned long long m[4] = {max4[0], max4[1], max4[2], max4[3]};
-    return agree_check(m) ? GM_OK : GM_E_COMM;
+extern "C" uint32_t gm_debug_red_words(void) { return RED_WORDS; }
+extern "C" void *gm_debug_red_new(void) { return new RedProto(); }
+extern "C" void gm_debug_red_free(void *p) { delete static_cast<RedProto *>(p); }
+// 1: this call must agree synchronously first (a block-only collective); 0: it issues the
+// combined collective at once, of RED_WORDS + *count words
+extern "C" int gm_debug_red_begin(void *p, uint64_t *count) {
+    const RedProto *r = static_cast<RedProto *>(p);
+    *count = r->agreed ? r->n : 0;
+    return r->agreed ? 0 : 1;
+}
+extern "C" int gm_debug_red_agree(void *p, const uint64_t *sum) {
+    unsigned long long w[RED_WORDS];
+    for (uint32_t k = 0; k < RED_WORDS; k++) w[k] = sum[k];
+    return static_cast<RedProto *>(p)->agree(w) ? GM_OK : GM_E_COMM;
+}
+// the summed block of a combined collective: GM_OK when its totals are valid (and the next call
+// needs no agreement), GM_E_COMM otherwise
+extern "C" int gm_debug_red_finish(void *p, const uint64_t *sum) {
+    unsigned long long w[RED_WORDS];
+    for (uint32_t k = 0; k < RED_WORDS; k++) w[k] = sum[k];
+    RedProto *r = static_cast<RedProto *>(p);
+    r->finish(w);
+    return r->last_valid ? GM_OK : GM_E_COMM;
 }
 
 extern "C" void gm_debug_update_hook(void (*fn)(void *), void *arg) {
@@ -2974,9 +3108,9 @@ extern "C" int64_t gm_debug_waf_prefilter(gm_ctx *c, const uint8_t *A, size_t le
     const TabHeader &h = c->gen->hdr;
     const uint32_t *bloom = (const uint32_t *)(c->gen->host_image.data() + h.off_waf_a);
     int64_t k = 0;
-    for (size_t p = 0; p + 4 <= len; p += 2) {   // even offsets only (stride-2 scan)
-        uint32_t w;
-        memcpy(&w, A + p, 4);
+    for (size_t p = 0; p + 3 <= len; p += 2) {   // even offsets only (stride-2 scan); the window's
+        uint32_t w = 0;                              // bytes past the arena read as 0
+        memcpy(&w, A + p, std::min<size_t>(4, len - p));
         const BloomProbe b = scan_probe(fold4(w), h.bloom_mul, h.bloom_pk);
         if ((bloom[b.block] & b.mask) == b.mask) { if ((size_t)k < cap && out) out[k] = p; k++; }
     }
@@ -2992,9 +3126,9 @@ extern "C" int64_t gm_debug_waf_prefilter2(gm_ctx *c, const uint8_t *A, size_t l
     const uint32_t *ctxb = (const uint32_t *)(c->gen->host_image.data() + h.off_waf_b);
     auto fb = [&](int64_t i) -> uint32_t { return (i >= 0 && (size_t)i < len ? A[i] : 0u) | 0x20u; };
     int64_t k = 0;
-    for (size_t p = 0; p + 4 <= len; p += 2) {
-        uint32_t w;
-        memcpy(&w, A + p, 4);
+    for (size_t p = 0; p + 3 <= len; p += 2) {
+        uint32_t w = 0;
+        memcpy(&w, A + p, std::min<size_t>(4, len - p));
         w = fold4(w);
         const BloomProbe b = scan_probe(w, h.bloom_mul, h.bloom_pk);
         if ((bloom[b.block] & b.mask) != b.mask) continue;
@@ -3420,7 +3554,7 @@ extern "C" int gm_upstream_uris(gm_ctx *c, const gm_batch *in, const gm_verdict 
 // tuning macros count when they differ from the shipped values.
 static constexpr uint32_t kBuildFlags =
 #if defined(GM_EXP_COUNT) || defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_EXP_ALW_NOEMIT) || \
-    defined(GM_EXP_ALW_COUNT) || GM_EXP_EXACT || defined(GM_EXP_EXACT_CNT)
+    defined(GM_EXP_ALW_COUNT)
     GM_BUILD_EXPERIMENT |
 #endif
 #if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_STG != 32 || \

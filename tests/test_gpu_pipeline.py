@@ -523,8 +523,9 @@ def test_held_verdicts_before_sync(torch_dev, set_shift, spill_shift):
     torch.cuda.synchronize()   # the kernels are done; gm_sync has not run
     pre = d_out.cpu().numpy().view(records.VERDICT_DTYPE).copy()
     peer = d_peer.cpu().numpy().view(np.uint32).copy()
-    assert int(e.debug_status()[3]) & (16 | 512 | 1024), "no set / spill overflow: the test exercises nothing"
     e.sync(0)
+    st = e.stats()
+    assert st["last_spill"] > 0 or st["last_redo"] > 0, f"no set / spill overflow: the test exercises nothing {st}"
     got = d_out.cpu().numpy().view(records.VERDICT_DTYPE)
     gh = d_hits[:e.stats()["last_hits"]].cpu().numpy().view(np.uint32)
     exp, eh = Oracle(b, 5).match(reqs, arena)

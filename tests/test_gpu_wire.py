@@ -131,6 +131,54 @@ def test_parse_then_match_chain(env, cfg):
         assert (exp["route_kind"] == 3).any() and (exp["match_idx"] != 0xFF).any()
 
 
+def _proxy_blob():
+    """the reference's `basic` VirtualServer with examples/proxy-protocol's ConfigMap (below)"""
+    from helpers import golden
+    from gpumatch import blob, confgen
+    from semantics_cases import ADDRS, _rules_vs
+    case = golden("reference_configs.json")["vs_configs"]["basic"]
+    p = confgen.default_config_params()
+    p.update(case["params"])
+    p = confgen.configmap_params({"proxy-protocol": "True", "real-ip-header": "proxy_protocol",
+                                  "set-real-ip-from": "192.168.192.168"}, p)
+    store = {"%s/%s" % (x["metadata"]["namespace"], x["metadata"]["name"]): x for x in case["vsrs"]}
+    files = confgen.virtual_server_files([case["vs"], _rules_vs("pp.example.com", {"variable": "$remote_addr"}, ADDRS)],
+                                         base=p, vsr_store=store, pem_name="",
+                                         endpoints_of=lambda ns, s_, port: case["endpoints"].get(f"{ns}/{s_}:{port}", []))
+    return blob.make_blob(confgen.render_main(p), files)
+
+
+def test_gpu_parse_fits_the_documented_bound(env):
+    """gm_parse_requests' documented arena bound (include/gpumatch.h) is the sum over
+    requests of align16(2 * len + raddr_len + 46) -- a record also carries $proxy_protocol_addr (up
+    to 46 B) after raddr.  Keep-alive requests of PROXY connections (GM_WIRE_PROXY_DONE) with the
+    longest raddr and an IPv6 paddr, in an arena of exactly that size: no overflow, the oracle's
+    records."""
+    torch, dev, e = env
+    b = _proxy_blob()
+    e.load(b, 9)
+    orc = Oracle(b, 9)
+    raddr = "2001:0db8:85a3:0000:0000:8a2e:0370:7334"   # 39 B (the field holds up to 40)
+    msgs, conn = [], []
+    for i in range(3000):
+        msgs.append(b"GET / HTTP/1.0\r\n\r\n" if i % 3 else b"GET /tea HTTP/1.0\r\n\r\n")
+        conn.append({"proxy_done": True, "paddr": "2001:db8:ffff:ffff:ffff:ffff:ffff:%04x" % i, "proxy_port": 4000 + i,
+                     "raddr": raddr + "0", "port": 80})
+    W, M = wire.build(msgs, conn, seed=3)
+    bound = int((((2 * M["len"].astype(np.int64) + M["raddr_len"] + 46) + 15) & ~15).sum())
+    d_w, d_m, d_r, d_a, d_len, cap = _gpu_parse(torch, dev, e, W, M, cap=bound)
+    e.sync(0)   # no GM_E_OVERFLOW
+    n = len(M)
+    got = d_r[:n * 64].cpu().numpy().view(records.REQ_DTYPE)
+    assert int(d_len.item()) <= bound
+    exp, ea = parse_requests(W, M, proxy_ports=orc.proxy_ports())
+    ga = d_a[:int(d_len.item())].cpu().numpy()
+    gf, ef = _fields(got, ga), _fields(exp, ea)
+    for f in records.WIRE_FIELDS:
+        assert gf[f] == ef[f], f
+    assert (got["pad0"][:, 0] >= 38).all() and (got["raddr_len"] == 40).all()
+
+
 def test_gpu_proxy_protocol_parity(env):
     """PROXY protocol on the GPU: the reference's `basic` VirtualServer fixture
     (virtualserver_test.go:163-282, ProxyProtocol true) with examples/proxy-protocol's ConfigMap

@@ -187,10 +187,11 @@ def test_prefilter_covers_every_literal_occurrence(stage2):
         hay, needle = (al, pat.lower()) if r.nocase else (a, pat)
         start = hay.find(needle)
         while start >= 0:
-            # stride-2 scan: the candidate is an even offset in [start - 1, start + len - 4]
-            # (4-byte literals: [start - 1, start + 1], the one-byte-extended key families)
+            # stride-2 scan: the candidate is an even offset in [start - 1, start + len - 3] (a key
+            # window inside the pattern, or one of the one-byte-extended key families: the byte
+            # before the pattern, or the byte after it -- gm_compile.cpp choose_keys)
             k = np.searchsorted(cand, start - 1)
-            assert k < len(cand) and cand[k] <= start + max(len(pat) - 4, 1), (pat, start)
+            assert k < len(cand) and cand[k] <= start + len(pat) - 3, (pat, start)
             assert cand[k] % 2 == 0
             checked += 1
             start = hay.find(needle, start + 1)
