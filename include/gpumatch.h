@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 9u   /* 9: gm_stats_t.csrc_hash, gm_build_hash; 8: PROXY protocol (gm_wire_msg 128 B, $proxy_protocol_addr in gm_req), last_redo;
+#define GM_ABI_VERSION 9u   /* 9: gm_stats_t.csrc_hash, gm_build_hash, GM_ACT_FORBIDDEN, GM_ROUTE_HELD; 8: PROXY protocol (gm_wire_msg 128 B, $proxy_protocol_addr in gm_req), last_redo;
                                7: GM_ACT_TOO_LARGE, GM_REQ_CHUNKED, gm_rejects, build flags; 6: n_rsl_reversed;
                                5: gm_update_upstream / gm_peers_migrate; 4: union-DFA stats */
 
@@ -150,7 +150,8 @@ typedef struct gm_verdict {
 enum {
     GM_ACT_PROXY        = 0,  /* proxy_pass to upstream_id                                 */
     GM_ACT_REDIRECT     = 1,  /* server-level `return 301` (ssl-redirect / x-forwarded-proto) */
-    GM_ACT_RETURN       = 2,  /* location `return <status>` (default server 404, health 200) */
+    GM_ACT_RETURN       = 2,  /* location `return <status>` (default server 404, health 200), or */
+                              /* a content handler the engine answers itself (stub_status: 200) */
     GM_ACT_AUTO_301     = 3,  /* prefix location auto_redirect ($uri + "/")               */
     GM_ACT_NOT_FOUND    = 4,  /* no location matched                                       */
     GM_ACT_BAD_REQUEST  = 5,  /* invalid Host                                              */
@@ -160,8 +161,10 @@ enum {
                               /* regex search reached a PCRE-only regex location whose     */
                               /* superset pattern matches: the data plane defers to nginx  */
     GM_ACT_NO_LISTENER  = 9,  /* no server listens on the port / TLS on a plain port      */
-    GM_ACT_TOO_LARGE    = 10  /* 413: the body exceeds client_max_body_size (nginx.ingress.tmpl:175, */
+    GM_ACT_TOO_LARGE    = 10, /* 413: the body exceeds client_max_body_size (nginx.ingress.tmpl:175, */
                               /* nginx.virtualserver.tmpl:93) -- no WAF phase, nothing proxied */
+    GM_ACT_FORBIDDEN    = 11  /* 403: an allow / deny rule denies the client address (after realip): */
+                              /* the stub_status server of nginx.tmpl:104-115 (-nginx-status-allow-cidrs) */
 };
 
 enum { GM_ROUTE_NONE = 0, GM_ROUTE_PLAIN = 1, GM_ROUTE_SPLIT = 2, GM_ROUTE_RULES = 3 };

@@ -146,6 +146,8 @@ struct Loc {
     uint32_t parser_off = 0;     // wallarm_parser_disable in the location (DEC_* bits)
     bool has_pd = false;
     bool pass_vars = false, grpc = false;
+    bool stub = false;           // stub_status (a content handler answering 200)
+    std::vector<std::pair<bool, std::string>> access;   // allow (false) / deny (true) rules here
     int code = 0;
     int waf = -1;
 };
@@ -163,6 +165,7 @@ struct Server {
     uint32_t parser_off = 0;     // server-level wallarm_parser_disable (DEC_* bits)
     std::string cmbs;            // server-level client_max_body_size ("" inherit)
     RealIpIR rip;
+    std::vector<std::pair<bool, std::string>> access;   // server-level allow / deny
     std::vector<std::pair<int, int>> listens;   // port, flags (1 ssl, 2 default)
     std::vector<std::string> names;
     std::vector<SIf> ifs;
@@ -199,6 +202,7 @@ struct Model {
     uint32_t rejected_other = 0, rejected_pcre = 0;
     std::string http_cmbs;       // http-level client_max_body_size ("" = nginx's default 1m)
     RealIpIR http_rip;
+    std::vector<std::pair<bool, std::string>> http_access;   // http-level allow / deny
     bool http_unknown = false;   // an http-level directive outside the known set: every server defers
     std::vector<std::string> reject_log;   // "context: directive" of every construct rejected
 };
@@ -241,6 +245,14 @@ int waf_mode(const std::string &s) {
 }
 
 std::string lower(std::string s) { for (auto &c : s) if (c >= 'A' && c <= 'Z') c |= 0x20; return s; }
+
+bool parse_cidr(const std::string &t, DCidr &c);
+// an allow / deny argument the engine reads (ngx_http_access_rule): `all`, `unix:`, an address or
+// CIDR; anything else (a host name nginx would refuse) is deferred like an unknown directive
+static bool access_arg_ok(const std::string &a) {
+    DCidr c;
+    return a == "all" || a == "unix:" || parse_cidr(a, c);
+}
 
 struct Builder {
     Model &M;
@@ -295,6 +307,10 @@ struct Builder {
                 L.parser_off |= decoder_bit(k.a[1]); L.has_pd = true;
             } else if (n == "client_max_body_size" && k.a.size() == 2) {
                 L.cmbs = k.a[1];
+            } else if ((n == "allow" || n == "deny") && k.a.size() == 2 && access_arg_ok(k.a[1])) {
+                L.access.push_back({n == "deny", k.a[1]});
+            } else if (n == "stub_status" && (k.a.size() == 1 || (k.a.size() == 2 && k.a[1] == "on"))) {
+                L.stub = true;   // (nginx.tmpl:104-115: the status server's only location)
             } else if (n == "location" || n == "if" || n == "rewrite") {
                 L.nested = true;
                 reject(where, k);
@@ -389,6 +405,8 @@ struct Builder {
                 location(S, k);
             } else if (n == "client_max_body_size" && k.a.size() == 2) {
                 S.cmbs = k.a[1];
+            } else if ((n == "allow" || n == "deny") && k.a.size() == 2 && access_arg_ok(k.a[1])) {
+                S.access.push_back({n == "deny", k.a[1]});
             } else if (realip_dir(S.rip, k)) {
             } else if (n == "set" && k.a.size() >= 2 && k.a[1] == "$hsts_header_val") {
             } else if (n == "error_page" && k.a.size() >= 3 && k.a.back().rfind("@grpcerror", 0) == 0) {
@@ -457,6 +475,8 @@ struct Builder {
                 // MIME types; the config-version server (verify.go:81-92, a unix-socket listener)
             } else if (n == "client_max_body_size" && d.a.size() == 2) {
                 M.http_cmbs = d.a[1];
+            } else if ((n == "allow" || n == "deny") && d.a.size() == 2 && access_arg_ok(d.a[1])) {
+                M.http_access.push_back({n == "deny", d.a[1]});
             } else if (realip_dir(M.http_rip, d)) {
             } else if (n == "wallarm_mode" && d.a.size() == 2) {
                 M.http_waf = waf_mode(d.a[1]);
@@ -1687,6 +1707,7 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
 
     // ---- locations, tries, regex locations, server ifs
     std::vector<DLoc> dlocs(M.locs.size());
+    for (DLoc &d : dlocs) d.access = GM_NONE;
     std::vector<DLocUri> dluri(M.locs.size());
     std::vector<DNode> nodes;
     std::vector<std::pair<uint32_t, uint32_t>> edge_list;   // key, child
@@ -1721,6 +1742,35 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     (void)is_redirect;
     std::vector<DRealIp> realips;
     std::vector<DCidr> cidrs;
+    std::vector<DAccRule> acc_rules;
+    std::vector<DAccList> acc_lists;
+    std::map<std::vector<std::pair<bool, std::string>>, uint32_t> acc_index;   // one list per distinct rule set
+    // the allow / deny rules in effect -> a DAccList index (GM_NONE: none), ngx_http_access_rule:
+    // `all` goes to both lists, an IPv4 CIDR to the first, an IPv6 one to the second; `unix:` rules
+    // never see a TCP client.  bad: a rule the engine does not read (a host name, a bad prefix).
+    auto access_list = [&](const std::vector<std::pair<bool, std::string>> &rules, bool &bad) -> uint32_t {
+        bad = false;
+        if (rules.empty()) return GM_NONE;
+        auto it = acc_index.find(rules);
+        if (it != acc_index.end()) return it->second;
+        std::vector<DAccRule> r4, r6;
+        for (const auto &r : rules) {
+            if (r.second == "unix:") continue;
+            DAccRule a{};
+            a.deny = r.first ? 1u : 0u;
+            if (r.second == "all") { r4.push_back(a); r6.push_back(a); continue; }
+            if (!parse_cidr(r.second, a.c)) { bad = true; continue; }
+            (a.c.family == 4 ? r4 : r6).push_back(a);
+        }
+        DAccList L{(uint32_t)acc_rules.size(), (uint32_t)r4.size(), 0, (uint32_t)r6.size()};
+        acc_rules.insert(acc_rules.end(), r4.begin(), r4.end());
+        L.first6 = (uint32_t)acc_rules.size();
+        acc_rules.insert(acc_rules.end(), r6.begin(), r6.end());
+        const uint32_t idx = (uint32_t)acc_lists.size();
+        acc_lists.push_back(L);
+        acc_index[rules] = idx;
+        return idx;
+    };
     auto body_of = [&](const std::string &own, const Server &S, bool &bad) -> uint32_t {
         // client_max_body_size in effect: the location's, else the server's, else the http
         // block's, else nginx's default 1m (ngx_http_core_merge_loc_conf)
@@ -1739,6 +1789,10 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
         if (sbad) { S.ifs.insert(S.ifs.begin(), SIf{"$uri", -1}); R.rejects.push_back("server: client_max_body_size " + S.cmbs); }
         // realip in effect (ngx_http_realip_merge_loc_conf: the server's set_real_ip_from list,
         // else the http block's; header and recursion merged one by one)
+        {   // allow / deny for a request that matches no location: the server block's own rules
+            bool abad = false;
+            D.access = access_list(!S.access.empty() ? S.access : M.http_access, abad);
+        }
         D.realip = GM_NONE;
         {
             const RealIpIR &a = S.rip, &h = M.http_rip;
@@ -1817,6 +1871,15 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             // wallarm_parser_disable (a location's own list replaces the server's, nginx's array merge)
             dluri[lid].flags |= (decoders & ~(L.has_pd ? L.parser_off : S.parser_off)) << LOCURI_DEC_SHIFT;
             dl.upstream = GM_NONE;
+            {   // allow / deny in effect: the location's own, else the server's, else the http block's
+                const auto &acc = !L.access.empty() ? L.access : !S.access.empty() ? S.access : M.http_access;
+                bool abad = false;
+                dl.access = access_list(acc, abad);
+                if (abad) {
+                    L.unknown = true; st.n_rejected_other++;
+                    R.rejects.push_back("location " + L.path + ": allow / deny with an address the engine does not read");
+                }
+            }
             dl.noregex = L.kind == NOREGEX;
             dl.is_named = L.kind == NAMED;
             bool lbad = false;
@@ -1858,7 +1921,14 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                     du.len = (uint32_t)L.pass_uri.size();
                     du.loc_len = (uint32_t)L.path.size();
                 }
-            } else dl.kind = LK_NONE;
+            } else if (L.stub) dl.kind = LK_STATUS;
+            else dl.kind = LK_NONE;
+            // the access phase beside the Wallarm module's (both in NGX_HTTP_ACCESS_PHASE, in an
+            // order the reference does not fix): a location with both defers
+            if (dl.access != GM_NONE && dl.waf_mode != GM_WAF_OFF && dl.kind != LK_RETURN && dl.kind != LK_UNSUPPORTED) {
+                dl.kind = LK_UNSUPPORTED; st.n_rejected_other++;
+                R.rejects.push_back("location " + L.path + ": allow / deny beside wallarm_mode");
+            }
 
             if (L.kind == PFX || L.kind == NOREGEX || L.kind == EXACT) {
                 D.trie_depth = std::max<uint32_t>(D.trie_depth, (uint32_t)L.path.size());
@@ -2517,6 +2587,8 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
     h.n_realip = (uint32_t)realips.size(); h.n_cidrs = (uint32_t)cidrs.size();
     st.n_realip = h.n_realip;
     h.off_realip = I.put(realips); h.off_cidrs = I.put(cidrs);
+    h.n_acc_rules = (uint32_t)acc_rules.size(); h.n_acc_lists = (uint32_t)acc_lists.size();
+    h.off_acc_rules = I.put(acc_rules); h.off_acc_lists = I.put(acc_lists);
     h.n_rk_cap = rkcap; h.n_rk_ids = (uint32_t)rk_ids.size(); h.n_rk_ents_keys = (uint32_t)rk_lists.size();
     h.off_rk = I.put(rk); h.off_rk_ids = I.put(rk_ids); h.off_rk_ents = I.put(rk_ents); h.off_rk_bloom = I.put(rk_bloom);
     h.n_rk_ents_n = (uint32_t)rk_ents.size();
@@ -2706,6 +2778,8 @@ GTab make_gtab(const TabHeader &h, const uint8_t *b, uint32_t gen) {
     t.rsl_head_slice = (const uint32_t *)(b + h.off_rsl_head_slice);
     t.realip = (const DRealIp *)(b + h.off_realip);
     t.cidrs = (const DCidr *)(b + h.off_cidrs);
+    t.acc_rules = (const DAccRule *)(b + h.off_acc_rules);
+    t.acc_lists = (const DAccList *)(b + h.off_acc_lists);
     t.n_always_lds = h.n_always_lds; t.n_alw_groups = h.n_alw_groups; t.n_alw_slices = h.n_alw_slices;
     t.n_rsl = h.n_rsl; t.n_rk_prefilter = h.n_rk_prefilter;
     t.n_ports = h.n_ports;

@@ -1140,6 +1140,45 @@ __device__ __forceinline__ void route_locphase(const uint8_t *A, const gm_req *r
 // server's limit when none) before that location's rewrite phase (ngx_http_core_find_config_phase);
 // a chunked body only when it is read -- by the proxying location, the final one after an
 // internal redirect (the chunked body filter)
+// ngx_http_access_module's handler (nginx 1.17.3, satisfy all) for the address the request's
+// connection has after the realip module: 0 allowed (no rule matched, or an allow), 1 denied (403),
+// 2 unknown to the engine (realip from a header it cannot read, an unparseable $remote_addr).
+// An IPv4 client is tested against the IPv4 list; an IPv6 one that maps an IPv4 address against
+// the IPv4 list when there is one (and only it), else against the IPv6 list.
+__device__ __noinline__ int access_eval(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t list, uint32_t rip) {
+    const Rec r = load_rec(rp);
+    InetAddr a;
+    a.fam = 0;
+    if (rip != GM_NONE) {
+        Ctx c;
+        ctx_init(c, A, r, &t, rip);
+        if (c.rip_state == RIPS_UNKNOWN) return 2;
+        a = c.ra;   // (realip_eval parsed the connection address into it first)
+    } else {
+        const uint64_t ra = r.base + r.uri_len + r.args_len + r.hdr_len + r.body_len + r.host_len + r.method_len + r.ruri_len;
+        a.fam = r.raddr_len <= 45 ? d_parse_addr(A + ra, r.raddr_len, a.b) : 0u;
+    }
+    if (a.fam == 0) return 2;
+    const DAccList L = t.acc_lists[list];
+    uint32_t fam = a.fam, first = L.first4, nr = L.n4;
+    const uint8_t *b = a.b;
+    if (fam == 6) {
+        bool mapped = b[10] == 0xFF && b[11] == 0xFF;
+        for (int i = 0; i < 10; i++) mapped = mapped && b[i] == 0;
+        if (mapped && L.n4) b += 12, fam = 4;
+        else { first = L.first6; nr = L.n6; }
+    }
+    const uint32_t nb = fam == 4 ? 4u : 16u;
+    for (uint32_t k = 0; k < nr; k++) {
+        const DAccRule R = t.acc_rules[first + k];
+        const uint8_t *ad = reinterpret_cast<const uint8_t *>(R.c.addr), *mk = reinterpret_cast<const uint8_t *>(R.c.mask);
+        bool hit = true;
+        for (uint32_t i = 0; i < nb; i++) hit = hit && (b[i] & mk[i]) == ad[i];
+        if (hit) return R.deny ? 1 : 0;
+    }
+    return 0;
+}
+
 template <bool FAST>
 __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
                           RouteOut &o) {
@@ -1147,13 +1186,20 @@ __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, co
     const bool chunked = req_chunked(rp);
     if (loc < 0) {
         if (!chunked && blen > h.servers[o.server].body_max) { too_large(o); return; }
+        const uint32_t sa = h.servers[o.server].access;   // (the server block's own conf: its access phase)
+        if (sa != GM_NONE) {
+            if (FAST) { o.slow = 1; return; }
+            const int a = access_eval(A, rp, *t.self, sa, h.servers[o.server].realip);
+            if (a == 1) { o.action = GM_ACT_FORBIDDEN; o.status = 403; return; }
+            if (a == 2) { o.action = GM_ACT_UNSUPPORTED; return; }
+        }
         o.action = GM_ACT_NOT_FOUND; o.status = 404; return;
     }
     o.loc = (uint32_t)loc;
     DLoc L = h.locs[loc];
     if (!chunked && blen > L.body_max) { too_large(o); return; }
     uint32_t fin = (uint32_t)loc;
-    if (FAST && (L.kind == LK_IRL_RULES || L.kind == LK_IRL_SPLIT)) { o.slow = 1; return; }
+    if (FAST && (L.kind == LK_IRL_RULES || L.kind == LK_IRL_SPLIT || L.access != GM_NONE)) { o.slow = 1; return; }
     if (L.kind == LK_IRL_RULES) {
         const DRules R = t.rules[L.route];
         const int idx = rules_generic(A, rp, *t.self, L.route, h.servers[o.server].realip);
@@ -1173,9 +1219,18 @@ __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, co
     if (L.kind == LK_IRL_RULES || L.kind == LK_IRL_SPLIT) {
         if (fin == GM_NONE) { o.action = GM_ACT_ERRPAGE; o.status = 302; return; }
         L = h.locs[fin];
-        if (L.kind != LK_PROXY && L.kind != LK_RETURN && L.kind != LK_NONE) { o.action = GM_ACT_UNSUPPORTED; return; }
+        if (L.kind != LK_PROXY && L.kind != LK_RETURN && L.kind != LK_NONE && L.kind != LK_STATUS) {
+            o.action = GM_ACT_UNSUPPORTED; return;
+        }
     }
+    // (`return` answers in the rewrite phase, before the access phase)
     if (L.kind == LK_RETURN) { o.action = is_redirect(L.ret_code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = L.ret_code; return; }
+    if (L.access != GM_NONE) {   // allow / deny (the FAST pass sent such locations here)
+        const int a = access_eval(A, rp, *t.self, L.access, h.servers[o.server].realip);
+        if (a == 1) { o.action = GM_ACT_FORBIDDEN; o.status = 403; return; }
+        if (a == 2) { o.action = GM_ACT_UNSUPPORTED; return; }
+    }
+    if (L.kind == LK_STATUS) { o.action = GM_ACT_RETURN; o.status = 200; return; }
     if (L.kind != LK_PROXY) { o.action = GM_ACT_NOT_FOUND; o.status = 404; return; }
     if (fin == (uint32_t)loc) o.kind = GM_ROUTE_PLAIN;
     if (chunked && blen > L.body_max) { too_large(o); return; }
@@ -1444,6 +1499,10 @@ struct Scratch {
     uint8_t *d_wtemp = nullptr; size_t cap_wtemp = 0;
     uint8_t *d_wscr = nullptr; size_t cap_wscr = 0;   // the wire parser's per-wave $uri scratch
     uint8_t *d_wsum = nullptr; size_t cap_wsum = 0;   // and its pass-1 summaries (WireSum, 80 B each)
+    uint32_t *d_wfull = nullptr; size_t cap_wfull = 0;   // pass 1's per-wave lists of the requests pass 2
+                                                         // writes one at a time, then their counts
+    uint32_t *d_wblk = nullptr; size_t cap_wblk = 0;     // pass 2's output block map (k_wire_blk)
+    uint2 *d_wpieces = nullptr; size_t cap_wpieces = 0;  // pass 1's chunked-body pieces (WIRE_PIECES each)
     gm_wire_msg *d_wmsg = nullptr; size_t cap_wmsg = 0;   // and the descriptors past their PROXY headers
     uint32_t *d_pk = nullptr; size_t cap_pk = 0;     // peer selection: keys, values (x2: sorted),
     uint32_t *d_pseg = nullptr; size_t cap_pseg = 0; // per-upstream ranges, periodic programs
@@ -1501,7 +1560,7 @@ struct Scratch {
     ~Scratch() {
         for (void *p : {(void *)d_status, (void *)d_blk2rec, (void *)d_cand, (void *)d_surv, (void *)d_pairs,
                         (void *)d_jobs, (void *)d_set, (void *)d_cnt, (void *)d_start, (void *)d_ccnt,
-                        (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp, (void *)d_wscr, (void *)d_wsum,
+                        (void *)d_temp, (void *)d_stage, (void *)d_wsize, (void *)d_wbase, (void *)d_wtemp, (void *)d_wscr, (void *)d_wsum, (void *)d_wfull, (void *)d_wblk, (void *)d_wpieces,
                         (void *)d_pk, (void *)d_pseg, (void *)d_pprog, (void *)d_ppat, (void *)d_ptemp,
                         (void *)d_usize, (void *)d_utemp, (void *)d_sreqs, (void *)d_sarena, (void *)d_sblk,
                         (void *)d_ssize, (void *)d_sbase, (void *)d_stemp, (void *)d_rq, (void *)d_rql, (void *)d_rqs, (void *)d_rqb, (void *)d_rqm, (void *)d_rqu, (void *)d_bctr, (void *)d_slow,
@@ -3346,15 +3405,31 @@ extern "C" int gm_parse_requests(gm_ctx *c, const uint8_t *wire, const gm_wire_m
         HIPCHK(c, hipGetLastError());
         msgs = S->d_wmsg;
     }
-    k_wire_size<<<blocks, 64 * WIRE_WAVES, 0, s>>>(wire, msgs, n, S->d_wsize, S->d_wscr, wsum);
+    const uint32_t fmask = proxy ? WIRE_FMASK_PROXY : WIRE_FMASK_PLAIN;
+    // pass 1's per-wave lists: a wave sizes requests gw, gw + W, ... -- at most `per` of them
+    const uint32_t W = blocks * WIRE_WAVES, per = (n + W - 1) / W;
+    if ((e = grow(c, s, S->d_wfull, S->cap_wfull, (size_t)W * per + W))) return e;
+    uint32_t *fcnt = S->d_wfull + (size_t)W * per;
+    const uint32_t nblk = (uint32_t)std::min<uint64_t>((arena_cap >> 10) + 1, 0xFFFFFFFFull);
+    if ((e = grow(c, s, S->d_wblk, S->cap_wblk, (size_t)nblk))) return e;
+    if ((e = grow(c, s, S->d_wpieces, S->cap_wpieces, (size_t)n * WIRE_PIECES))) return e;
+    k_wire_size<<<blocks, 64 * WIRE_WAVES, 0, s>>>(wire, msgs, n, S->d_wsize, S->d_wscr, wsum, fmask, S->d_wfull, per, fcnt,
+                                                   S->d_wpieces);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(S->d_wtemp, tmp, S->d_wsize, S->d_wbase, (int)n + 1, s));
-    k_wire_emit<<<blocks, 64 * WIRE_WAVES, 0, s>>>(wire, msgs, n, S->d_wsize, S->d_wbase, reqs, arena, arena_cap,
-                                                   arena_len_dev, S->d_status + PARSE_STATUS_WORD, S->d_wscr,
-                                                   wsum);
+    // pass 2: the block map, the flat gather of nearly every slot (a lane per 16-byte chunk), the
+    // void batch's records, the full lists
+    const uint32_t lb = std::min<uint32_t>((n + 255) / 256, (uint32_t)c->cu_count * 8);
+    k_wire_blk<<<lb, 256, 0, s>>>(S->d_wbase, n, S->d_wblk, nblk);
+    HIPCHK(c, hipGetLastError());
+    k_wire_gather<<<(uint32_t)c->cu_count * 16, 256, 0, s>>>(wire, msgs, n, S->d_wsize, S->d_wbase, reqs, arena, arena_cap,
+                                                           arena_len_dev, S->d_status + PARSE_STATUS_WORD, wsum, S->d_wblk,
+                                                           fmask, S->d_wpieces);
+    HIPCHK(c, hipGetLastError());
+    k_wire_void<<<lb, 256, 0, s>>>(msgs, n, S->d_wsize, S->d_wbase, reqs, arena_cap);
     HIPCHK(c, hipGetLastError());
     k_wire_emit_full<<<blocks, 64 * WIRE_WAVES, 0, s>>>(wire, msgs, n, S->d_wsize, S->d_wbase, reqs, arena, arena_cap,
-                                                        S->d_wscr, wsum);
+                                                        S->d_wscr, wsum, fmask, S->d_wfull, per, fcnt);
     HIPCHK(c, hipGetLastError());
     return G.done(c);
 }

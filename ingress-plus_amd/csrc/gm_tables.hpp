@@ -54,6 +54,8 @@ struct DServer {
     uint32_t realip;              // DRealIp index (set_real_ip_from ...), GM_NONE: none
     uint32_t body_max;            // client_max_body_size of the server level (a request that
                                   // matches no location), BODY_UNLIMITED: none
+    uint32_t access;              // DAccList of the server level's allow / deny (a request that
+                                  // matches no location), GM_NONE: none
 };
 // client_max_body_size (version1/nginx.ingress.tmpl:175, version2/nginx.virtualserver.tmpl:93):
 // a body longer than this gets 413; 0 (nginx's "no limit") and limits >= 4 GiB never trigger
@@ -123,7 +125,7 @@ struct DEdge { uint32_t key; uint32_t child; int32_t child_prefix; uint32_t pad;
 
 // ---- locations -------------------------------------------------------------------------
 enum : uint8_t { LK_PROXY = 0, LK_RETURN = 1, LK_IRL_SPLIT = 2, LK_IRL_RULES = 3, LK_UNSUPPORTED = 4,
-                 LK_NONE = 5, LK_IRL_EMPTY = 6 };
+                 LK_NONE = 5, LK_IRL_EMPTY = 6, LK_STATUS = 7 /* stub_status: a 200 content handler */ };
 struct DLoc {
     uint8_t  kind;           // LK_*
     uint8_t  noregex;        // ^~
@@ -134,8 +136,14 @@ struct DLoc {
     uint32_t route;          // DSplit / DRules index for IRLs
     uint32_t body_max;       // client_max_body_size in effect here (BODY_UNLIMITED: none, or a
                              // location whose own identity is uncertain: nested / PCRE-only)
-    uint32_t pad;
+    uint32_t access;         // DAccList of the allow / deny rules in effect here, GM_NONE: none
 };
+// ngx_http_access_module (nginx 1.17.3) rules in effect at a location -- its own, else its
+// server's, else the http block's (ngx_http_access_merge_loc_conf): the IPv4 list (IPv4 and `all`
+// rules, config order: alcf->rules) and the IPv6 list (IPv6 and `all`: alcf->rules6).  A rule is
+// a DCidr (family 0 for `all`: mask 0) and its verdict.
+struct DAccRule { DCidr c; uint32_t deny; uint32_t pad[2]; };
+struct DAccList { uint32_t first4, n4, first6, n6; };
 
 // The upstream request URI of a proxying location (§8 f1, nginx.org/rewrites: the URI part of
 // proxy_pass, annotations.go:347-361, version1/nginx.ingress.tmpl:194-196), indexed like DLoc.
@@ -402,6 +410,8 @@ struct TabHeader {
     uint64_t off_alw_rl;           // always-run members' rule lists (zones << 24 | rule)
     uint64_t off_lit_chk;          // DLitChk per DLit
     uint32_t n_wild, pad_wild;     // wildcard server names (both tables)
+    uint32_t n_acc_rules, n_acc_lists;   // allow / deny rules and the lists locations point at
+    uint64_t off_acc_rules, off_acc_lists;
 };
 // The route's hot tables -- ports, the three name tables, servers, server ifs, small-location
 // lists, locations and the name strings -- are laid out first and contiguously in the image;
@@ -431,6 +441,7 @@ struct GTab {                // device pointers, built on host from the image ba
     const uint8_t *rsl_pbit;
     const uint32_t *rsl_heads; uint32_t n_rsl_heads; const uint32_t *rsl_head_slice;
     const DRealIp *realip; const DCidr *cidrs;
+    const DAccRule *acc_rules; const DAccList *acc_lists;
     const uint32_t *alw_rl;
     const DLitChk *lit_chk;
     uint32_t n_always_lds, n_alw_groups, n_alw_slices, n_rsl, n_rk_prefilter;

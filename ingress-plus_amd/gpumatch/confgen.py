@@ -73,6 +73,12 @@ def default_config_params() -> dict:
         # real-ip-recursive, configmaps.go:153-169)
         "SetRealIPFrom": [], "RealIPHeader": "", "RealIPRecursive": False,
         "HSTS": False, "HSTSMaxAge": 2592000, "HSTSIncludeSubdomains": False, "HSTSBehindProxy": False,
+        # the status server of the main template (nginx.tmpl:104-125), from the controller's flags:
+        # -nginx-status (default true), -nginx-status-port (8080), -nginx-status-allow-cidrs
+        # ("127.0.0.1"), and -enable-prometheus-metrics (false) for the unix-socket one
+        # (cmd/nginx-ingress/main.go:108-113, 329-332)
+        "NginxStatus": True, "NginxStatusPort": 8080, "NginxStatusAllowCIDRs": ["127.0.0.1"],
+        "StubStatusOverUnixSocketForOSS": False,
     }
 
 
@@ -1079,8 +1085,9 @@ def configmap_params(data: dict, params: dict | None = None) -> dict:
 
 
 def render_main(params: dict | None = None, wallarm_global_mode: str | None = None) -> str:
-    """The http{} part of version1/nginx.tmpl that affects request classification:
-    the default server (:81-102) and the conf.d include point (:128-129)."""
+    """The http{} part of version1/nginx.tmpl that affects request classification: the default
+    server (:81-102), the stub_status server (:104-115, on by default: the controller's
+    -nginx-status flag) and the conf.d include point (:128-129)."""
     p = params or default_config_params()
     L = []
     if p.get("MainEnableWallarm"):
@@ -1097,8 +1104,15 @@ def render_main(params: dict | None = None, wallarm_global_mode: str | None = No
     if p.get("HealthStatus"):
         L += ["        location /nginx-health {", "            default_type text/plain;",
               '            return 200 "healthy\\n";', "        }"]
-    L += ["        location / {", "           return 404;", "        }", "    }",
-          "    include /etc/nginx/config-version.conf;", "    include /etc/nginx/conf.d/*.conf;",
+    L += ["        location / {", "           return 404;", "        }", "    }"]
+    if p.get("NginxStatus", True):   # stub_status (nginx.tmpl:104-115)
+        L += ["    server {", f"        listen {p.get('NginxStatusPort', 8080)};"]
+        L += [f"        allow {c};" for c in p.get("NginxStatusAllowCIDRs", ["127.0.0.1"])]
+        L += ["        deny all;", "        location /stub_status {", "            stub_status;", "        }", "    }"]
+    if p.get("StubStatusOverUnixSocketForOSS"):   # (nginx.tmpl:117-125: a unix-socket listener, no TCP client)
+        L += ["    server {", "        listen unix:/var/run/nginx-status.sock;", "        access_log off;",
+              "        location /stub_status {", "            stub_status;", "        }", "    }"]
+    L += ["    include /etc/nginx/config-version.conf;", "    include /etc/nginx/conf.d/*.conf;",
           "    server {", "        listen unix:/var/run/nginx-502-server.sock;", "        access_log off;",
           "        location / {", "            return 502;", "        }", "    }", "}"]
     return "\n".join(L) + "\n"

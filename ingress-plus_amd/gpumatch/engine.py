@@ -26,7 +26,8 @@ GM_CREATE_COMPILE_ONLY = 0x1
 GM_BATCH_HOST = 0x1
 
 ACT = {0: "PROXY", 1: "REDIRECT", 2: "RETURN", 3: "AUTO_301", 4: "NOT_FOUND", 5: "BAD_REQUEST", 6: "BLOCK",
-       7: "ERRPAGE", 8: "UNSUPPORTED", 9: "NO_LISTENER", 10: "TOO_LARGE"}
+       7: "ERRPAGE", 8: "UNSUPPORTED", 9: "NO_LISTENER", 10: "TOO_LARGE", 11: "FORBIDDEN"}
+GM_ACT_FORBIDDEN = 11
 GM_ACT_TOO_LARGE = 10
 GM_REQ_CHUNKED = 0x10
 GM_BUILD_EXPERIMENT, GM_BUILD_TUNING = 0x1, 0x2

@@ -155,6 +155,12 @@ static int parse_block(lexer *L, dir_t *parent, int depth) {
 /* ------------------------------------------------------------------ model */
 enum { LK_PREFIX, LK_EXACT, LK_NOREGEX, LK_REGEX, LK_REGEX_I, LK_NAMED };
 
+/* an address block (ngx_cidr_t): set_real_ip_from, allow / deny */
+typedef struct { uint8_t fam; uint8_t addr[16], mask[16]; } ocidr_t;
+/* an ngx_http_access_module rule (allow / deny): `all`, `unix:`, or a CIDR */
+typedef struct { int deny, all, unix_; ocidr_t c; } oacc_t;
+typedef struct { int n; oacc_t *r; } oacl_t;
+
 typedef struct {
     int kind; char *path; int plen; pcre *re;
     int id, server;
@@ -172,12 +178,13 @@ typedef struct {
     char *cmbs;               /* client_max_body_size written here, NULL: inherited */
     int64_t body_max;         /* the limit in effect (-1: none), set once the server is known */
     pcre *relaxed;            /* its superset pattern (orc_relax), NULL = none */
+    oacl_t acc;               /* allow / deny written here (n 0: inherited) */
+    int stub;                 /* stub_status: a content handler answering 200 */
 } loc_t;
 
 typedef struct { char *var; int op; char *val; pcre *re; int code; char *text; int is_return_only; int unsupported; } sif_t;
 
 /* ngx_http_realip_module settings (set_real_ip_from / real_ip_header / real_ip_recursive) */
-typedef struct { uint8_t fam; uint8_t addr[16], mask[16]; } ocidr_t;
 typedef struct {
     int nfrom; char **from;    /* NULL (nfrom 0) = unset */
     char *header;              /* NULL = unset */
@@ -197,6 +204,7 @@ typedef struct {
     int nifs; sif_t *ifs;
     int nlocs; int *locs;
     int waf_mode;
+    oacl_t acc;               /* server-level allow / deny */
 } srv_t;
 
 typedef struct { char *key; int klen; pcre *re; int is_re; char *val; } mparam_t;
@@ -235,6 +243,7 @@ typedef struct orc_ctx {
     char **ups; int nups;
     int http_waf;
     char *http_cmbs; orip_t http_rip; int http_unknown;
+    oacl_t http_acc;          /* http-level allow / deny */
     sig_t *sig; int nsig;
     int decoders;             /* the signature set's "@decoders" (DEC bits) */
     /* CPU-baseline engine (orc_set_prefilter): a regex runs on a zone only if its required factor
@@ -529,6 +538,42 @@ static int o_cidr_match(const srv_t *S, const oaddr_t *a) {
     }
     return 0;
 }
+/* allow / deny <arg> (ngx_http_access_rule, nginx 1.17.3): `all`, `unix:`, or an address / CIDR */
+/* 0: an argument the engine does not read (a host name): the directive is deferred like an
+ * unknown one, and no rule is added */
+static int oacl_add(oacl_t *L, const char *verb, const char *arg) {
+    oacc_t a; memset(&a, 0, sizeof a);
+    a.deny = !strcmp(verb, "deny");
+    if (!strcmp(arg, "all")) a.all = 1;
+    else if (!strcmp(arg, "unix:")) a.unix_ = 1;
+    else if (!o_ptocidr(arg, &a.c)) return 0;
+    L->r = realloc(L->r, sizeof(oacc_t) * (size_t)(L->n + 1));
+    L->r[L->n++] = a;
+    return 1;
+}
+/* ngx_http_access_handler with satisfy all: 1 = a deny rule matched the client address (403),
+ * 0 = allowed.  An IPv4 client walks the rules for AF_INET in config order (IPv4 CIDRs and `all`);
+ * an IPv4-mapped IPv6 client walks them too when there are any (and only them), other IPv6
+ * clients the AF_INET6 ones (IPv6 CIDRs and `all`); `unix:` rules never see a TCP client. */
+static int oacl_denies(const oacl_t *L, const oaddr_t *a) {
+    int fam = a->fam; const uint8_t *b = a->b;
+    static const uint8_t mapped[12] = {0,0,0,0,0,0,0,0,0,0,0xFF,0xFF};
+    int has4 = 0;
+    for (int i = 0; i < L->n; i++) if (L->r[i].all || (!L->r[i].unix_ && L->r[i].c.fam == 4)) has4 = 1;
+    if (fam == 6 && has4 && !memcmp(b, mapped, 12)) { fam = 4; b += 12; }
+    for (int i = 0; i < L->n; i++) {
+        const oacc_t *r = &L->r[i];
+        if (r->unix_) continue;
+        if (!r->all) {
+            if (r->c.fam != fam) continue;
+            int ok = 1;
+            for (int k = 0; k < (fam == 4 ? 4 : 16) && ok; k++) ok = (b[k] & r->c.mask[k]) == r->c.addr[k];
+            if (!ok) continue;
+        }
+        return r->deny;
+    }
+    return 0;
+}
 static int o_ntop(const oaddr_t *a, char *out) {
     if (a->fam == 4) return sprintf(out, "%u.%u.%u.%u", a->b[0], a->b[1], a->b[2], a->b[3]);
     const uint8_t *p = a->b;
@@ -611,6 +656,7 @@ static void walk_http(build_t *B, dir_t *h) {
                     !strcmp(d->args[1], "/etc/nginx/config-version.conf"))) {
         } else if (!strcmp(n, "client_max_body_size") && d->nargs == 2) {
             c->http_cmbs = strdup(d->args[1]);
+        } else if ((!strcmp(n, "allow") || !strcmp(n, "deny")) && d->nargs == 2 && oacl_add(&c->http_acc, n, d->args[1])) {
         } else if (orc_realip_dir(&c->http_rip, d)) {
         } else if (!strcmp(n, "wallarm_mode") && d->nargs == 2) {
             c->http_waf = waf_mode_of(d->args[1]);
@@ -729,6 +775,10 @@ static void add_location(build_t *B, srv_t *S, dir_t *d, int srv_waf) {
             L.nested = 1;   /* nested location / if / rewrite: outside the restated subset */
         } else if (!strcmp(k->args[0], "client_max_body_size") && k->nargs == 2) {
             L.cmbs = strdup(k->args[1]);
+        } else if ((!strcmp(k->args[0], "allow") || !strcmp(k->args[0], "deny")) && k->nargs == 2 &&
+                   oacl_add(&L.acc, k->args[0], k->args[1])) {
+        } else if (!strcmp(k->args[0], "stub_status") && (k->nargs == 1 || (k->nargs == 2 && !strcmp(k->args[1], "on")))) {
+            L.stub = 1;
         } else if (!strcmp(k->args[0], "error_page") && k->nargs >= 3 &&
                    !strncmp(k->args[k->nargs - 1], "@grpcerror", 10)) {
             /* gRPC error pages: a named location answering the same status */
@@ -835,6 +885,7 @@ static void add_server(build_t *B, dir_t *s, int http_waf) {
             add_location(B, &S, d, S.waf_mode);
         } else if (!strcmp(n, "client_max_body_size") && d->nargs == 2) {
             S.cmbs = strdup(d->args[1]);
+        } else if ((!strcmp(n, "allow") || !strcmp(n, "deny")) && d->nargs == 2 && oacl_add(&S.acc, n, d->args[1])) {
         } else if (orc_realip_dir(&S.rip, d)) {
         } else if ((!strcmp(n, "set") && d->nargs >= 2 && !strcmp(d->args[1], "$hsts_header_val")) ||
                    (!strcmp(n, "error_page") && d->nargs >= 3 && !strncmp(d->args[d->nargs - 1], "@grpcerror", 10)) ||
@@ -1979,6 +2030,25 @@ static void waf_scan(orc_ctx *c, rq_t *q, uint8_t *mark, hitbuf_t *out, int dec_
     for (size_t i = first; i < out->n; i++) mark[out->ids[i]] = 0;
 }
 
+/* the allow / deny rules in effect at a location: its own, else its server's, else the http
+ * block's (ngx_http_access_merge_loc_conf) */
+static const oacl_t *loc_acl(const orc_ctx *c, const srv_t *S, const loc_t *L) {
+    return L->acc.n ? &L->acc : S->acc.n ? &S->acc : &c->http_acc;
+}
+/* the engine's contract (gm_compile.cpp): a content location with rules beside wallarm_mode (the
+ * two access-phase handlers' order is not fixed by the reference) is deferred */
+static int loc_access_defer(const orc_ctx *c, const srv_t *S, const loc_t *L) {
+    return loc_acl(c, S, L)->n && !L->has_return && L->waf_mode != GM_WAF_OFF;
+}
+/* the access phase for the address the connection has after realip: 0 allowed, 1 denied (403),
+ * 2 unknown to the engine (realip from a source it cannot read, an unparseable address) */
+static int access_phase(ev_t *E, const oacl_t *A) {
+    if (!A->n) return 0;
+    sv ra = get_var(E, "remote_addr", 11);
+    oaddr_t a;
+    if (E->unknown || !o_parse_addr(ra.p, ra.n, &a)) return 2;
+    return oacl_denies(A, &a);
+}
 static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdict *v, scratch_t *sc,
                      uint8_t *mark, hitbuf_t *hits, uint32_t *nh) {
     rq_t q; rq_init(&q, r, arena);
@@ -2026,6 +2096,10 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
     int lid = find_location(c, S, q.uri, &a301);
     if (lid < 0) {
         if (TOO_LARGE(S->body_max)) { v->action = GM_ACT_TOO_LARGE; v->status = 413; return; }
+        /* no location: the server block's own configuration runs the access phase */
+        const int ap = access_phase(&E, S->acc.n ? &S->acc : &c->http_acc);
+        if (ap == 1) { v->action = GM_ACT_FORBIDDEN; v->status = 403; return; }
+        if (ap == 2) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
         v->action = GM_ACT_NOT_FOUND; v->status = 404; return;
     }
     v->location_id = (uint32_t)lid;
@@ -2033,7 +2107,7 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
     if (TOO_LARGE(L->body_max)) { v->action = GM_ACT_TOO_LARGE; v->status = 413; return; }
 #undef TOO_LARGE
     if (a301) { v->action = GM_ACT_AUTO_301; v->status = 301; return; }
-    if (L->pcre_only || L->nested || L->unknown) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
+    if (L->pcre_only || L->nested || L->unknown || loc_access_defer(c, S, L)) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
     loc_t *F = L;   /* location that runs the content phase */
     if (L->has_return && L->ret_code == 418 && L->err418) {
         int pidx = -2, part = -2;
@@ -2050,7 +2124,7 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
             int nl = find_named(c, S, target);
             if (nl < 0) { v->action = GM_ACT_NOT_FOUND; v->status = 404; return; }
             F = &c->loc[nl];
-            if (F->nested) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
+            if (F->nested || loc_access_defer(c, S, F)) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
         } else if (target.n == 0) {
             v->action = GM_ACT_ERRPAGE; v->status = 302; return;
         } else {
@@ -2068,6 +2142,12 @@ static void eval_one(orc_ctx *c, const gm_req *r, const uint8_t *arena, gm_verdi
                      F->ret_code == 308) ? GM_ACT_REDIRECT : GM_ACT_RETURN;
         v->status = (uint32_t)F->ret_code; return;
     }
+    {   /* the access phase (after `return`, which answers in the rewrite phase) */
+        const int ap = access_phase(&E, loc_acl(c, S, F));
+        if (ap == 1) { v->action = GM_ACT_FORBIDDEN; v->status = 403; return; }
+        if (ap == 2) { v->action = GM_ACT_UNSUPPORTED; v->status = 0; return; }
+    }
+    if (F->stub && !F->has_proxy) { v->action = GM_ACT_RETURN; v->status = 200; return; }
     if (!F->has_proxy) { v->action = GM_ACT_NOT_FOUND; v->status = 404; return; }
     if (chunked && F->body_max >= 0 && (int64_t)r->body_len > F->body_max) {
         v->action = GM_ACT_TOO_LARGE; v->status = 413; return;

@@ -12,8 +12,11 @@ and the GPU parity tests (tests/test_gpu_semantics.py).
   set_real_ip_from, $remote_addr (a whitelisted VS condition variable, validation.go:357) and the
   ip_hash key come from X-Real-IP / X-Forwarded-For / a named header.  The reference's own
   virtualserver_test.go:225-263 carries SetRealIPFrom 0.0.0.0/0, X-Real-IP, recursive.
-- default-deny: snippet directives the engine does not model (`deny all;`, auth_basic, ...) make the
-  requests reaching them GM_ACT_UNSUPPORTED, counted in n_rejected_other.
+- default-deny: snippet directives the engine does not model (auth_basic, auth_request, ...) make
+  the requests reaching them GM_ACT_UNSUPPORTED, counted in n_rejected_other.
+- the access module (allow / deny, round 6): the main template's stub_status server
+  (nginx.tmpl:104-115, -nginx-status-allow-cidrs), snippet rules at server and location level,
+  IPv4 / IPv6 / IPv4-mapped clients, the address after realip, `return` before the access phase.
 
 The expected answers are nginx 1.17.3 behaviour written out by hand (parity unpinned: no
 reference test pins them beyond the fixture's fields); the engine and the oracle must also agree
@@ -23,7 +26,7 @@ from __future__ import annotations
 
 from gpumatch import blob, confgen
 
-PROXY, REDIRECT, RETURN, AUTO_301, NOT_FOUND, UNSUPPORTED, TOO_LARGE = 0, 1, 2, 3, 4, 8, 10
+PROXY, REDIRECT, RETURN, AUTO_301, NOT_FOUND, UNSUPPORTED, TOO_LARGE, FORBIDDEN = 0, 1, 2, 3, 4, 8, 10, 11
 ANY = None   # oracle parity only
 
 
@@ -235,9 +238,10 @@ def default_deny_case():
     """Snippets the engine does not model: `deny all;` in one Ingress's locations, an access rule in
     another's server, an `if` doing more than `return` -- and neutral snippets that stay compiled."""
     a = _ingress("denied", "denied.example.com", [("/", "a-svc"), ("/x", "a-svc")],
-                 {"nginx.org/location-snippets": "deny all;"})
+                 {"nginx.org/location-snippets": "auth_basic closed;"})
     bsrv = _ingress("acl", "acl.example.com", [("/", "b-svc")],
-                    {"nginx.org/server-snippets": "allow 10.0.0.0/8;\ndeny all;", "nginx.org/redirect-to-https": "true"})
+                    {"nginx.org/server-snippets": "auth_request /auth;\nallow unknown.example;",
+                     "nginx.org/redirect-to-https": "true"})
     c = _ingress("neutral", "neutral.example.com", [("/", "c-svc")],
                  {"nginx.org/location-snippets": "add_header X-Frame-Options DENY;\nproxy_set_header X-A b;",
                   "nginx.org/server-snippets": "if ($http_x_debug) { set $dbg 1; }"})
@@ -255,9 +259,54 @@ def default_deny_case():
         ({"host": "ok.example.com", "uri": "/z"}, PROXY),
     ]
     # rejected constructs gm_rejects lists (each once)
-    rejects = ["location /: deny all", "location /x: deny all", "server: allow 10.0.0.0/8", "server: deny all",
-               "server: if ($http_x_debug)"]
+    rejects = ["location /: auth_basic closed", "location /x: auth_basic closed", "server: auth_request /auth",
+               "server: allow unknown.example", "server: if ($http_x_debug)"]
     return b, cases, rejects
+
+
+def access_case():
+    """ngx_http_access_module (nginx 1.17.3, satisfy all): the stock main config's stub_status server
+    (port 8080, allow 127.0.0.1, deny all) and a status server with more CIDRs; snippet rules in a
+    server (inherited by its locations) and in a location (replacing the server's); IPv6 and
+    IPv4-mapped clients; a `return` location (rewrite phase: before the access phase); a realip
+    server whose rules see the X-Real-IP address."""
+    p = confgen.default_config_params()
+    p["NginxStatusAllowCIDRs"] = ["127.0.0.1", "10.8.0.0/16", "2001:db8::/32"]
+    srv = _ingress("acl", "acl.example.com", [("/", "b-svc"), ("/open", "c-svc")],
+                   {"nginx.org/server-snippets": "deny 10.1.2.3;\nallow 10.0.0.0/8;\nallow ::1;\ndeny all;",
+                    })
+    loc = _ingress("loc", "loc.example.com", [("/", "d-svc")],
+                   {"nginx.org/location-snippets": "allow 192.168.0.0/16;\ndeny all;"})
+    ret = _ingress("ret", "ret.example.com", [("/", "e-svc")],
+                   {"nginx.org/server-snippets": "deny all;", "nginx.org/redirect-to-https": "true"})
+    rip = _ingress("rip", "rip.example.com", [("/", "f-svc")],
+                   {"nginx.org/server-snippets": "set_real_ip_from 10.0.0.0/8;\nallow 1.2.3.0/24;\ndeny all;"})
+    b = blob.make_blob(confgen.render_main(p), confgen.ingress_files([srv, loc, ret, rip]))
+
+    def st(raddr, uri="/stub_status"):
+        return {"host": "x", "uri": uri, "raddr": raddr, "port": 8080, "https": False}
+    a, lo, rt, rp = "acl.example.com", "loc.example.com", "ret.example.com", "rip.example.com"
+    cases = [
+        (st("127.0.0.1"), RETURN), (st("127.0.0.2"), FORBIDDEN), (st("10.8.3.4"), RETURN),
+        (st("2001:db8:1::5"), RETURN), (st("2001:db9::5"), FORBIDDEN), (st("::ffff:127.0.0.1"), RETURN),
+        (st("::ffff:10.9.0.1"), FORBIDDEN), (st("::1"), FORBIDDEN),
+        (st("10.8.3.4", "/other"), NOT_FOUND), (st("9.9.9.9", "/other"), FORBIDDEN),   # the server level's rules
+        ({"host": a, "uri": "/", "raddr": "10.1.2.3"}, FORBIDDEN),      # the first matching rule decides
+        ({"host": a, "uri": "/", "raddr": "10.1.2.4"}, PROXY),
+        ({"host": a, "uri": "/open", "raddr": "11.0.0.1"}, FORBIDDEN),
+        ({"host": a, "uri": "/", "raddr": "::1"}, PROXY),
+        ({"host": a, "uri": "/", "raddr": "::ffff:10.0.0.9"}, PROXY),   # mapped: the IPv4 rules
+        ({"host": a, "uri": "/", "raddr": "2001:db8::7"}, FORBIDDEN),
+        ({"host": lo, "uri": "/", "raddr": "192.168.7.7"}, PROXY),
+        ({"host": lo, "uri": "/", "raddr": "10.0.0.1"}, FORBIDDEN),
+        ({"host": rt, "uri": "/", "raddr": "10.0.0.1"}, FORBIDDEN),
+        ({"host": rt, "uri": "/", "raddr": "10.0.0.1", "headers": [("X-Forwarded-Proto", "http")]}, REDIRECT),
+        ({"host": rp, "uri": "/", "raddr": "10.0.0.1", "headers": [("X-Real-IP", "1.2.3.9")]}, PROXY),
+        ({"host": rp, "uri": "/", "raddr": "10.0.0.1", "headers": [("X-Real-IP", "1.2.4.9")]}, FORBIDDEN),
+        ({"host": rp, "uri": "/", "raddr": "1.2.3.1", "headers": [("X-Real-IP", "8.8.8.8")]}, PROXY),   # untrusted
+        ({"host": rp, "uri": "/", "raddr": "not-an-address"}, UNSUPPORTED),
+    ]
+    return b, cases
 
 
 def http_unknown_case():
@@ -274,7 +323,8 @@ def http_unknown_case():
     return b, cases
 
 
-ROUTE_CASES = {"body_limit": body_limit_case, "vs_body": vs_body_case, "http_unknown": http_unknown_case}
+ROUTE_CASES = {"body_limit": body_limit_case, "vs_body": vs_body_case, "http_unknown": http_unknown_case,
+               "access": access_case}
 # expected: the rules route's match index (0xFF default), or UNSUPPORTED for a deferred verdict
 MATCH_CASES = {"realip_xff": realip_xff_case, "realip_xrealip": realip_xrealip_case,
                "realip_header_port": realip_header_port_case, "realip_proxy_protocol": realip_proxy_protocol_case,

@@ -9,8 +9,8 @@ libgpumatch.so against the oracle, bit for bit, on tests/semantics_cases.py's kn
   20k requests of random forwarded-address lists through a rules route and `hash $remote_addr
   $remote_port consistent` / ip_hash balancers (the address text and bytes the device computes
   must equal the oracle's);
-- default-deny: `deny all;` in location snippets, access rules in server snippets, http-level
-  unknown directives: GM_ACT_UNSUPPORTED, counted;
+- default-deny: auth_basic / auth_request snippets and http-level unknown directives:
+  GM_ACT_UNSUPPORTED, counted; the access module (allow / deny, the stock stub_status server);
 - the wire parser's chunked flag (GM_REQ_CHUNKED) feeding the 413 decision."""
 
 import numpy as np
@@ -248,3 +248,32 @@ def test_wire_chunked_body_limit_gpu(eng):
     exp, _ = Oracle(b, 5).match(reqs, arena)
     assert_verdicts_equal(got, exp, None, None, "wire chunked")
     assert (exp["action"] == SC.TOO_LARGE).sum() > 5 and (exp["action"] == SC.PROXY).sum() > 5
+
+
+def test_stock_main_config_gpu(eng):
+    """the main config a stock controller renders (nginx.tmpl with its defaults:
+    -nginx-status true, port 8080, allow 127.0.0.1, deny all) compiles with 0 rejects, and requests
+    to every listener -- the status server's included, from allowed and denied IPv4 / IPv6 / mapped
+    clients -- equal the oracle's verdicts on the GPU."""
+    from gpumatch import workloads
+    b = workloads.c1_blob()
+    eng.load(b, 4)
+    assert eng.stats()["n_rejected_other"] == 0, eng.rejects()
+    rng = np.random.Generator(np.random.PCG64(8080))
+    addrs = ["127.0.0.1", "127.0.0.2", "10.0.0.1", "::1", "::ffff:127.0.0.1", "2001:db8::1", "192.168.1.1"]
+    items = []
+    for i in range(6000):
+        k = int(rng.integers(0, 4))
+        it = {"raddr": addrs[int(rng.integers(0, len(addrs)))]}
+        if k == 0:
+            it.update(host="localhost", uri=["/stub_status", "/stub_status/x", "/", "/other"][int(rng.integers(0, 4))],
+                      port=8080)
+        elif k == 1:
+            it.update(host="cafe.example.com", uri=["/tea", "/coffee", "/", "/tea/x"][int(rng.integers(0, 4))],
+                      https=bool(rng.random() < 0.5))
+        else:
+            it.update(host=["nope.example.com", "cafe.example.com"][int(rng.integers(0, 2))], uri="/")
+        items.append(it)
+    v = _both(eng, b, items, gen=4)
+    st = v[[it.get("port") == 8080 for it in items]]
+    assert (st["action"] == SC.FORBIDDEN).sum() > 100 and (st["status"] == 200).sum() > 50

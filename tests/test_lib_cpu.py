@@ -37,7 +37,8 @@ def eng():
 def test_compile_cafe(eng):
     eng.load(workloads.c1_blob(), 7)
     s = eng.stats()
-    assert s["gen"] == 7 and s["n_servers"] == 3 and s["n_locations"] == 4 and s["n_upstreams"] == 2
+    # the default server, the stub_status server (nginx.tmpl:104-115, on by default), cafe's two
+    assert s["gen"] == 7 and s["n_servers"] == 4 and s["n_locations"] == 5 and s["n_upstreams"] == 2
     assert s["n_rejected_other"] == 0 and s["n_rejected_pcre"] == 0
 
 
