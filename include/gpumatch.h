@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GM_ABI_VERSION 9u   /* 9: gm_stats_t.csrc_hash, gm_build_hash, GM_ACT_FORBIDDEN, GM_ROUTE_HELD; 8: PROXY protocol (gm_wire_msg 128 B, $proxy_protocol_addr in gm_req), last_redo;
+#define GM_ABI_VERSION 10u  /* 10: gm_sync_batches, GM_E_EARLIER; 9: gm_stats_t.csrc_hash, gm_build_hash, GM_ACT_FORBIDDEN, GM_ROUTE_HELD; 8: PROXY protocol (gm_wire_msg 128 B, $proxy_protocol_addr in gm_req), last_redo;
                                7: GM_ACT_TOO_LARGE, GM_REQ_CHUNKED, gm_rejects, build flags; 6: n_rsl_reversed;
                                5: gm_update_upstream / gm_peers_migrate; 4: union-DFA stats */
 
@@ -46,6 +46,10 @@ extern "C" {
 #define GM_E_NODEVICE   -8   /* compute call on a compile-only context                 */
 #define GM_E_STALE      -9   /* gm_update_upstream: the live generation changed under it
                                 (a load or another update published first); nothing published */
+#define GM_E_EARLIER   -10   /* gm_match_batch: an EARLIER batch of the stream completed void in the
+                                sync this call forced (PENDING_MAX unsynced batches, or a GM_BATCH_HOST
+                                batch behind device ones); this batch was not enqueued.
+                                gm_sync_batches names the void batch(es) */
 
 /* ---------------------------------------------------------------- gm_create flags */
 #define GM_CREATE_COMPILE_ONLY  0x1u  /* no HIP device: compile + stats only (host tests) */
@@ -294,8 +298,8 @@ int         gm_load_generation(gm_ctx *ctx, const void *blob, size_t len, uint32
  * call enqueues every stage and returns without waiting for the device (no host round trip for
  * intermediate counts -- they stay in device status words).  out[i] receives the verdict of
  * reqs[i]; the hit ids of request i are hit_ids[out[i].first_hit_off .. + n_hits), ascending,
- * requests in order.  gm_sync(ctx, stream) completes the stream's last batch and reports
- * capacity overflow (GM_E_OVERFLOW: the batch's verdicts are void; an internal WAF buffer that
+ * requests in order.  gm_sync(ctx, stream) completes the stream's pending batches (the multi-batch
+ * contract below) and reports capacity overflow (GM_E_OVERFLOW: a batch's verdicts are void; an internal WAF buffer that
  * overflowed is doubled for the stream's next batch, so a retry of the batch succeeds once the
  * buffers fit the traffic).
  * Thread-safe per (ctx, stream) pair: each stream has its own scratch buffers, so batches on
@@ -307,6 +311,23 @@ int         gm_load_generation(gm_ctx *ctx, const void *blob, size_t len, uint32
 int         gm_match_batch(gm_ctx *ctx, const gm_batch *in, gm_verdict *out,
                            uint32_t *hit_ids, size_t hit_cap, void *stream);
 int         gm_sync(gm_ctx *ctx, void *stream);
+
+/* The multi-batch contract.  A stream may hold up to 64 (PENDING_MAX) enqueued, unsynced batches;
+ * gm_sync completes ALL of them (not just the last), in enqueue order, and its GM_E_OVERFLOW means
+ * "at least one of them is void".  Until the gm_sync that completes a batch, its reqs / arena /
+ * out / hit_ids buffers must stay allocated and unmodified: a batch whose WAF dedupe set overflowed
+ * is completed inside gm_sync by re-running it (the stream's last batch by a continuation over its
+ * scratch, earlier ones whole from their inputs).  The 65th unsynced gm_match_batch, and a
+ * GM_BATCH_HOST batch behind device batches, first completes the earlier ones synchronously; if one
+ * of those is void it returns GM_E_EARLIER and does not enqueue the new batch.
+ * gm_sync_batches is gm_sync with the outcome per batch: it completes the stream's pending batches
+ * and writes status[i] (GM_OK, or GM_E_OVERFLOW for a void batch -- its verdicts are garbage and its
+ * counters were not committed: retry it, and only it) for every batch completed since the previous
+ * gm_sync / gm_sync_batches on the stream, forced completions included, in enqueue order; it
+ * returns that number of batches (entries past `cap` are not written), or a negative GM_E_* for an
+ * error no batch status describes (HIP; gm_parse_requests / gm_upstream_uris capacity, which gm_sync
+ * reports the same way; the statuses are then kept for the next call).  gm_sync discards them. */
+int         gm_sync_batches(gm_ctx *ctx, void *stream, int32_t *status, size_t cap);
 
 /* Per-location and per-signature hit counters of this device, u64, cumulative since the
  * generation was loaded (or gm_counters_reset): [0, n_locations) locations,

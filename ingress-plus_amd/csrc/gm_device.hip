@@ -1225,6 +1225,7 @@ __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, co
     }
     // (`return` answers in the rewrite phase, before the access phase)
     if (L.kind == LK_RETURN) { o.action = is_redirect(L.ret_code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = L.ret_code; return; }
+    if (fin == (uint32_t)loc && L.kind == LK_PROXY) o.kind = GM_ROUTE_PLAIN;   // (a 403 / 413 keeps the route)
     if (L.access != GM_NONE) {   // allow / deny (the FAST pass sent such locations here)
         const int a = access_eval(A, rp, *t.self, L.access, h.servers[o.server].realip);
         if (a == 1) { o.action = GM_ACT_FORBIDDEN; o.status = 403; return; }
@@ -1232,7 +1233,6 @@ __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, co
     }
     if (L.kind == LK_STATUS) { o.action = GM_ACT_RETURN; o.status = 200; return; }
     if (L.kind != LK_PROXY) { o.action = GM_ACT_NOT_FOUND; o.status = 404; return; }
-    if (fin == (uint32_t)loc) o.kind = GM_ROUTE_PLAIN;
     if (chunked && blen > L.body_max) { too_large(o); return; }
     o.action = GM_ACT_PROXY; o.status = 0; o.ups = L.upstream; o.waf = L.waf_mode;
 }
@@ -1556,6 +1556,10 @@ struct Scratch {
         gm_verdict *h_out = nullptr; uint32_t *h_hits = nullptr; size_t h_hit_cap = 0;
     };
     std::vector<Replay> pending;
+    // per-batch outcome (GM_OK / GM_E_OVERFLOW) of the batches completed since the last gm_sync /
+    // gm_sync_batches, in enqueue order: appended by each completion (a forced one in gm_match_batch
+    // too), handed out and cleared by the next explicit sync
+    std::vector<int32_t> sync_log;
     bool last_is_batch = false;   // the stream's last call was a gm_match_batch (its scratch in place)
     ~Scratch() {
         for (void *p : {(void *)d_status, (void *)d_blk2rec, (void *)d_cand, (void *)d_surv, (void *)d_pairs,
@@ -2793,8 +2797,11 @@ static int sync_pending(gm_ctx *c, Scratch *S) {
                 c->last_hits = S->h_status[4];
             }
         }
+        ovs[i] = ov;
         err |= ov;
     }
+    // (the same conditions as the batch-void errors below, per batch)
+    for (uint32_t ov : ovs) S->sync_log.push_back((ov & (OV_HITS | OV_DEC)) || ov_held(ov) ? GM_E_OVERFLOW : GM_OK);
     if (parse_ov) return fail(c, GM_E_OVERFLOW, "gm_parse_requests: arena capacity exceeded");
     if (upuri_ov) return fail(c, GM_E_OVERFLOW, "gm_upstream_uris: output capacity exceeded");
     if (err & OV_HITS) return fail(c, GM_E_OVERFLOW, "hit_ids capacity exceeded (the batch's counters were not committed)");
@@ -2817,6 +2824,9 @@ int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit
     // oldest are completed here first (synchronously), so no batch's overflow goes unreported
     if (S->pending.size() >= PENDING_MAX) {
         const int e0 = sync_pending(c, S);
+        if (e0 == GM_E_OVERFLOW)
+            return fail(c, GM_E_EARLIER, "an earlier batch of this stream completed void in the forced sync (" +
+                                         t_err + "); this batch was not enqueued");
         if (e0) return e0;
     }
     std::shared_lock<std::shared_mutex> lk(c->gen_mu);
@@ -2845,6 +2855,9 @@ int gm_match_batch(gm_ctx *c, const gm_batch *in, gm_verdict *out, uint32_t *hit
     // holds one staged batch at a time (the staging buffer is reused), so earlier ones complete first
     if (!S->pending.empty()) {
         const int e0 = sync_pending(c, S);
+        if (e0 == GM_E_OVERFLOW)
+            return fail(c, GM_E_EARLIER, "an earlier batch of this stream completed void before the staged batch (" +
+                                         t_err + "); this batch was not enqueued");
         if (e0) return e0;
         rp.slot = 0;
     }
@@ -2878,7 +2891,26 @@ int gm_sync(gm_ctx *c, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     Scratch *S = scratch_for(c, s);
     if (!S) return fail(c, GM_E_NOMEM, t_err);
-    return sync_pending(c, S);
+    const int e = sync_pending(c, S);
+    S->sync_log.clear();
+    return e;
+}
+
+int gm_sync_batches(gm_ctx *c, void *stream, int32_t *status, size_t cap) {
+    if (!c || (!status && cap)) return fail(c, GM_E_INVAL, "null argument");
+    if (c->flags & GM_CREATE_COMPILE_ONLY) return 0;
+    HIPCHK(c, hipSetDevice(c->dev));
+    hipStream_t s = (hipStream_t)stream;
+    Scratch *S = scratch_for(c, s);
+    if (!S) return fail(c, GM_E_NOMEM, t_err);
+    const int e = sync_pending(c, S);
+    if (e && e != GM_E_OVERFLOW) return e;   // (a HIP error: the log stays for the next call)
+    const uint32_t parse_ov = S->h_status[PARSE_STATUS_WORD + 3], upuri_ov = S->h_status[UPURI_STATUS_WORD];
+    if (e && (parse_ov || upuri_ov)) return e;   // not a gm_match_batch's: reported as gm_sync does
+    const size_t n = S->sync_log.size();
+    for (size_t i = 0; i < n && i < cap; i++) status[i] = S->sync_log[i];
+    S->sync_log.clear();
+    return n > 0x7FFFFFFFu ? 0x7FFFFFFF : (int)n;
 }
 
 int gm_counters(gm_ctx *c, uint64_t *out, size_t n) {

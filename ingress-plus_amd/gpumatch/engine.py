@@ -18,10 +18,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GM_LIB") or os.path.join(os.path.dirname(HERE), "libgpumatch.so")
 
 GM_OK = 0
-GM_ABI_VERSION = 9   # include/gpumatch.h
+GM_ABI_VERSION = 10   # include/gpumatch.h
 GM_E_OVERFLOW = -4
 GM_E_STALE = -9
 GM_E_COMM = -7
+GM_E_EARLIER = -10
 GM_CREATE_COMPILE_ONLY = 0x1
 GM_BATCH_HOST = 0x1
 
@@ -80,7 +81,7 @@ EXPORTS = ["gm_create", "gm_destroy", "gm_abi_version", "gm_load_generation", "g
            "gm_counters", "gm_counters_reset", "gm_comm_unique_id", "gm_comm_init", "gm_counters_allreduce",
            "gm_stats", "gm_last_error", "gm_normalize_uris", "gm_counters_global", "gm_parse_requests",
            "gm_peers_init", "gm_select_peers", "gm_release_peers", "gm_peer_address", "gm_upstream_uris",
-           "gm_update_upstream", "gm_peers_migrate", "gm_rejects", "gm_build_hash"]
+           "gm_update_upstream", "gm_peers_migrate", "gm_rejects", "gm_build_hash", "gm_sync_batches"]
 
 # gm_peer_state (include/gpumatch.h)
 PEER_STATE_DTYPE = np.dtype([("conns", "<u4"), ("current_weight", "<i4"), ("flags", "<u4"), ("reserved", "<u4")])
@@ -107,6 +108,7 @@ def lib():
         L.gm_match_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(GmBatch), ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_size_t, ctypes.c_void_p]
         L.gm_sync.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.gm_sync_batches.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
         L.gm_counters.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
         L.gm_counters_reset.argtypes = [ctypes.c_void_p]
         L.gm_comm_unique_id.argtypes = [ctypes.c_void_p]
@@ -217,6 +219,15 @@ class Engine:
 
     def sync(self, stream=0):
         self._chk(lib().gm_sync(self.h, stream))
+
+    def sync_batches(self, stream=0, cap=256) -> list:
+        """gm_sync_batches: the outcome (GM_OK / GM_E_OVERFLOW) of every batch completed since the
+        stream's previous sync, in enqueue order."""
+        st = (ctypes.c_int32 * cap)()
+        n = lib().gm_sync_batches(self.h, stream, st, cap)
+        if n < 0:
+            self._chk(n)
+        return [int(st[i]) for i in range(min(n, cap))]
 
     def match_host(self, reqs: np.ndarray, arena: np.ndarray, hit_cap: int | None = None):
         """Host numpy in, host numpy out (staged through HBM by the library)."""

@@ -479,6 +479,52 @@ def test_two_batches_before_one_sync(torch_dev):
     assert_verdicts_equal(got_b, exp_b, gh_b, eh_b, "queued batch B after a void A")
     assert np.array_equal(e.counters(), _one_batch_counters(e, got_b, gh_b))
     e.close()
+    # the same, through gm_sync_batches: the void batch is named (B, A, B: only the middle one)
+    e = engine.Engine(0)
+    e.load(b, 5)
+    B1 = enqueue(e, rb, ab, 8 * len(rb) + 1024)
+    A = enqueue(e, ra, aa, 10)
+    B2 = enqueue(e, rb, ab, 8 * len(rb) + 1024)
+    assert e.sync_batches(0) == [engine.GM_OK, engine.GM_E_OVERFLOW, engine.GM_OK]
+    assert e.sync_batches(0) == []   # handed out once
+    for bufs in (B1, B2):
+        got_b, gh_b = read(bufs, int(len(eh_b)))
+        assert_verdicts_equal(got_b, exp_b, gh_b, eh_b, "queued batch B beside a void A")
+    assert np.array_equal(e.counters(), 2 * _one_batch_counters(e, got_b, gh_b))
+    e.close()
+
+
+def test_forced_sync_names_the_earlier_batch(torch_dev):
+    """the 65th unsynced gm_match_batch completes the earlier 64 first; when one of them
+    is void it answers GM_E_EARLIER (not the new batch's own outcome) and does not enqueue the new
+    batch; gm_sync_batches then names the void one among the 64."""
+    torch, dev = torch_dev
+    ss, b = workloads.c4_stress_generation()
+    r, a = records.gen_c4(64, ss, seed=workloads.C4_STRESS_POOL_SEED + 21, plant_rate=0.5, stress=True)
+    exp, eh = Oracle(b, 5).match(r, a)
+    assert len(eh) > 4
+    e = engine.Engine(0)
+    e.load(b, 5)
+    d_reqs, d_arena = _to_dev(torch, dev, r, a)
+    outs = [torch.empty(len(r) * 32, dtype=torch.uint8, device=dev) for _ in range(65)]
+    hits = [torch.zeros(len(eh) + 1024, dtype=torch.int32, device=dev) for _ in range(65)]
+    for i in range(64):
+        cap = 2 if i == 7 else hits[i].numel()   # batch 7 overflows its hit_ids
+        e.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), len(a), len(r), outs[i].data_ptr(), hits[i].data_ptr(),
+                    cap, 0)
+    with pytest.raises(engine.GmError) as ei:
+        e.match_ptr(d_reqs.data_ptr(), d_arena.data_ptr(), len(a), len(r), outs[64].data_ptr(), hits[64].data_ptr(),
+                    hits[64].numel(), 0)
+    assert ei.value.code == engine.GM_E_EARLIER
+    st = e.sync_batches(0)
+    assert len(st) == 64 and st[7] == engine.GM_E_OVERFLOW
+    assert all(x == engine.GM_OK for i, x in enumerate(st) if i != 7)
+    got = outs[63].cpu().numpy().view(records.VERDICT_DTYPE)
+    assert_verdicts_equal(got, exp, hits[63][:len(eh)].cpu().numpy().view(np.uint32), eh, "batch 63")
+    # 63 clean batches counted, the void one and the refused 65th not
+    one = _one_batch_counters(e, got, hits[63][:len(eh)].cpu().numpy().view(np.uint32))
+    assert np.array_equal(e.counters(), 63 * one)
+    e.close()
 
 
 GM_ROUTE_HELD = 0x80
