@@ -2266,20 +2266,20 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
             sl.first_group = (uint32_t)alw.size();
             sl.n_groups = (uint32_t)(g1 - g0);
             sl.server = server;
-            // clsa[b * NGP + j] = group j's row 0 offset in the slice + 2 x byte b's class in group j:
-            // the byte offset of b's transition column, so a step adds it to the chain's row and
-            // reads (alw_cls_bytes; NGP = 4 or 8 u32 per byte, one or two 16-byte LDS reads)
-            const uint32_t ngp = alw_cls_ngp(sl.n_groups), hdr = alw_cls_bytes(sl.n_groups);
+            // the dead row (zeros), then clsa[b * NGB + j] = 2 x byte b's class in group j: the byte
+            // offset of b's column within group j's rows (alw_cls_bytes; NGB = 4 or 8 bytes per byte)
+            const uint32_t ngb = alw_cls_ngb(sl.n_groups), hdr = alw_cls_bytes(sl.n_groups);
             std::vector<uint32_t> tro(g1 - g0, 0);
             {
                 uint32_t o = hdr;
                 for (size_t j = g0; j < g1; j++) { tro[j - g0] = o; o += (uint32_t)((tab_bytes(gdfa[j]) + 15) & ~size_t(15)); }
+                if (o > 4u * 65535u) alw_layout_err = true;   // (rows / 4 fit a u16: never past the LDS)
             }
-            std::vector<uint32_t> clsa((size_t)(ALW_CLS_IDENTITY + 1) * ngp, 0);
+            std::vector<uint8_t> clsa(hdr, 0);
             for (size_t j = g0; j < g1; j++) {
                 for (int b = 0; b < 256; b++)
-                    clsa[(size_t)b * ngp + (j - g0)] = tro[j - g0] + 2u * gdfa[j].cls[b];
-                clsa[(size_t)ALW_CLS_IDENTITY * ngp + (j - g0)] = tro[j - g0] + 2u * (uint32_t)gdfa[j].n_classes;
+                    clsa[ALW_DEAD_BYTES + (size_t)b * ngb + (j - g0)] = (uint8_t)(2u * gdfa[j].cls[b]);
+                clsa[ALW_DEAD_BYTES + (size_t)ALW_CLS_IDENTITY * ngb + (j - g0)] = (uint8_t)(2u * (uint32_t)gdfa[j].n_classes);
             }
             const uint8_t *cb = reinterpret_cast<const uint8_t *>(clsa.data());
             alw_pack.insert(alw_pack.end(), cb, cb + hdr);
@@ -2302,15 +2302,18 @@ CompileResult compile_generation(const uint8_t *blob, size_t len, uint32_t gen) 
                 std::vector<uint32_t> perm(S, 0);
                 uint32_t nid = 1;
                 for (size_t q = 1; q < S; q++) if (!emits[q]) perm[q] = nid++;
-                g.emit_row = (uint32_t)(2 * R * nid);
+                // a state's row: its byte offset in the slice / 4; the dead state 0 (the shared dead row)
+                const uint32_t gb = tro[j - g0];
+                auto row4 = [&](uint32_t id) -> uint16_t { return id ? (uint16_t)((gb + 2 * R * id) >> 2) : (uint16_t)0; };
+                g.emit_row = row4(nid);
                 for (size_t q = 1; q < S; q++) if (emits[q]) perm[q] = nid++;
-                g.start_row = (uint32_t)(2 * R * perm[1]);
+                g.start_row = row4(perm[1]);
                 std::vector<uint16_t> rows(S * R, 0);
                 for (size_t q = 1; q < S; q++) {
                     const size_t o = (size_t)perm[q] * R;
                     for (size_t c = 0; c < Cn; c++)
-                        rows[o + c] = (uint16_t)(2 * R * perm[m.trans[q * Cn + c] & 0x3FFF]);
-                    rows[o + Cn] = (uint16_t)(2 * R * perm[q]);   // the identity column
+                        rows[o + c] = row4(perm[m.trans[q * Cn + c] & 0x3FFF]);
+                    rows[o + Cn] = row4(perm[q]);   // the identity column
                     rows[o + Cp] = (uint16_t)m.emit[q]; rows[o + Cp + 1] = (uint16_t)(m.emit[q] >> 16);
                     rows[o + Cp + 2] = (uint16_t)m.endm[q]; rows[o + Cp + 3] = (uint16_t)(m.endm[q] >> 16);
                 }

@@ -37,6 +37,16 @@
 
 using namespace gm;
 
+// uint64_t is unsigned long here, for which HIP's device min / max have no overload: such calls
+// (or a mix with unsigned long long) resolved to the double ones (v_cvt_f64 ... v_min_f64 per
+// call, exact only below 2^53)
+__device__ __forceinline__ unsigned long min(unsigned long a, unsigned long b) { return a < b ? a : b; }
+__device__ __forceinline__ unsigned long max(unsigned long a, unsigned long b) { return a > b ? a : b; }
+__device__ __forceinline__ unsigned long min(unsigned long a, unsigned long long b) { return a < b ? a : (unsigned long)b; }
+__device__ __forceinline__ unsigned long min(unsigned long long a, unsigned long b) { return a < b ? (unsigned long)a : b; }
+__device__ __forceinline__ unsigned long max(unsigned long a, unsigned long long b) { return a > b ? a : (unsigned long)b; }
+__device__ __forceinline__ unsigned long max(unsigned long long a, unsigned long b) { return a > b ? (unsigned long)a : b; }
+
 // ============================================================================ device helpers
 namespace {
 
@@ -1839,10 +1849,17 @@ gm_ctx *gm_create(int hip_device, uint32_t flags) {
                               (const void *)k_rloc_multi<3>, (const void *)k_rloc_multi<4>,
                               (const void *)k_rloc_multi<5>, (const void *)k_rloc_multi<6>,
                               (const void *)k_rloc_multi<7>, (const void *)k_rloc_multi<8>};
-        for (const void *f : alws)
+        for (const void *f : alws) {
             if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ALWAYS_LDS_BYTES) != hipSuccess) {
                 t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
             }
+            // their chains address the slice by its LDS offset (alw_step): the dynamic LDS must start
+            // at 0, i.e. the kernels hold no static __shared__
+            hipFuncAttributes fa{};
+            if (hipFuncGetAttributes(&fa, f) != hipSuccess || fa.sharedSizeBytes != 0) {
+                t_err = "union-DFA kernel with static LDS (alw_step needs its slice at LDS offset 0)"; delete c; return nullptr;
+            }
+        }
         if (hipFuncSetAttribute((const void *)k_rloc_heads, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)(HEADS_LDS_SLOTS * RSL_HEAD_WORDS * 4)) != hipSuccess) {
             t_err = "hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed"; delete c; return nullptr;
@@ -3070,11 +3087,10 @@ extern "C" int gm_debug_alw_profile(gm_ctx *c, const gm_req *reqs, const uint8_t
         const DAlwSlice &sl = sls[si];
         if (sl.server != GM_NONE) continue;
         const uint8_t *P = img + h.off_alw_pack + sl.off;
-        const uint32_t *clsa = reinterpret_cast<const uint32_t *>(P);
-        const uint32_t ngp = alw_cls_ngp(sl.n_groups);
+        const uint8_t *clsa = P + ALW_DEAD_BYTES;
+        const uint32_t ngb = alw_cls_ngb(sl.n_groups);
         for (uint32_t j = 0; j < sl.n_groups; j++) {
             const DAlwGroup &gr = grs[sl.first_group + j];
-            const uint8_t *G = P + gr.tr_off;
             for (uint32_t r = 0; r < n; r++) {
                 const gm_req &q = reqs[r];
                 const uint32_t lens[4] = {q.uri_len, q.args_len, q.hdr_len, q.body_len};
@@ -3086,7 +3102,7 @@ extern "C" int gm_debug_alw_profile(gm_ctx *c, const gm_req *reqs, const uint8_t
                         for (uint32_t i = 0; i < lens[z] && row; i++) {
                             const uint32_t b = arena[o + i];
                             uint16_t nx;
-                            memcpy(&nx, P + row + clsa[b * ngp + j], 2);   // (the column includes tr_off)
+                            memcpy(&nx, P + 4 * row + clsa[b * ngb + j], 2);   // (rows: slice offset / 4)
                             tot++;
                             if (row == gr.start_row) { at++; if (nx == gr.start_row) stay++; }
                             row = nx;
@@ -3409,11 +3425,11 @@ extern "C" int gm_parse_requests(gm_ctx *c, const uint8_t *wire, const gm_wire_m
     if ((e = grow(c, s, S->d_wsize, S->cap_wsize, (size_t)n + 1))) return e;
     if ((e = grow(c, s, S->d_wbase, S->cap_wbase, (size_t)n + 1))) return e;
     if ((e = grow(c, s, S->d_wtemp, S->cap_wtemp, tmp))) return e;
-    // the parser's waves are persistent (grid-stride): 8 waves per SIMD are resident (WIRE_OCC),
-    // i.e. 8 blocks per CU -- a larger grid would only queue, and its per-wave $uri scratch
+    // the parser's waves are persistent (grid-stride): GM_WIRE_WPE waves per SIMD are resident (WIRE_OCC),
+    // i.e. GM_WIRE_WPE blocks per CU -- a larger grid would only queue, and its per-wave $uri scratch
     // (WIRE_SCR each) would hold memory no resident wave uses
     const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + WIRE_WAVES - 1) / WIRE_WAVES,
-                                                                     (uint32_t)c->cu_count * 8));
+                                                                     (uint32_t)c->cu_count * GM_WIRE_WPE));
     if ((e = grow(c, s, S->d_wscr, S->cap_wscr, (size_t)blocks * WIRE_WAVES * WIRE_SCR))) return e;
     if ((e = grow(c, s, S->d_wsum, S->cap_wsum, (size_t)n * sizeof(WireSum)))) return e;
     WireSum *wsum = reinterpret_cast<WireSum *>(S->d_wsum);
@@ -3666,7 +3682,7 @@ static constexpr uint32_t kBuildFlags =
 #endif
 #if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_STG != 32 || \
     GM_ROUTE_BPC != 1 || GM_ROUTE_PRIO != 0 || GM_ROUTE_WPE != GM_ROUTE_WPE_SHIPPED || GM_EXP_GRIDMUL != 8 || \
-    GM_EXP_WPE != 3 || GM_RLOC_CTX != 1 || GM_RLOC_PREF != 0 || GM_ALW_SLICE_GROUPS != 8 || GM_WIRE_WPE != 8 || \
+    GM_EXP_WPE != 3 || GM_RLOC_CTX != 1 || GM_RLOC_PREF != 0 || GM_ALW_SLICE_GROUPS != 8 || GM_WIRE_WPE != 6 || \
     GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1 || GM_EXACT_BPC != 6 || !defined(GM_DFA_INL_SHIPPED)
     GM_BUILD_TUNING |
 #endif

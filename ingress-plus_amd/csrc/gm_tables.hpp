@@ -303,25 +303,32 @@ __host__ __device__ inline uint32_t peer_draw(uint64_t lo, uint64_t hi, uint32_t
 // pass over a zone answers a whole group.  Groups are packed into slices of <= ALW_SLICE_GROUPS
 // groups that fit ALWAYS_LDS_BYTES together; k_waf_always_multi stages one slice in LDS and runs a
 // transition chain per group of the slice.
-// Slice pack (16-B aligned): clsa u32[257 * NGP] (NGP = 4 for up to four groups, else 8; entry
-// b * NGP + j = group j's tr_off + 2 x byte b's class in group j: the offset of b's column in the
-// group's row 0, so a chain's step is one add to its row and one u16 read, and a byte's entries for
-// four groups are one 16-byte LDS read; entry 256 the identity columns) | per group, its rows.  A
-// row (state) is Cp + 4 u16: the transitions of the C classes, the identity column (the row's own
-// offset), padded to Cp = alw_row_cols(C), then the state's emit mask and end mask (u32 each).  A transition
-// is the target row's byte offset in the group: the step needs no multiply, and row 0 (the dead
-// state) is all zeros.  The emitting states are numbered last, from row emit_row on: a chain
-// entered one within a chunk iff the largest row it took there is >= emit_row (one max per step,
-// no flag bit to strip).
+// Slice pack (16-B aligned): the shared dead row (ALW_DEAD_BYTES of zeros at offset 0) | clsa
+// u8[257 * NGB] (NGB = 4 for up to four groups, else 8; entry b * NGB + j = 2 x byte b's class in
+// group j: the byte offset of b's column within a row of group j, so the class columns of a byte
+// for every group of the slice are one 4- or 8-byte LDS read, and the read's lanes spread over the
+// banks as the bytes do -- a 16-byte entry per byte took ~9 LDS cycles per wave-byte on C4 stress
+// text against ~4 for these; entry 256 the identity columns) | per group, its rows.  A row (state)
+// is Cp + 4 u16: the transitions of the C classes, the identity column (the row's own value),
+// padded to Cp = alw_row_cols(C), then the state's emit mask and end mask (u32 each).  A
+// transition, and a chain's row, is the target row's byte offset IN THE SLICE / 4 (rows are 4-byte
+// aligned; u16 reaches 256 KiB): a step is one shift-add (row << 2) + column and one u16 read, with
+// no per-group base, and the value 0 -- the dead state of every group -- reads the shared dead row.
+// The emitting states are numbered last, from row emit_row on: a chain entered one within a chunk
+// iff the largest row it took there is >= emit_row (one max per step, no flag bit to strip).
 constexpr uint32_t ALWAYS_LDS_BYTES = 160 * 1024;
-constexpr uint32_t ALW_GROUP_BYTES = 64 * 1024 - 64;   // row byte offsets fit a u16 with the flag bit
+constexpr uint32_t ALW_GROUP_BYTES = 64 * 1024 - 64;
 constexpr uint32_t ALW_GROUP_MAX = 32;
-constexpr uint32_t ALW_CLASSES_MAX = 127;
-__host__ __device__ constexpr uint32_t alw_cls_ngp(uint32_t n_groups) { return n_groups <= 4 ? 4u : 8u; }
-// entries 0..255: the bytes; entry 256: every group's identity column (a row's own offset: a step
+constexpr uint32_t ALW_CLASSES_MAX = 127;   // (2 x the identity class fits the u8 column)
+// the shared dead row: zeros over every group's columns and masks (2 x 128 + 8 bytes)
+constexpr uint32_t ALW_DEAD_BYTES = 272;
+__host__ __device__ constexpr uint32_t alw_cls_ngb(uint32_t n_groups) { return n_groups <= 4 ? 4u : 8u; }
+// entries 0..255: the bytes; entry 256: every group's identity column (a row's own value: a step
 // that changes nothing, for the bytes past a chunk's end)
 constexpr uint32_t ALW_CLS_IDENTITY = 256;
-__host__ __device__ constexpr uint32_t alw_cls_bytes(uint32_t n_groups) { return 257u * 4u * alw_cls_ngp(n_groups); }
+__host__ __device__ constexpr uint32_t alw_cls_bytes(uint32_t n_groups) {
+    return ALW_DEAD_BYTES + ((257u * alw_cls_ngb(n_groups) + 15u) & ~15u);
+}
 // a group's row: its classes, the identity column (class n_classes), padded to even, then the emit
 // and end masks (u32 each)
 __host__ __device__ constexpr uint32_t alw_row_cols(uint32_t n_classes) { return (n_classes + 2) & ~1u; }
@@ -331,15 +338,15 @@ __host__ __device__ constexpr uint32_t alw_row_cols(uint32_t n_classes) { return
 constexpr uint32_t ALW_SLICE_GROUPS = GM_ALW_SLICE_GROUPS;
 constexpr uint32_t ALW_BUILD_STATES = 8192;   // product states before minimisation
 struct DAlwGroup {
-    uint32_t tr_off;         // byte offset of row 0 from the slice start
+    uint32_t tr_off;         // byte offset of the group's rows from the slice start
     uint32_t mask_off;       // byte offset of the emit mask within a row (2 Cp); the end mask follows
-    uint32_t start_row;      // byte offset of the start state's row (row 1)
+    uint32_t start_row;      // the start state's row (its byte offset in the slice / 4)
     uint32_t n_classes, n_states;
     uint32_t zone_mask[4];   // members (bit k) that scan zone z
     uint32_t first;          // member k: a location slice's value alw_rule[first + k]; an always-run
                              // group's rule list alw_rl[alw_rule[first + k] .. alw_rule[first + k + 1])
     uint32_t zones;          // zones some member scans
-    uint32_t emit_row;       // byte offset of the first emitting state's row (rows past it emit too)
+    uint32_t emit_row;       // the first emitting state's row (slice offset / 4; rows past it emit too)
 };
 struct DAlwSlice {
     uint32_t off, len;       // bytes of the pack
