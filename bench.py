@@ -419,11 +419,12 @@ def stress_leg(torch, engine, records, workloads, args, local):
             "stage_ms": {k: float(np.mean(v)) for k, v in ms.items()}}
 
 
-# The committed profile of this bench's C4 scan (scripts/scan_profile.py over a rocprofv3
+# The committed profiles of this bench's C4 scan (scripts/scan_profile.py over a rocprofv3
 # --kernel-trace --stats run and the PMC passes of scripts/pmc.sh on the same tree), stamped with
-# the hash of the kernel sources.  Selected by name, and used only when that hash matches the tree
-# being benched: a new kernel never pairs with an old profile (VERDICT r2 "Next round" 1).
-SCAN_PROFILE = "profiles/r5f_scan_profile.json"
+# the hash of the kernel sources: profiles/*_scan_profile.json.  The one whose hash is the
+# library's is used; none is used when no hash matches: a new kernel never pairs with an old
+# profile (VERDICT r2 "Next round" 1).
+SCAN_PROFILE_GLOB = "profiles/*_scan_profile.json"
 
 
 def profiled(zone_bytes: int, lib_hash: str) -> dict:
@@ -439,20 +440,29 @@ def profiled(zone_bytes: int, lib_hash: str) -> dict:
     from scan_profile import csrc_hash
     here = lib_hash
     tree = csrc_hash(ROOT)
-    path = os.path.join(ROOT, SCAN_PROFILE)
     out = {"traffic": None, "frac_profiled": None, "csrc_hash": here, "tree_hash": tree,
            "anchor": "frac_profiled (rocprofv3 average of k_waf_scan; `frac` is the HIP-event time on this run)"}
     if here != tree:
         out["lib_status"] = f"library built from {here}, sources beside it hash {tree}"
-    if not os.path.exists(path):
-        out["profile_status"] = f"no profile ({SCAN_PROFILE} missing)"
+    import glob
+    found = []
+    for path in sorted(glob.glob(os.path.join(ROOT, SCAN_PROFILE_GLOB)), key=os.path.getmtime):
+        try:
+            found.append((os.path.relpath(path, ROOT), json.load(open(path))))
+        except (OSError, ValueError):
+            continue
+    if not found:
+        out["profile_status"] = f"no profile ({SCAN_PROFILE_GLOB})"
         return out
-    s = json.load(open(path))
-    out["profile_source"] = SCAN_PROFILE
-    if s.get("csrc_hash") != here:
-        out["profile_status"] = (f"stale: profiled sources {s.get('csrc_hash')} != benched sources {here}; "
-                                 "traffic and frac_profiled withheld")
+    same = [(p, s) for p, s in found if s.get("csrc_hash") == here]
+    if not same:
+        p, s = found[-1]
+        out["profile_status"] = (f"stale: no profile of the benched sources {here} (newest: {p}, "
+                                 f"{s.get('csrc_hash')}); traffic and frac_profiled withheld")
         return out
+    # (of several same-tree profiles, one with its PMC passes first, then the newest)
+    p, s = sorted(same, key=lambda ps: ps[1].get("pmc_csrc_hash") == here)[-1]
+    out["profile_source"] = p
     out["profile_status"] = "same tree"
     avg = s.get("k_waf_scan_avg_ns")
     if avg:
