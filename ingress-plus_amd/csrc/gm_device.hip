@@ -18,6 +18,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <chrono>
 #include <cstring>
@@ -205,6 +206,63 @@ __device__ bool hdr_name_is(const uint8_t *A, uint64_t ns, uint32_t nl, const ui
     return true;
 }
 
+// A header (one line: no join), cookie or argument value as one arena span [vo, vo + vl):
+// ngx_http_variable_unknown_header's first line, ngx_http_parse_multi_header_lines over every
+// Cookie line, ngx_http_arg.  false: no such header / cookie / argument (the value "").  Spans
+// stay in registers: rules_generic keeps them there instead of in a Val (lane-private memory).
+__device__ bool span_http(const uint8_t *A, uint64_t hdrs, uint32_t hlen, const uint8_t *nm, uint32_t nml,
+                          uint64_t &vo, uint32_t &vl) {
+    HdrIt it{hdrs, hdrs + hlen};
+    uint64_t ns, vs; uint32_t nl, l;
+    while (hdr_next(A, it, ns, nl, vs, l))
+        if (hdr_name_is(A, ns, nl, nm, nml)) { vo = vs; vl = l; return true; }
+    return false;
+}
+__device__ bool span_cookie(const uint8_t *A, uint64_t hdrs, uint32_t hlen, const uint8_t *nm, uint32_t nml,
+                            uint64_t &vo, uint32_t &vl) {
+    HdrIt it{hdrs, hdrs + hlen};
+    uint64_t ns, vs; uint32_t nl, l;
+    const uint8_t cookie[7] = "cookie";
+    while (hdr_next(A, it, ns, nl, vs, l)) {
+        if (!hdr_name_is(A, ns, nl, cookie, 6)) continue;
+        if (nml > l) continue;
+        uint64_t start = vs, end = vs + l;
+        while (start < end) {
+            bool ok = end - start >= nml;
+            for (uint32_t k = 0; ok && k < nml; k++) if (lc(A[start + k]) != nm[k]) ok = false;
+            if (ok) {
+                start += nml;
+                while (start < end && A[start] == ' ') start++;
+                // (nginx: `*start++ != '='` -- the byte tested is consumed even when it is not '=',
+                // so a ';' or ',' there does not end the skip below)
+                if (start < end && A[start++] == '=') {
+                    while (start < end && A[start] == ' ') start++;
+                    const uint64_t last = find_byte(A, start, end, ';');
+                    vo = start; vl = (uint32_t)(last - start);
+                    return true;
+                }
+            }
+            start = find_byte2(A, start, end, ';', ',');
+            if (start < end) start++;
+            while (start < end && A[start] == ' ') start++;
+        }
+    }
+    return false;
+}
+// the first occurrence of the name at an argument start ("&" or the beginning) followed by '=':
+// only argument starts can qualify, so they are visited directly
+__device__ bool span_arg(const uint8_t *A, uint64_t a, uint32_t n, const uint8_t *nm, uint32_t L,
+                         uint64_t &vo, uint32_t &vl) {
+    for (uint32_t p = 0; p + L < n;) {
+        bool ok = true;
+        for (uint32_t k = 0; ok && k < L; k++) if (lc(A[a + p + k]) != nm[k]) ok = false;
+        const uint32_t amp = (uint32_t)(find_byte(A, a + p, a + n, '&') - a);
+        if (ok && A[a + p + L] == '=') { vo = a + p + L + 1; vl = amp - (p + L + 1); return true; }
+        p = amp + 1;
+    }
+    return false;
+}
+
 __device__ void get_var(Ctx &c, const GTab &t, uint32_t src_id, Val &v) {
     v.clear();
     const DSrc s = t.srcs[src_id];
@@ -267,13 +325,15 @@ __device__ void get_var(Ctx &c, const GTab &t, uint32_t src_id, Val &v) {
         return;
     }
     const uint8_t *nm = t.bytes + s.name_off;
+    uint64_t vo = 0;
+    uint32_t vl = 0;
     if (s.kind == SRC_HTTP) {
+        if (!s.join) { if (span_http(A, c.hdrs, r.hdr_len, nm, s.name_len, vo, vl)) v.add(A + vo, vl); return; }
         HdrIt it{c.hdrs, c.hdrs + r.hdr_len};
-        uint64_t ns, vs; uint32_t nl, vl;
+        uint64_t ns, vs; uint32_t nl;
         bool have = false;
         while (hdr_next(A, it, ns, nl, vs, vl)) {
             if (!hdr_name_is(A, ns, nl, nm, s.name_len)) continue;
-            if (!s.join) { v.add(A + vs, vl); return; }
             if (have) v.add(c_const + (s.join == ';' ? 9 : 11), 2);
             v.add(A + vs, vl);
             have = true;
@@ -281,51 +341,11 @@ __device__ void get_var(Ctx &c, const GTab &t, uint32_t src_id, Val &v) {
         return;
     }
     if (s.kind == SRC_COOKIE) {
-        // ngx_http_parse_multi_header_lines over every Cookie line
-        HdrIt it{c.hdrs, c.hdrs + r.hdr_len};
-        uint64_t ns, vs; uint32_t nl, vl;
-        const uint8_t cookie[7] = "cookie";
-        while (hdr_next(A, it, ns, nl, vs, vl)) {
-            if (!hdr_name_is(A, ns, nl, cookie, 6)) continue;
-            if (s.name_len > vl) continue;
-            uint64_t start = vs, end = vs + vl;
-            while (start < end) {
-                bool ok = end - start >= s.name_len;
-                for (uint32_t k = 0; ok && k < s.name_len; k++) if (lc(A[start + k]) != nm[k]) ok = false;
-                if (ok) {
-                    start += s.name_len;
-                    while (start < end && A[start] == ' ') start++;
-                    if (start < end && A[start] == '=') {
-                        start++;
-                        while (start < end && A[start] == ' ') start++;
-                        const uint64_t last = find_byte(A, start, end, ';');
-                        v.add(A + start, (uint32_t)(last - start));
-                        return;
-                    }
-                }
-                start = find_byte2(A, start, end, ';', ',');
-                if (start < end) start++;
-                while (start < end && A[start] == ' ') start++;
-            }
-        }
+        if (span_cookie(A, c.hdrs, r.hdr_len, nm, s.name_len, vo, vl)) v.add(A + vo, vl);
         return;
     }
     if (s.kind == SRC_ARG) {
-        // ngx_http_arg
-        // the first occurrence of the name at an argument start ("&" or the beginning) followed
-        // by '=': only argument starts can qualify, so they are visited directly
-        uint64_t a = c.args;
-        uint32_t n = r.args_len, L = s.name_len;
-        for (uint32_t p = 0; p + L < n;) {
-            bool ok = true;
-            for (uint32_t k = 0; ok && k < L; k++) if (lc(A[a + p + k]) != nm[k]) ok = false;
-            const uint32_t amp = (uint32_t)(find_byte(A, a + p, a + n, '&') - a);
-            if (ok && A[a + p + L] == '=') {
-                v.add(A + a + p + L + 1, amp - (p + L + 1));
-                return;
-            }
-            p = amp + 1;
-        }
+        if (span_arg(A, c.args, r.args_len, nm, s.name_len, vo, vl)) v.add(A + vo, vl);
     }
 }
 
@@ -749,19 +769,23 @@ struct HotTabs {
     const DSmallLoc *small; const DLoc *locs; const uint8_t *name_bytes;
 };
 // NOV6: an IPv6 literal returns -2 (the caller's slow path): its byte loop indexes hw by a
-// variable, which puts the words in scratch for every request
-template <bool NOV6 = false>
-__device__ __forceinline__ int host_fast(const uint32_t (&hw)[8], uint32_t n, const GTab &t, const HotTabs &h,
+// variable, which puts the words in scratch for every request.  NW: the host's words in
+// registers, 8 (<= 32 bytes, the route's prefetched window) or 16 (<= 64 bytes, loaded by the
+// caller: round 6 -- C2's 38-byte VirtualServer host took the arena-byte path, a load per byte)
+template <bool NOV6 = false, int NW = 8>
+__device__ __forceinline__ int host_fast(const uint32_t (&hw)[NW], uint32_t n, const GTab &t, const HotTabs &h,
                                          uint32_t pi, uint32_t &server) {
+    static_assert(NW == 8 || NW == 16, "host words");
+    using M = typename std::conditional<NW == 8, uint32_t, uint64_t>::type;
     server = GM_NONE;
     int host_len;
-    if (NOV6 && (hw[0] & 0xFF) == '[') return -2;
-    if (!NOV6 && (hw[0] & 0xFF) == '[') {
+    if ((NOV6 || NW != 8) && (hw[0] & 0xFF) == '[') return -2;
+    if (!NOV6 && NW == 8 && (hw[0] & 0xFF) == '[') {
         int dot_pos = (int)n, state = 0;
         bool bad = false;
         host_len = (int)n;
         for (int i = 0; i < (int)n; i++) {
-            const uint32_t ch = byte_of(hw, i);
+            const uint32_t ch = (hw[(i >> 2) & (NW - 1)] >> (8 * (i & 3))) & 0xFF;
             if (ch == '.') { bad |= dot_pos == i - 1; dot_pos = i; }
             else if (ch == ':') { if (state == 0) { host_len = i; state = 2; } }
             else if (ch == '[') { if (i == 0) state = 1; }
@@ -771,24 +795,26 @@ __device__ __forceinline__ int host_fast(const uint32_t (&hw)[8], uint32_t n, co
         if (dot_pos == host_len - 1) host_len--;
         if (bad || host_len <= 0) return -1;
     } else {
-        uint32_t dots = 0, colons = 0, badm = 0;
+        M dots = 0, colons = 0;
+        uint32_t badm = 0;
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
+        for (int k = 0; k < NW; k++) {
             const int rem = (int)n - 4 * k;
             const uint32_t lm = rem >= 4 ? 0xFFFFFFFFu : rem > 0 ? (1u << (8 * rem)) - 1 : 0u;
             const uint32_t w = hw[k];
-            dots |= flags_nibble(byte_eq_flags(w, '.') & lm) << (4 * k);
-            colons |= flags_nibble(byte_eq_flags(w, ':') & lm) << (4 * k);
+            dots |= (M)flags_nibble(byte_eq_flags(w, '.') & lm) << (4 * k);
+            colons |= (M)flags_nibble(byte_eq_flags(w, ':') & lm) << (4 * k);
             badm |= (byte_eq_flags(w, '/') | byte_eq_flags(w, 0)) & lm;
         }
         if (badm || (dots & (dots >> 1))) return -1;
-        host_len = colons ? __builtin_ctz(colons) : (int)n;
-        if (dots && 31 - __builtin_clz(dots) == host_len - 1) host_len--;
+        host_len = colons ? (NW == 8 ? __builtin_ctz((uint32_t)colons) : __builtin_ctzll((uint64_t)colons)) : (int)n;
+        if (dots && (NW == 8 ? 31 - __builtin_clz((uint32_t)dots) : 63 - __builtin_clzll((uint64_t)dots)) == host_len - 1)
+            host_len--;
         if (host_len <= 0) return -1;
     }
     uint32_t hs = name_hash_init((uint32_t)host_len);
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
+    for (int k = 0; k < NW; k++) {
         const int rem = host_len - 4 * k;
         if (rem <= 0) break;
         const uint32_t m = rem >= 4 ? 0xFFFFFFFFu : (1u << (8 * rem)) - 1;
@@ -799,14 +825,17 @@ __device__ __forceinline__ int host_fast(const uint32_t (&hw)[8], uint32_t n, co
         const DName e = h.names[i];
         if (e.hash == 0) break;
         if (e.hash == hs && e.port_idx == pi && e.name_len == (uint32_t)host_len) {
-            uint32_t tw[8];
-            load_span32(h.name_bytes, e.name_off, ~0ull, tw);   // the name strings end with 64 B of slack
             uint32_t diff = 0;
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const int rem = host_len - 4 * k;
-                const uint32_t m = rem >= 4 ? 0xFFFFFFFFu : rem > 0 ? (1u << (8 * rem)) - 1 : 0u;
-                diff |= (lower4(hw[k]) ^ tw[k]) & m;
+            for (int hlf = 0; hlf < NW / 8; hlf++) {
+                uint32_t tw[8];
+                load_span32(h.name_bytes, e.name_off + 32 * hlf, ~0ull, tw);   // the name strings end with 64 B of slack
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int rem = host_len - 4 * (k + 8 * hlf);
+                    const uint32_t m = rem >= 4 ? 0xFFFFFFFFu : rem > 0 ? (1u << (8 * rem)) - 1 : 0u;
+                    diff |= (lower4(hw[k + 8 * hlf]) ^ tw[k]) & m;
+                }
             }
             if (diff == 0) { server = e.server; break; }
         }
@@ -858,40 +887,71 @@ __device__ __noinline__ int server_if_generic(const uint8_t *A, const gm_req *rp
 // engine cannot know)
 __device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t rules_idx,
                                           uint32_t rip) {
+#ifdef GM_EXP_NO_RULES   // measurement build: no conditions (timing only)
+    return 0xFF;
+#endif
     const Rec r = load_rec(rp);
     const DRules R = t.rules[rules_idx];
-    Ctx c;
-    ctx_init(c, A, r, &t, rip);
-    Val v;
-    // header / cookie / argument values are looked up once per request, not once per condition
-    // that reads them (every match of a rules route repeats the route's conditions); variables
-    // are cheap and some share c.scratch, so they are not kept
+    const uint64_t o_args = r.base + r.uri_len, o_hdrs = o_args + r.args_len;
+    // header (one line) / cookie / argument values are single arena spans, looked up once per
+    // request (every match of a rules route repeats the route's conditions) and kept in registers;
+    // the other variables go through a Val in the lane's private memory, as before (round 6:
+    // C2's conditions read headers, cookies and arguments only)
     constexpr int MEMO = 4;
-    Val memo[MEMO];
-    uint32_t msrc[MEMO];
-    int nmemo = 0;
+    uint32_t msrc[MEMO], mlen[MEMO];
+    uint64_t moff[MEMO];
+#pragma unroll
+    for (int q = 0; q < MEMO; q++) { msrc[q] = GM_NONE; mlen[q] = 0; moff[q] = 0; }
+    Ctx c;
+    bool have_ctx = false;
+    Val v;
     uint32_t bits = 0;
     for (uint32_t ch = 0; ch < R.n_chains; ch++) {
         int32_t nd = (int32_t)t.chain_heads[R.first_chain + ch];
         int guard = 0;
         while (nd >= 0 && guard++ < 64) {
             const DCond cd = t.conds[nd];
-            const Val *vp = nullptr;
-            for (int q = 0; q < nmemo; q++) if (msrc[q] == cd.src) vp = &memo[q];
-            if (!vp) {
-                if (nmemo < MEMO && t.srcs[cd.src].kind != SRC_VAR) {
-                    get_var(c, t, cd.src, memo[nmemo]);
-                    msrc[nmemo] = cd.src;
-                    vp = &memo[nmemo++];
-                } else {
-                    get_var(c, t, cd.src, v);
-                    vp = &v;
-                }
-            }
-            if (vp->unknown) return -1;
+            const DSrc sr = t.srcs[cd.src];
             bool m;
-            if (cd.is_regex) m = vp->total > 0 && dfa_run_val(t, cd.dfa, *vp);
-            else m = val_eq(*vp, t.bytes + cd.key_off, cd.key_len, true);
+            if (sr.kind != SRC_VAR && !(sr.kind == SRC_HTTP && sr.join)) {
+                uint64_t off = 0;
+                uint32_t len = 0;
+                bool hit = false;
+#pragma unroll
+                for (int q = 0; q < MEMO; q++) if (msrc[q] == cd.src) { off = moff[q]; len = mlen[q]; hit = true; }
+                if (!hit) {
+                    const uint8_t *nm = t.bytes + sr.name_off;
+                    bool f;
+#ifdef GM_EXP_RULES_NOSPAN   // measurement build: every header / cookie / argument empty (timing only)
+                    if (true) f = false; else
+#endif
+                    if (sr.kind == SRC_HTTP) f = span_http(A, o_hdrs, r.hdr_len, nm, sr.name_len, off, len);
+                    else if (sr.kind == SRC_COOKIE) f = span_cookie(A, o_hdrs, r.hdr_len, nm, sr.name_len, off, len);
+                    else f = span_arg(A, o_args, r.args_len, nm, sr.name_len, off, len);
+                    if (!f) { off = 0; len = 0; }
+                    bool put = false;
+#pragma unroll
+                    for (int q = 0; q < MEMO; q++)
+                        if (!put && msrc[q] == GM_NONE) { msrc[q] = cd.src; moff[q] = off; mlen[q] = len; put = true; }
+                }
+                if (cd.is_regex) {
+                    m = len > 0 && dfa_run_bytes(t, cd.dfa, A + off, len);
+                } else {
+                    m = len == cd.key_len;
+                    const uint8_t *key = t.bytes + cd.key_off;
+                    for (uint32_t k = 0; m && k < len; k++) m = lc(A[off + k]) == key[k];
+                }
+            } else {
+#ifdef GM_EXP_RULES_NOVAR   // measurement build: every other variable empty (timing only)
+                v.clear();
+#else
+                if (!have_ctx) { ctx_init(c, A, r, &t, rip); have_ctx = true; }
+                get_var(c, t, cd.src, v);
+#endif
+                if (v.unknown) return -1;
+                if (cd.is_regex) m = v.total > 0 && dfa_run_val(t, cd.dfa, v);
+                else m = val_eq(v, t.bytes + cd.key_off, cd.key_len, true);
+            }
             nd = m ? cd.next_true : cd.next_false;
         }
         if (nd == NEXT_1) bits |= 1u << ch;
@@ -918,6 +978,9 @@ __device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, co
 // split_clients: murmur2 of the source -> part index (0xFF none, 0xFFFFFFFF unsupported value)
 __device__ __noinline__ uint32_t split_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t split_idx,
                                                uint32_t rip) {
+#ifdef GM_EXP_NO_SPLIT   // measurement build: no split key (timing only)
+    return 0;
+#endif
     const Rec r = load_rec(rp);
     const DSplit Sp = t.splits[split_idx];
     Ctx c;
@@ -981,7 +1044,9 @@ __device__ __forceinline__ void too_large(RouteOut &o) {
 // literal host takes the arena-byte path; a request that needs a generic server `if`, the
 // regex-location prefilter or a rules / split route stops with o.slow set, and k_route's SLOW
 // pass (a second launch over the list of such requests) routes it again with the calls.
-template <bool FAST = false>
+// LONGHOST: hosts of 33..64 bytes through the 16-word SWAR path (the route kernels beside the
+// WAF scan, held to GM_ROUTE_WPE waves, leave it out: it spilled them)
+template <bool FAST = false, bool LONGHOST = true>
 __device__ __forceinline__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const RoutePre &pre,
                           const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb, int32_t rk_in = RK_INLINE,
                           bool *pend = nullptr) {
@@ -1010,6 +1075,17 @@ __device__ __forceinline__ void route_one(const uint8_t *A, uint64_t alen, const
         if (r.host_len <= 32) {
             hl = host_fast<FAST>(pre.hw, r.host_len, t, h, pi, s);
             if (FAST && hl == -2) {   // an IPv6 literal: the arena-byte path
+                hl = validate_host(A + f_host, r.host_len);
+                if (hl >= 0) s = name_probe(h.names, t.names_mask, h.name_bytes, A + f_host, 0, (uint32_t)hl, pi);
+            }
+        } else if (LONGHOST && r.host_len <= 64) {   // 33..64 bytes: the same SWAR over 16 words
+            uint32_t hw16[16], lo[8], hi[8];
+            load_span_n(A, f_host, alen, 32, lo);
+            load_span_n(A, f_host + 32, alen, r.host_len - 32, hi);
+#pragma unroll
+            for (int k = 0; k < 8; k++) { hw16[k] = lo[k]; hw16[8 + k] = hi[k]; }
+            hl = host_fast<true, 16>(hw16, r.host_len, t, h, pi, s);
+            if (hl == -2) {   // an IPv6 literal: the arena-byte path
                 hl = validate_host(A + f_host, r.host_len);
                 if (hl >= 0) s = name_probe(h.names, t.names_mask, h.name_bytes, A + f_host, 0, (uint32_t)hl, pi);
             }
@@ -1359,7 +1435,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
             if (SLOW) i = q.list[x].x;
             r = load_rec(reqs + i);
             route_prefetch(A, arena_len, r, pre);
-            route_one<FASTK>(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
+            route_one<FASTK, (WPE < GM_ROUTE_WPE_SHIPPED)>(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
                              RK && q.list ? RK_DEFER : RK_INLINE, &pend);
         }
         const bool slow = FASTK && o.slow;
@@ -1473,6 +1549,7 @@ struct Generation {
             if (p) (void)hipFree(p);
     }
 };
+
 
 // batches a stream may hold before gm_sync (the next gm_match_batch completes them first)
 constexpr uint32_t PENDING_MAX = 64;
@@ -3677,6 +3754,7 @@ extern "C" int gm_upstream_uris(gm_ctx *c, const gm_batch *in, const gm_verdict 
 // tuning macros count when they differ from the shipped values.
 static constexpr uint32_t kBuildFlags =
 #if defined(GM_EXP_COUNT) || defined(GM_EXP_RLOC_NOREC) || defined(GM_EXP_RLOC_NOSB) || defined(GM_EXP_ALW_NOEMIT) || \
+    defined(GM_EXP_NO_RULES) || defined(GM_EXP_NO_SPLIT) || defined(GM_EXP_RULES_NOSPAN) || defined(GM_EXP_RULES_NOVAR) || \
     defined(GM_EXP_ALW_COUNT)
     GM_BUILD_EXPERIMENT |
 #endif

@@ -1,4 +1,5 @@
-cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests_${TAG}.log 2>&1; rc=$?; tail -3 gpurun_out/gpu_tests_${TAG}.log; [ $rc -eq 0 ] || exit $rc
-KT_ONLY=1 bash scripts/pmc_alw.sh || exit $?
-timeout -k 10 400 python -u bench.py --no-cpu > gpurun_out/bench_${TAG}.log 2>&1 || exit $?
-grep -h '"metric"' gpurun_out/bench_${TAG}.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('C4', d['ms_per_step'], d['stage_ms'], 'stress', d['stress']['ms_per_step'], d['stress']['stage_ms'])"
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+R=$GRAFT_REPO_ROOT
+cd /tmp && TMPDIR=/tmp timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/cfg_${TAG}_c2 -o run --output-format csv \
+   -- python3 $R/scripts/bench_config.py --config c2 --no-cpu --steps 5 --warmup 1 > $R/gpurun_out/cfg_${TAG}_c2.log 2>&1 || exit $?
+cd $R && python3 scripts/kstats.py $(find gpurun_out/cfg_${TAG}_c2 -name "*kernel_stats.csv" | head -1) | head -4

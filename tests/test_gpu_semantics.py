@@ -170,6 +170,79 @@ def test_rules_route_many_chains(eng):
     assert len(set(v["match_idx"].tolist())) >= 6
 
 
+def test_rules_header_cookie_arg_spans(eng):
+    """The SLOW pass's span pre-pass (k_rule_spans: a wave per request over its header block staged
+    in LDS) against the oracle's walks: a header condition (name case and '-' / '_' variants,
+    repeated lines -- the first wins --, spaces around values, CR-less and colon-less lines), a
+    cookie condition over 0-3 Cookie lines (look-alike names, ',' and ';' separators, spaces around
+    '='), an argument condition; plus requests past the pre-pass's limits (> 255 header lines,
+    > 4 KiB of headers, > 16 Cookie lines) that rules_generic walks itself."""
+    rng = np.random.Generator(np.random.PCG64(41))
+    ups = [{"name": f"u{k}", "service": f"svc{k}", "port": 80} for k in range(5)]
+    vs = {"metadata": {"name": "sp", "namespace": "default"},
+          "spec": {"host": "sp.example.com", "upstreams": ups,
+                   "routes": [{"path": "/", "rules": {
+                       "conditions": [{"header": "X-Ab-C"}, {"cookie": "sess"}, {"argument": "q"}],
+                       "matches": [{"values": ["v1", "v1", "v1"], "upstream": "u1"},
+                                   {"values": ["~^v[0-9]$", "v2", "~2"], "upstream": "u2"},
+                                   {"values": ["", "~^v", "v3"], "upstream": "u3"},
+                                   {"values": ["v3", "", ""], "upstream": "u4"}],
+                       "defaultUpstream": "u0"}}]}}
+    b = SC._vs_blob(vs)
+    vals = ["v1", "v2", "v3", "V1", "x", ""]
+    names = ["X-Ab-C", "x-ab-c", "X_AB_C", "X-Ab-Cd", "X-Ab"]
+    ck_tok = ["sess=v1", "sess=v2", " sess = v3", "sess2=v1", "SESS=v2", "xsess=v1", "sess", "a=b", "sess=v3;x"]
+    args = ["q=v1", "q=v2", "Q=v3", "aq=v1", "q=", "q", "x=1&q=v2", "q=v3&q=v1", "&q=v1"]
+    items = []
+    for i in range(6000):
+        hdrs = [("Accept", "*/*"), ("User-Agent", "t" * int(rng.integers(0, 60)))]
+        for _ in range(int(rng.integers(0, 3))):
+            v = vals[int(rng.integers(0, len(vals)))]
+            v = " " * int(rng.integers(0, 3)) + v + " " * int(rng.integers(0, 3))
+            hdrs.insert(int(rng.integers(0, len(hdrs) + 1)), (names[int(rng.integers(0, len(names)))], v))
+        for _ in range(int(rng.integers(0, 4))):
+            toks = [ck_tok[int(t)] for t in rng.integers(0, len(ck_tok), int(rng.integers(1, 5)))]
+            seps = ["; ", ";", ", ", " ; "]
+            hdrs.append(("Cookie", seps[int(rng.integers(0, 4))].join(toks)))
+        u = rng.random()
+        if u < 0.05:
+            hdrs.append(("X-Raw", "a\nNoColonLine"))          # a line without ':' (bare LF)
+        elif u < 0.08:
+            hdrs += [("X-H", "1")] * 300                      # > 255 lines: the walk
+        elif u < 0.10:
+            hdrs.append(("X-Big", "b" * 5000))                 # > 4 KiB: the walk
+        elif u < 0.12:
+            hdrs += [("Cookie", "k=v")] * 20                   # > 16 Cookie lines: the walk
+        a = "&".join(args[int(t)] for t in rng.integers(0, len(args), int(rng.integers(0, 3))))
+        items.append({"host": "sp.example.com", "uri": "/", "args": a, "headers": hdrs})
+    v = _both(eng, b, items)
+    assert eng.stats()["n_rejected_other"] == 0, eng.rejects()
+    got = set(v["match_idx"].tolist())
+    assert {0, 1, 2, 3, 0xFF} <= got, got
+
+
+def test_long_host_names(eng):
+    """Hosts of 33..64 bytes take the route's 16-word SWAR path (round 6), longer ones the arena
+    bytes: case, a port, a trailing dot, a ".." and a '/' in them, IPv6 literals, lengths 32 / 33 /
+    64 / 65 around the boundaries, against the oracle."""
+    long_host = "a" * 20 + ".virtual-server.example.com"        # 47 bytes
+    edge64 = "b" * 48 + ".example.com.xy"                          # 63 bytes
+    ups = [{"name": "u0", "service": "svc0", "port": 80}]
+    vss = []
+    for k, h in enumerate([long_host, edge64, "c" * 21 + ".example.com"]):   # (the last: 33 bytes)
+        vss.append({"metadata": {"name": f"lh{k}", "namespace": "default"},
+                    "spec": {"host": h, "upstreams": ups, "routes": [{"path": "/", "upstream": "u0"}]}})
+    p = confgen.default_config_params()
+    b = blob.make_blob(confgen.render_main(p), confgen.virtual_server_files(vss, base=p, pem_name=""))
+    hosts = [long_host, long_host.upper(), long_host + ":8080", long_host + ".", long_host + "..",
+             edge64, edge64 + "z", edge64 + "zz", edge64.upper() + ":1", "c" * 21 + ".example.com",
+             "c" * 20 + ".example.com", "d" * 40 + "/x.example.com", "e" * 30 + "..example.com",
+             "[2001:db8::1]:80" + "f" * 20, "[" + "1" * 40 + "]", "g" * 64, "h" * 65, "x" * 33, ""]
+    items = [{"host": h, "uri": "/", "https": bool(i % 2)} for i in range(4) for h in hosts]
+    v = _both(eng, b, items)
+    assert (v["server_id"] != v["server_id"][-1]).any()
+
+
 def _peer_pair(e, b, items, gen=4):
     import torch
     dev = torch.device("cuda", 0)
