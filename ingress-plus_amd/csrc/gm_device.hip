@@ -167,25 +167,38 @@ __device__ uint64_t find_byte2(const uint8_t *A, uint64_t p, uint64_t e, uint32_
 
 // iterate "Name: value\r\n" lines (ngx_http_parse_header_line); returns false at end
 struct HdrIt { uint64_t pos, end; };
-__device__ bool hdr_next(const uint8_t *A, HdrIt &it, uint64_t &ns, uint32_t &nl, uint64_t &vs, uint32_t &vl) {
+// the next line's name only: [ns, ns + nl) up to its first ':' (c), the line ending at e (its LF,
+// or the block's end); the value is read only for a line whose name matters (hdr_value) -- its CR
+// check and space trims were three dependent byte loads per line of every walk (round 6)
+__device__ bool hdr_next_name(const uint8_t *A, HdrIt &it, uint64_t &ns, uint32_t &nl, uint64_t &c, uint64_t &e) {
     while (it.pos < it.end) {
-        uint64_t st = it.pos;
-        const uint64_t e = find_byte(A, st, it.end, '\n');
+        const uint64_t st = it.pos;
+        e = find_byte(A, st, it.end, '\n');
         it.pos = e + 1;
-        uint64_t le = e;
-        if (le > st && A[le - 1] == '\r') le--;
-        const uint64_t c = find_byte(A, st, le, ':');
-        if (c >= le) continue;
+        // (a ':' before the LF is before the line's CR too: a CR-less search finds the same one)
+        c = find_byte(A, st, e, ':');
+        if (c >= e) continue;
         ns = st; nl = (uint32_t)(c - st);
-        // the value without leading / trailing spaces (nginx skips ' ' only: a tab is value)
-        uint64_t v0 = c + 1;
-        while (v0 < le && A[v0] == ' ') v0++;
-        uint64_t v1 = le;
-        while (v1 > v0 && A[v1 - 1] == ' ') v1--;
-        vs = v0; vl = (uint32_t)(v1 - v0);
         return true;
     }
     return false;
+}
+// the value of a line hdr_next_name returned: without the CR before its LF, without leading /
+// trailing spaces (nginx skips ' ' only: a tab is value)
+__device__ __forceinline__ void hdr_value(const uint8_t *A, uint64_t ns, uint64_t c, uint64_t e, uint64_t &vs, uint32_t &vl) {
+    uint64_t le = e;
+    if (le > ns && A[le - 1] == '\r') le--;
+    uint64_t v0 = c + 1;
+    while (v0 < le && A[v0] == ' ') v0++;
+    uint64_t v1 = le;
+    while (v1 > v0 && A[v1 - 1] == ' ') v1--;
+    vs = v0; vl = (uint32_t)(v1 - v0);
+}
+__device__ bool hdr_next(const uint8_t *A, HdrIt &it, uint64_t &ns, uint32_t &nl, uint64_t &vs, uint32_t &vl) {
+    uint64_t c, e;
+    if (!hdr_next_name(A, it, ns, nl, c, e)) return false;
+    hdr_value(A, ns, c, e, vs, vl);
+    return true;
 }
 
 // header name vs a lowercase name, case-insensitively (the headers_in hash: lowcase_key)
@@ -213,18 +226,19 @@ __device__ bool hdr_name_is(const uint8_t *A, uint64_t ns, uint32_t nl, const ui
 __device__ bool span_http(const uint8_t *A, uint64_t hdrs, uint32_t hlen, const uint8_t *nm, uint32_t nml,
                           uint64_t &vo, uint32_t &vl) {
     HdrIt it{hdrs, hdrs + hlen};
-    uint64_t ns, vs; uint32_t nl, l;
-    while (hdr_next(A, it, ns, nl, vs, l))
-        if (hdr_name_is(A, ns, nl, nm, nml)) { vo = vs; vl = l; return true; }
+    uint64_t ns, c, e; uint32_t nl;
+    while (hdr_next_name(A, it, ns, nl, c, e))
+        if (hdr_name_is(A, ns, nl, nm, nml)) { hdr_value(A, ns, c, e, vo, vl); return true; }
     return false;
 }
 __device__ bool span_cookie(const uint8_t *A, uint64_t hdrs, uint32_t hlen, const uint8_t *nm, uint32_t nml,
                             uint64_t &vo, uint32_t &vl) {
     HdrIt it{hdrs, hdrs + hlen};
-    uint64_t ns, vs; uint32_t nl, l;
+    uint64_t ns, vs, c, e; uint32_t nl, l;
     const uint8_t cookie[7] = "cookie";
-    while (hdr_next(A, it, ns, nl, vs, l)) {
+    while (hdr_next_name(A, it, ns, nl, c, e)) {
         if (!hdr_name_is(A, ns, nl, cookie, 6)) continue;
+        hdr_value(A, ns, c, e, vs, l);
         if (nml > l) continue;
         uint64_t start = vs, end = vs + l;
         while (start < end) {
