@@ -165,6 +165,30 @@ __device__ uint64_t find_byte2(const uint8_t *A, uint64_t p, uint64_t e, uint32_
     return find_flagged(A, p, e, [p1, p2](uint32_t w) { return zero_bytes(w ^ p1) | zero_bytes(w ^ p2); });
 }
 
+// the first ':' or LF in A[p, e) (e if neither); colon: it is the ':'
+__device__ uint64_t find_colon_lf(const uint8_t *A, uint64_t p, uint64_t e, bool &colon) {
+    colon = false;
+    if (p >= e) return e;
+    for (uint64_t b = p & ~15ull; b < e; b += 16) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(A + b);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t zc = zero_bytes(w[k] ^ 0x3A3A3A3Au), zl = zero_bytes(w[k] ^ 0x0A0A0A0Au);
+            uint32_t z = zc | zl;
+            const uint64_t wb = b + 4 * k;   // bytes [wb, wb + 4)
+            if (p > wb) z = p - wb >= 4 ? 0u : z & (~0u << (8 * (uint32_t)(p - wb)));
+            if (wb + 4 > e) z = e <= wb ? 0u : z & ((1u << (8 * (uint32_t)(e - wb))) - 1u);
+            if (z) {
+                const uint32_t bit = (uint32_t)__builtin_ctz(z);
+                colon = ((zc >> bit) & 1u) != 0;
+                return wb + (bit >> 3);
+            }
+        }
+    }
+    return e;
+}
+
 // iterate "Name: value\r\n" lines (ngx_http_parse_header_line); returns false at end
 struct HdrIt { uint64_t pos, end; };
 // the next line's name only: [ns, ns + nl) up to its first ':' (c), the line ending at e (its LF,
@@ -173,11 +197,14 @@ struct HdrIt { uint64_t pos, end; };
 __device__ bool hdr_next_name(const uint8_t *A, HdrIt &it, uint64_t &ns, uint32_t &nl, uint64_t &c, uint64_t &e) {
     while (it.pos < it.end) {
         const uint64_t st = it.pos;
-        e = find_byte(A, st, it.end, '\n');
+        // the first ':' or LF: a ':' first names the line (its LF is searched from there on), a LF
+        // first ends a line with no name (a ':' before the LF is before the line's CR too)
+        bool colon;
+        const uint64_t x = find_colon_lf(A, st, it.end, colon);
+        if (!colon) { e = x; it.pos = e + 1; continue; }
+        c = x;
+        e = find_byte(A, c + 1, it.end, '\n');
         it.pos = e + 1;
-        // (a ':' before the LF is before the line's CR too: a CR-less search finds the same one)
-        c = find_byte(A, st, e, ':');
-        if (c >= e) continue;
         ns = st; nl = (uint32_t)(c - st);
         return true;
     }
