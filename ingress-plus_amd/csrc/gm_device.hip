@@ -258,6 +258,32 @@ __device__ bool span_http(const uint8_t *A, uint64_t hdrs, uint32_t hlen, const 
         if (hdr_name_is(A, ns, nl, nm, nml)) { hdr_value(A, ns, c, e, vo, vl); return true; }
     return false;
 }
+// a cookie in one Cookie line's value [vs, vs + l): ngx_http_parse_multi_header_lines' loop
+__device__ bool cookie_in_line(const uint8_t *A, uint64_t vs, uint32_t l, const uint8_t *nm, uint32_t nml,
+                               uint64_t &vo, uint32_t &vl) {
+    if (nml > l) return false;
+    uint64_t start = vs, end = vs + l;
+    while (start < end) {
+        bool ok = end - start >= nml;
+        for (uint32_t k = 0; ok && k < nml; k++) if (lc(A[start + k]) != nm[k]) ok = false;
+        if (ok) {
+            start += nml;
+            while (start < end && A[start] == ' ') start++;
+            // (nginx: `*start++ != '='` -- the byte tested is consumed even when it is not '=',
+            // so a ';' or ',' there does not end the skip below)
+            if (start < end && A[start++] == '=') {
+                while (start < end && A[start] == ' ') start++;
+                const uint64_t last = find_byte(A, start, end, ';');
+                vo = start; vl = (uint32_t)(last - start);
+                return true;
+            }
+        }
+        start = find_byte2(A, start, end, ';', ',');
+        if (start < end) start++;
+        while (start < end && A[start] == ' ') start++;
+    }
+    return false;
+}
 __device__ bool span_cookie(const uint8_t *A, uint64_t hdrs, uint32_t hlen, const uint8_t *nm, uint32_t nml,
                             uint64_t &vo, uint32_t &vl) {
     HdrIt it{hdrs, hdrs + hlen};
@@ -266,27 +292,7 @@ __device__ bool span_cookie(const uint8_t *A, uint64_t hdrs, uint32_t hlen, cons
     while (hdr_next_name(A, it, ns, nl, c, e)) {
         if (!hdr_name_is(A, ns, nl, cookie, 6)) continue;
         hdr_value(A, ns, c, e, vs, l);
-        if (nml > l) continue;
-        uint64_t start = vs, end = vs + l;
-        while (start < end) {
-            bool ok = end - start >= nml;
-            for (uint32_t k = 0; ok && k < nml; k++) if (lc(A[start + k]) != nm[k]) ok = false;
-            if (ok) {
-                start += nml;
-                while (start < end && A[start] == ' ') start++;
-                // (nginx: `*start++ != '='` -- the byte tested is consumed even when it is not '=',
-                // so a ';' or ',' there does not end the skip below)
-                if (start < end && A[start++] == '=') {
-                    while (start < end && A[start] == ' ') start++;
-                    const uint64_t last = find_byte(A, start, end, ';');
-                    vo = start; vl = (uint32_t)(last - start);
-                    return true;
-                }
-            }
-            start = find_byte2(A, start, end, ';', ',');
-            if (start < end) start++;
-            while (start < end && A[start] == ' ') start++;
-        }
+        if (cookie_in_line(A, vs, l, nm, nml, vo, vl)) return true;
     }
     return false;
 }
@@ -947,6 +953,7 @@ __device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, co
     bool have_ctx = false;
     Val v;
     uint32_t bits = 0;
+    bool walked = false;   // the route's header / cookie sources were resolved by one walk
     for (uint32_t ch = 0; ch < R.n_chains; ch++) {
         int32_t nd = (int32_t)t.chain_heads[R.first_chain + ch];
         int guard = 0;
@@ -960,6 +967,80 @@ __device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, co
                 bool hit = false;
 #pragma unroll
                 for (int q = 0; q < MEMO; q++) if (msrc[q] == cd.src) { off = moff[q]; len = mlen[q]; hit = true; }
+                if (!hit && !walked && (sr.kind == SRC_HTTP || sr.kind == SRC_COOKIE)) {
+                    // one header walk for every header (one line) and cookie source on the
+                    // route's chains (their true paths; up to the free memo slots): C2's
+                    // /backends route read X-Version and the Cookie lines in two walks
+                    walked = true;
+                    uint32_t ps[MEMO], pk[MEMO], pl[MEMO];
+                    const uint8_t *pn[MEMO];
+                    bool pf[MEMO];
+                    uint64_t po[MEMO];
+                    uint32_t pv[MEMO];
+                    uint32_t np = 0;
+#pragma unroll
+                    for (int q = 0; q < MEMO; q++) { ps[q] = GM_NONE; pk[q] = 0; pl[q] = 0; pn[q] = nullptr; pf[q] = false; po[q] = 0; pv[q] = 0; }
+                    uint32_t nfree = 0;
+#pragma unroll
+                    for (int q = 0; q < MEMO; q++) nfree += msrc[q] == GM_NONE ? 1u : 0u;
+                    for (uint32_t c2 = 0; c2 < R.n_chains && np < nfree; c2++) {
+                        int32_t n2 = (int32_t)t.chain_heads[R.first_chain + c2];
+                        for (int g2 = 0; n2 >= 0 && g2 < 64 && np < nfree; g2++) {
+                            const DCond d2 = t.conds[n2];
+                            const DSrc s2 = t.srcs[d2.src];
+                            if ((s2.kind == SRC_HTTP && !s2.join) || s2.kind == SRC_COOKIE) {
+                                bool dup = false;
+#pragma unroll
+                                for (int q = 0; q < MEMO; q++) dup |= msrc[q] == d2.src || ps[q] == d2.src;
+                                if (!dup) {
+                                    bool put = false;
+#pragma unroll
+                                    for (int q = 0; q < MEMO; q++)
+                                        if (!put && q == (int)np) {
+                                            ps[q] = d2.src; pk[q] = s2.kind; pl[q] = s2.name_len; pn[q] = t.bytes + s2.name_off;
+                                            put = true;
+                                        }
+                                    np++;
+                                }
+                            }
+                            n2 = d2.next_true;
+                        }
+                    }
+                    uint32_t left = np;
+                    HdrIt it{o_hdrs, o_hdrs + r.hdr_len};
+                    uint64_t ns, cc, ee;
+                    uint32_t nl;
+                    const uint8_t cookie[7] = "cookie";
+                    while (left && hdr_next_name(A, it, ns, nl, cc, ee)) {
+                        const bool is_ck = hdr_name_is(A, ns, nl, cookie, 6);
+                        uint64_t lvs = 0;
+                        uint32_t lvl = 0;
+                        if (is_ck) hdr_value(A, ns, cc, ee, lvs, lvl);
+#pragma unroll
+                        for (int q = 0; q < MEMO; q++) {
+                            if (pf[q] || ps[q] == GM_NONE) continue;
+                            if (pk[q] == SRC_HTTP) {
+                                if (hdr_name_is(A, ns, nl, pn[q], pl[q])) {
+                                    hdr_value(A, ns, cc, ee, po[q], pv[q]); pf[q] = true; left--;
+                                }
+                            } else if (is_ck && cookie_in_line(A, lvs, lvl, pn[q], pl[q], po[q], pv[q])) {
+                                pf[q] = true; left--;
+                            }
+                        }
+                    }
+                    // into the memo (not found: the empty value)
+#pragma unroll
+                    for (int q = 0; q < MEMO; q++) {
+                        if (ps[q] == GM_NONE) continue;
+                        bool put = false;
+#pragma unroll
+                        for (int q2 = 0; q2 < MEMO; q2++)
+                            if (!put && msrc[q2] == GM_NONE) {
+                                msrc[q2] = ps[q]; moff[q2] = pf[q] ? po[q] : 0; mlen[q2] = pf[q] ? pv[q] : 0; put = true;
+                            }
+                        if (ps[q] == cd.src) { off = pf[q] ? po[q] : 0; len = pf[q] ? pv[q] : 0; hit = true; }
+                    }
+                }
                 if (!hit) {
                     const uint8_t *nm = t.bytes + sr.name_off;
                     bool f;
