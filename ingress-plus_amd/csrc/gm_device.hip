@@ -2563,6 +2563,9 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         return GM_OK;
     };
     if (mark(0)) return GM_E_HIP;
+#ifndef GM_SLOW_WPE
+#define GM_SLOW_WPE 3   // the SLOW route pass's waves per SIMD target (its header walks are latency-bound)
+#endif
     const uint32_t route_blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
                                                                            (uint32_t)c->cu_count * GM_EXP_GRIDMUL));
     unsigned long long *ctr = S->d_bctr;
@@ -2656,7 +2659,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
         else {
             GM_ROUTE_LAUNCH(3, false, false, route_blocks, route_lds(t, false), s, reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), qs);
             HIPCHK(c, hipGetLastError());
-            k_route<3, false, false, true><<<route_blocks, ROUTE_BLOCK, route_lds(t, false), s>>>(
+            k_route<GM_SLOW_WPE, false, false, true><<<route_blocks, ROUTE_BLOCK, route_lds(t, false), s>>>(
                 reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), qs);
         }
         HIPCHK(c, hipGetLastError());
@@ -3883,7 +3886,8 @@ static constexpr uint32_t kBuildFlags =
 #if GM_SCAN_BLOCK != 1024 || GM_SCAN_CPOL != 2 || GM_SCAN_DEPTH != 6 || GM_SCAN_STG != 32 || \
     GM_ROUTE_BPC != 1 || GM_ROUTE_PRIO != 0 || GM_ROUTE_WPE != GM_ROUTE_WPE_SHIPPED || GM_EXP_GRIDMUL != 8 || \
     GM_EXP_WPE != 3 || GM_RLOC_CTX != 1 || GM_RLOC_PREF != 0 || GM_ALW_SLICE_GROUPS != 8 || GM_WIRE_WPE != 6 || \
-    GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1 || GM_EXACT_BPC != 6 || !defined(GM_DFA_INL_SHIPPED)
+    GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1 || GM_EXACT_BPC != 6 || !defined(GM_DFA_INL_SHIPPED) || \
+    GM_SLOW_WPE != 3
     GM_BUILD_TUNING |
 #endif
     0u;

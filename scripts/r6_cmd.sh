@@ -1,2 +1,2 @@
-cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && timeout -k 10 600 python -u -m pytest tests/test_gpu_semantics.py tests/test_gpu_parity.py tests/test_gpu_reference.py -x -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests_${TAG}.log 2>&1; rc=$?; tail -3 gpurun_out/gpu_tests_${TAG}.log; [ $rc -eq 0 ] || exit $rc
-CONFIGS="c2" TAG=$TAG bash scripts/ab_configs.sh main main
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+CONFIGS="c2" TAG=$TAG bash scripts/ab_configs.sh main slow5 slow6 main slow5 slow6
