@@ -135,14 +135,21 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
 // the first position of a byte flagged by `hit` (per-word flags) in A[p, e), or e: whole aligned
 // 16-byte blocks (the first and the last masked to [p, e): an aligned block never leaves the
 // allocation), exact SWAR flags per word
-template <class F>
+// NB = 2: 32 bytes a step, the second block's load out with the first -- for a header walk's LF
+// search over a long value, otherwise a chain of dependent 16-byte loads (round 6); NB = 1 where
+// the registers matter more (the FAST route pass)
+template <int NB = 1, class F>
 __device__ __forceinline__ uint64_t find_flagged(const uint8_t *A, uint64_t p, uint64_t e, F hit) {
     if (p >= e) return e;
-    for (uint64_t b = p & ~15ull; b < e; b += 16) {
-        const uint4 q = *reinterpret_cast<const uint4 *>(A + b);
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    for (uint64_t b = p & ~15ull; b < e; b += 16 * NB) {
+        uint32_t w[4 * NB];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int j = 0; j < NB; j++) {
+            const uint4 q = j == 0 || b + 16 * j < e ? *reinterpret_cast<const uint4 *>(A + b + 16 * j) : make_uint4(0, 0, 0, 0);
+            w[4 * j] = q.x; w[4 * j + 1] = q.y; w[4 * j + 2] = q.z; w[4 * j + 3] = q.w;
+        }
+#pragma unroll
+        for (int k = 0; k < 4 * NB; k++) {
             uint32_t z = hit(w[k]);
             const uint64_t wb = b + 4 * k;   // bytes [wb, wb + 4)
             if (p > wb) z = p - wb >= 4 ? 0u : z & (~0u << (8 * (uint32_t)(p - wb)));
@@ -154,9 +161,10 @@ __device__ __forceinline__ uint64_t find_flagged(const uint8_t *A, uint64_t p, u
 }
 
 // first position of byte `ch` in A[p, e), or e
+template <int NB = 1>
 __device__ uint64_t find_byte(const uint8_t *A, uint64_t p, uint64_t e, uint32_t ch) {
     const uint32_t pat = ch * 0x01010101u;
-    return find_flagged(A, p, e, [pat](uint32_t w) { return zero_bytes(w ^ pat); });
+    return find_flagged<NB>(A, p, e, [pat](uint32_t w) { return zero_bytes(w ^ pat); });
 }
 
 // first position of either byte in A[p, e), or e
@@ -166,14 +174,19 @@ __device__ uint64_t find_byte2(const uint8_t *A, uint64_t p, uint64_t e, uint32_
 }
 
 // the first ':' or LF in A[p, e) (e if neither); colon: it is the ':'
+template <int NB = 1>
 __device__ uint64_t find_colon_lf(const uint8_t *A, uint64_t p, uint64_t e, bool &colon) {
     colon = false;
     if (p >= e) return e;
-    for (uint64_t b = p & ~15ull; b < e; b += 16) {
-        const uint4 q = *reinterpret_cast<const uint4 *>(A + b);
-        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    for (uint64_t b = p & ~15ull; b < e; b += 16 * NB) {   // (NB blocks a step, as find_flagged)
+        uint32_t w[4 * NB];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int j = 0; j < NB; j++) {
+            const uint4 q = j == 0 || b + 16 * j < e ? *reinterpret_cast<const uint4 *>(A + b + 16 * j) : make_uint4(0, 0, 0, 0);
+            w[4 * j] = q.x; w[4 * j + 1] = q.y; w[4 * j + 2] = q.z; w[4 * j + 3] = q.w;
+        }
+#pragma unroll
+        for (int k = 0; k < 4 * NB; k++) {
             const uint32_t zc = zero_bytes(w[k] ^ 0x3A3A3A3Au), zl = zero_bytes(w[k] ^ 0x0A0A0A0Au);
             uint32_t z = zc | zl;
             const uint64_t wb = b + 4 * k;   // bytes [wb, wb + 4)
@@ -194,6 +207,7 @@ struct HdrIt { uint64_t pos, end; };
 // the next line's name only: [ns, ns + nl) up to its first ':' (c), the line ending at e (its LF,
 // or the block's end); the value is read only for a line whose name matters (hdr_value) -- its CR
 // check and space trims were three dependent byte loads per line of every walk (round 6)
+template <int NB = 1>
 __device__ bool hdr_next_name(const uint8_t *A, HdrIt &it, uint64_t &ns, uint32_t &nl, uint64_t &c, uint64_t &e) {
     while (it.pos < it.end) {
         const uint64_t st = it.pos;
@@ -203,13 +217,14 @@ __device__ bool hdr_next_name(const uint8_t *A, HdrIt &it, uint64_t &ns, uint32_
         const uint64_t x = find_colon_lf(A, st, it.end, colon);
         if (!colon) { e = x; it.pos = e + 1; continue; }
         c = x;
-        e = find_byte(A, c + 1, it.end, '\n');
+        e = find_byte<NB>(A, c + 1, it.end, '\n');
         it.pos = e + 1;
         ns = st; nl = (uint32_t)(c - st);
         return true;
     }
     return false;
 }
+// (NB: the LF search's 16-byte blocks per step, find_flagged)
 // the value of a line hdr_next_name returned: without the CR before its LF, without leading /
 // trailing spaces (nginx skips ' ' only: a tab is value)
 __device__ __forceinline__ void hdr_value(const uint8_t *A, uint64_t ns, uint64_t c, uint64_t e, uint64_t &vs, uint32_t &vl) {
@@ -250,11 +265,12 @@ __device__ bool hdr_name_is(const uint8_t *A, uint64_t ns, uint32_t nl, const ui
 // ngx_http_variable_unknown_header's first line, ngx_http_parse_multi_header_lines over every
 // Cookie line, ngx_http_arg.  false: no such header / cookie / argument (the value "").  Spans
 // stay in registers: rules_generic keeps them there instead of in a Val (lane-private memory).
+template <int NB = 1>
 __device__ bool span_http(const uint8_t *A, uint64_t hdrs, uint32_t hlen, const uint8_t *nm, uint32_t nml,
                           uint64_t &vo, uint32_t &vl) {
     HdrIt it{hdrs, hdrs + hlen};
     uint64_t ns, c, e; uint32_t nl;
-    while (hdr_next_name(A, it, ns, nl, c, e))
+    while (hdr_next_name<NB>(A, it, ns, nl, c, e))
         if (hdr_name_is(A, ns, nl, nm, nml)) { hdr_value(A, ns, c, e, vo, vl); return true; }
     return false;
 }
@@ -284,12 +300,13 @@ __device__ bool cookie_in_line(const uint8_t *A, uint64_t vs, uint32_t l, const 
     }
     return false;
 }
+template <int NB = 1>
 __device__ bool span_cookie(const uint8_t *A, uint64_t hdrs, uint32_t hlen, const uint8_t *nm, uint32_t nml,
                             uint64_t &vo, uint32_t &vl) {
     HdrIt it{hdrs, hdrs + hlen};
     uint64_t ns, vs, c, e; uint32_t nl, l;
     const uint8_t cookie[7] = "cookie";
-    while (hdr_next_name(A, it, ns, nl, c, e)) {
+    while (hdr_next_name<NB>(A, it, ns, nl, c, e)) {
         if (!hdr_name_is(A, ns, nl, cookie, 6)) continue;
         hdr_value(A, ns, c, e, vs, l);
         if (cookie_in_line(A, vs, l, nm, nml, vo, vl)) return true;
@@ -932,6 +949,7 @@ __device__ __noinline__ int server_if_generic(const uint8_t *A, const gm_req *rp
 
 // rules route (compiled map chains) -> result index (0xFF default; -1 a condition read a value the
 // engine cannot know)
+template <int NB>
 __device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, const GTab &t, uint32_t rules_idx,
                                           uint32_t rip) {
 #ifdef GM_EXP_NO_RULES   // measurement build: no conditions (timing only)
@@ -1011,7 +1029,7 @@ __device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, co
                     uint64_t ns, cc, ee;
                     uint32_t nl;
                     const uint8_t cookie[7] = "cookie";
-                    while (left && hdr_next_name(A, it, ns, nl, cc, ee)) {
+                    while (left && hdr_next_name<NB>(A, it, ns, nl, cc, ee)) {
                         const bool is_ck = hdr_name_is(A, ns, nl, cookie, 6);
                         uint64_t lvs = 0;
                         uint32_t lvl = 0;
@@ -1047,8 +1065,8 @@ __device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, co
 #ifdef GM_EXP_RULES_NOSPAN   // measurement build: every header / cookie / argument empty (timing only)
                     if (true) f = false; else
 #endif
-                    if (sr.kind == SRC_HTTP) f = span_http(A, o_hdrs, r.hdr_len, nm, sr.name_len, off, len);
-                    else if (sr.kind == SRC_COOKIE) f = span_cookie(A, o_hdrs, r.hdr_len, nm, sr.name_len, off, len);
+                    if (sr.kind == SRC_HTTP) f = span_http<NB>(A, o_hdrs, r.hdr_len, nm, sr.name_len, off, len);
+                    else if (sr.kind == SRC_COOKIE) f = span_cookie<NB>(A, o_hdrs, r.hdr_len, nm, sr.name_len, off, len);
                     else f = span_arg(A, o_args, r.args_len, nm, sr.name_len, off, len);
                     if (!f) { off = 0; len = 0; }
                     bool put = false;
@@ -1144,14 +1162,14 @@ constexpr uint32_t SLOW_STATUS_WORD = 17;   // batch status word: requests for k
 // (URI <= RLOC_URI_CAP, n_rloc <= RLOC_BM_BITS) sets *pend and returns; >= -1 -- k_rloc's answer
 // (the location index, -1 none).  *sid_out: the server chosen (valid whenever *pend is set).
 constexpr int32_t RK_INLINE = -3, RK_DEFER = -2;
-template <bool FAST = false>
+template <bool FAST = false, bool LONGHOST = true>
 __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
                           RouteOut &o);
 // the request's body length and whether it is chunked, re-read from its record where the 413
 // check needs them (kept in registers across the location walk they cost the route spills)
 __device__ __forceinline__ uint32_t req_body_len(const gm_req *rp) { return reinterpret_cast<const uint32_t *>(rp)[5]; }
 __device__ __forceinline__ bool req_chunked(const gm_req *rp) { return reinterpret_cast<const uint32_t *>(rp)[9] & GM_REQ_CHUNKED; }
-template <bool FAST>
+template <bool FAST, bool LONGHOST>
 __device__ __forceinline__ void route_locphase(const uint8_t *A, const gm_req *rp, const Rec &r, const RoutePre &pre,
                                                const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb,
                                                int32_t rk_in, bool *pend, const DServer &S, uint32_t sid);
@@ -1166,8 +1184,9 @@ __device__ __forceinline__ void too_large(RouteOut &o) {
 // literal host takes the arena-byte path; a request that needs a generic server `if`, the
 // regex-location prefilter or a rules / split route stops with o.slow set, and k_route's SLOW
 // pass (a second launch over the list of such requests) routes it again with the calls.
-// LONGHOST: hosts of 33..64 bytes through the 16-word SWAR path (the route kernels beside the
-// WAF scan, held to GM_ROUTE_WPE waves, leave it out: it spilled them)
+// LONGHOST: hosts of 33..64 bytes through the 16-word SWAR path, and rules_generic's header walks
+// searching 32 bytes a step (the route kernels beside the WAF scan, held to GM_ROUTE_WPE waves,
+// leave both out: they spilled them / cost them a wave)
 template <bool FAST = false, bool LONGHOST = true>
 __device__ __forceinline__ void route_one(const uint8_t *A, uint64_t alen, const gm_req *rp, const Rec &r, const RoutePre &pre,
                           const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb, int32_t rk_in = RK_INLINE,
@@ -1242,13 +1261,13 @@ __device__ __forceinline__ void route_one(const uint8_t *A, uint64_t alen, const
         }
         if (hit) { o.action = is_redirect(f.code) ? GM_ACT_REDIRECT : GM_ACT_RETURN; o.status = f.code; return; }
     }
-    route_locphase<FAST>(A, rp, r, pre, t, h, o, rkb, rk_in, pend, S, sid);
+    route_locphase<FAST, LONGHOST>(A, rp, r, pre, t, h, o, rkb, rk_in, pend, S, sid);
 }
 
 // route_one's location phase: trie walk (exact, longest prefix, auto_redirect), then regex
 // locations, then route_loc.  The first 32 URI bytes come from registers (a window shifted one
 // dword per 4 bytes).
-template <bool FAST>
+template <bool FAST, bool LONGHOST>
 __device__ __forceinline__ void route_locphase(const uint8_t *A, const gm_req *rp, const Rec &r, const RoutePre &pre,
                                                const GTab &t, const HotTabs h, RouteOut &o, const uint32_t *rkb,
                                                int32_t rk_in, bool *pend, const DServer &S, uint32_t sid) {
@@ -1338,7 +1357,7 @@ __device__ __forceinline__ void route_locphase(const uint8_t *A, const gm_req *r
             if (loc < 0) loc = best;
         }
     }
-    route_loc<FAST>(A, rp, t, h, loc, o);
+    route_loc<FAST, LONGHOST>(A, rp, t, h, loc, o);
 }
 
 // The rest of route_one once the location is known (loc < 0: none): location kinds, rules and
@@ -1387,7 +1406,7 @@ __device__ __noinline__ int access_eval(const uint8_t *A, const gm_req *rp, cons
     return 0;
 }
 
-template <bool FAST>
+template <bool FAST, bool LONGHOST>
 __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, const GTab &t, const HotTabs h, int32_t loc,
                           RouteOut &o) {
     const uint32_t blen = req_body_len(rp);
@@ -1410,7 +1429,7 @@ __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, co
     if (FAST && (L.kind == LK_IRL_RULES || L.kind == LK_IRL_SPLIT || L.access != GM_NONE)) { o.slow = 1; return; }
     if (L.kind == LK_IRL_RULES) {
         const DRules R = t.rules[L.route];
-        const int idx = rules_generic(A, rp, *t.self, L.route, h.servers[o.server].realip);
+        const int idx = rules_generic<LONGHOST ? 2 : 1>(A, rp, *t.self, L.route, h.servers[o.server].realip);
         o.kind = GM_ROUTE_RULES;
         if (idx < 0) { o.action = GM_ACT_UNSUPPORTED; return; }
         o.match = (uint8_t)idx;
@@ -1552,7 +1571,7 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
             if (loc < 0) loc = q.best[x];
             o.server = e.y; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0; o.action = GM_ACT_NO_LISTENER;
             o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF; o.pend_best = -1; o.slow = 0;
-            route_loc(A, reqs + i, t, h, loc, o);
+            route_loc<false, (WPE < GM_ROUTE_WPE_SHIPPED)>(A, reqs + i, t, h, loc, o);
         } else {
             if (SLOW) i = q.list[x].x;
             r = load_rec(reqs + i);
