@@ -1024,27 +1024,36 @@ __device__ __noinline__ int rules_generic(const uint8_t *A, const gm_req *rp, co
                             n2 = d2.next_true;
                         }
                     }
+                    // line by line, LF first: a wanted name (a $http_ / $cookie_ suffix: no ':')
+                    // of length L names the line iff its first ':' is at st + L, so the ':' probes
+                    // at st + L go out beside the LF search instead of a ':' search before it
+                    // (hdr_next_name's semantics; one dependent search per line instead of two)
                     uint32_t left = np;
-                    HdrIt it{o_hdrs, o_hdrs + r.hdr_len};
-                    uint64_t ns, cc, ee;
-                    uint32_t nl;
+                    const uint64_t he = o_hdrs + r.hdr_len;
                     const uint8_t cookie[7] = "cookie";
-                    while (left && hdr_next_name<NB>(A, it, ns, nl, cc, ee)) {
-                        const bool is_ck = hdr_name_is(A, ns, nl, cookie, 6);
+                    for (uint64_t st = o_hdrs; left && st < he;) {
+                        const bool ck = st + 6 < he && A[st + 6] == ':';
+                        bool cq[MEMO];
+#pragma unroll
+                        for (int q = 0; q < MEMO; q++)
+                            cq[q] = !pf[q] && ps[q] != GM_NONE && pk[q] == SRC_HTTP && st + pl[q] < he && A[st + pl[q]] == ':';
+                        const uint64_t e = find_byte<NB>(A, st, he, '\n');
+                        const bool is_ck = ck && st + 6 < e && hdr_name_is(A, st, 6, cookie, 6);
                         uint64_t lvs = 0;
                         uint32_t lvl = 0;
-                        if (is_ck) hdr_value(A, ns, cc, ee, lvs, lvl);
+                        if (is_ck) hdr_value(A, st, st + 6, e, lvs, lvl);
 #pragma unroll
                         for (int q = 0; q < MEMO; q++) {
                             if (pf[q] || ps[q] == GM_NONE) continue;
                             if (pk[q] == SRC_HTTP) {
-                                if (hdr_name_is(A, ns, nl, pn[q], pl[q])) {
-                                    hdr_value(A, ns, cc, ee, po[q], pv[q]); pf[q] = true; left--;
+                                if (cq[q] && st + pl[q] < e && hdr_name_is(A, st, pl[q], pn[q], pl[q])) {
+                                    hdr_value(A, st, st + pl[q], e, po[q], pv[q]); pf[q] = true; left--;
                                 }
                             } else if (is_ck && cookie_in_line(A, lvs, lvl, pn[q], pl[q], po[q], pv[q])) {
                                 pf[q] = true; left--;
                             }
                         }
+                        st = e + 1;
                     }
                     // into the memo (not found: the empty value)
 #pragma unroll

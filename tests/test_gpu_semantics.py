@@ -171,12 +171,12 @@ def test_rules_route_many_chains(eng):
 
 
 def test_rules_header_cookie_arg_spans(eng):
-    """The SLOW pass's span pre-pass (k_rule_spans: a wave per request over its header block staged
-    in LDS) against the oracle's walks: a header condition (name case and '-' / '_' variants,
-    repeated lines -- the first wins --, spaces around values, CR-less and colon-less lines), a
-    cookie condition over 0-3 Cookie lines (look-alike names, ',' and ';' separators, spaces around
-    '='), an argument condition; plus requests past the pre-pass's limits (> 255 header lines,
-    > 4 KiB of headers, > 16 Cookie lines) that rules_generic walks itself."""
+    """rules_generic's header / cookie / argument spans (its one LF-first header walk for every
+    header and cookie source of the route) against the oracle's walks: a header condition (name case
+    and '-' / '_' variants, repeated lines -- the first wins --, spaces around values, CR-less and
+    colon-less lines, a ':' inside a name of the wanted length), a cookie condition over 0-3 Cookie
+    lines (look-alike names, a "Cook:e" line, ',' and ';' separators, spaces around '='), an
+    argument condition; long blocks (300 lines, 5 KiB values, 20 Cookie lines)."""
     rng = np.random.Generator(np.random.PCG64(41))
     ups = [{"name": f"u{k}", "service": f"svc{k}", "port": 80} for k in range(5)]
     vs = {"metadata": {"name": "sp", "namespace": "default"},
@@ -190,7 +190,7 @@ def test_rules_header_cookie_arg_spans(eng):
                        "defaultUpstream": "u0"}}]}}
     b = SC._vs_blob(vs)
     vals = ["v1", "v2", "v3", "V1", "x", ""]
-    names = ["X-Ab-C", "x-ab-c", "X_AB_C", "X-Ab-Cd", "X-Ab"]
+    names = ["X-Ab-C", "x-ab-c", "X_AB_C", "X-Ab-Cd", "X-Ab", "X:Ab-C"]
     ck_tok = ["sess=v1", "sess=v2", " sess = v3", "sess2=v1", "SESS=v2", "xsess=v1", "sess", "a=b", "sess=v3;x"]
     args = ["q=v1", "q=v2", "Q=v3", "aq=v1", "q=", "q", "x=1&q=v2", "q=v3&q=v1", "&q=v1"]
     items = []
@@ -207,12 +207,16 @@ def test_rules_header_cookie_arg_spans(eng):
         u = rng.random()
         if u < 0.05:
             hdrs.append(("X-Raw", "a\nNoColonLine"))          # a line without ':' (bare LF)
+        elif u < 0.065:
+            hdrs.insert(0, ("X-Raw", "a\nX-Ab-C\r"))          # the wanted name on a colon-less line
         elif u < 0.08:
-            hdrs += [("X-H", "1")] * 300                      # > 255 lines: the walk
+            hdrs.insert(0, ("Cook:e", "sess=v2"))              # "cookie"'s length, a ':' inside
+        elif u < 0.09:
+            hdrs += [("X-H", "1")] * 300                      # 300 lines
         elif u < 0.10:
-            hdrs.append(("X-Big", "b" * 5000))                 # > 4 KiB: the walk
+            hdrs.append(("X-Big", "b" * 5000))                 # a 5 KiB value
         elif u < 0.12:
-            hdrs += [("Cookie", "k=v")] * 20                   # > 16 Cookie lines: the walk
+            hdrs += [("Cookie", "k=v")] * 20                   # 20 Cookie lines
         a = "&".join(args[int(t)] for t in rng.integers(0, len(args), int(rng.integers(0, 3))))
         items.append({"host": "sp.example.com", "uri": "/", "args": a, "headers": hdrs})
     v = _both(eng, b, items)
