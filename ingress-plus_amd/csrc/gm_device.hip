@@ -2594,6 +2594,12 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
 #ifndef GM_SLOW_WPE
 #define GM_SLOW_WPE 3   // the SLOW route pass's waves per SIMD target (its header walks are latency-bound)
 #endif
+#ifndef GM_SOLO_WPE
+// the FAST route pass's waves per SIMD target without a WAF phase (C1 / C2 / C5).  Measured (round 6,
+// ms per 10M): 4 -> C2 4.89 / C1 0.490 / C5 1.317 against 4.90 / 0.491 / 1.331 at 3 (noise); 5 -> C1
+// 0.477 but C2 5.28 (no 16-word long-host path at 5) and C5 1.348
+#define GM_SOLO_WPE 3
+#endif
     const uint32_t route_blocks = std::max<uint32_t>(1, std::min<uint32_t>((n + ROUTE_BLOCK - 1) / ROUTE_BLOCK,
                                                                            (uint32_t)c->cu_count * GM_EXP_GRIDMUL));
     unsigned long long *ctr = S->d_bctr;
@@ -2685,7 +2691,7 @@ static int run_batch(gm_ctx *c, Scratch *S, const Generation *g, const gm_req *r
     if (!waf) {
         if (rk) GM_ROUTE_LAUNCH(3, true, false, route_blocks, route_lds(t, false), s, reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), q);
         else {
-            GM_ROUTE_LAUNCH(3, false, false, route_blocks, route_lds(t, false), s, reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), qs);
+            GM_ROUTE_LAUNCH(GM_SOLO_WPE, false, false, route_blocks, route_lds(t, false), s, reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), qs);
             HIPCHK(c, hipGetLastError());
             k_route<GM_SLOW_WPE, false, false, true><<<route_blocks, ROUTE_BLOCK, route_lds(t, false), s>>>(
                 reqs, n, A, alen, t, out, ctr, nullptr, nblk, nullptr, 0, dlen, route_hist_n(t, false), qs);
@@ -3915,7 +3921,7 @@ static constexpr uint32_t kBuildFlags =
     GM_ROUTE_BPC != 1 || GM_ROUTE_PRIO != 0 || GM_ROUTE_WPE != GM_ROUTE_WPE_SHIPPED || GM_EXP_GRIDMUL != 8 || \
     GM_EXP_WPE != 3 || GM_RLOC_CTX != 1 || GM_RLOC_PREF != 0 || GM_ALW_SLICE_GROUPS != 8 || GM_WIRE_WPE != 6 || \
     GM_WIRE_WPE_EMIT != GM_WIRE_WPE || GM_WIRE_CANON != 1 || GM_EXACT_BPC != 6 || !defined(GM_DFA_INL_SHIPPED) || \
-    GM_SLOW_WPE != 3
+    GM_SLOW_WPE != 3 || GM_SOLO_WPE != 3
     GM_BUILD_TUNING |
 #endif
     0u;
