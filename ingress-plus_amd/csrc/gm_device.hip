@@ -1435,7 +1435,8 @@ __device__ __forceinline__ void route_loc(const uint8_t *A, const gm_req *rp, co
     DLoc L = h.locs[loc];
     if (!chunked && blen > L.body_max) { too_large(o); return; }
     uint32_t fin = (uint32_t)loc;
-    if (FAST && (L.kind == LK_IRL_RULES || L.kind == LK_IRL_SPLIT || L.access != GM_NONE)) { o.slow = 1; return; }
+    // (2: stopped with the server and the location known -- k_route's SLOW pass resumes here)
+    if (FAST && (L.kind == LK_IRL_RULES || L.kind == LK_IRL_SPLIT || L.access != GM_NONE)) { o.slow = 2; return; }
     if (L.kind == LK_IRL_RULES) {
         const DRules R = t.rules[L.route];
         const int idx = rules_generic<LONGHOST ? 2 : 1>(A, rp, *t.self, L.route, h.servers[o.server].realip);
@@ -1582,11 +1583,21 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
             o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF; o.waf = GM_WAF_OFF; o.pend_best = -1; o.slow = 0;
             route_loc<false, (WPE < GM_ROUTE_WPE_SHIPPED)>(A, reqs + i, t, h, loc, o);
         } else {
-            if (SLOW) i = q.list[x].x;
-            r = load_rec(reqs + i);
-            route_prefetch(A, arena_len, r, pre);
-            route_one<FASTK, (WPE < GM_ROUTE_WPE_SHIPPED)>(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
-                             RK && q.list ? RK_DEFER : RK_INLINE, &pend);
+            uint32_t rsm = 0;
+            if (SLOW) { const uint2 e = q.list[x]; i = e.x; rsm = e.y; }
+            if (SLOW && rsm) {
+                // the first pass stopped in route_loc (a rules / split location, an access list):
+                // the server and location it found, only the location's own step again
+                o.server = (rsm >> 16) & 0x7FFFu; o.loc = GM_NONE; o.ups = GM_NONE; o.status = 0;
+                o.action = GM_ACT_NO_LISTENER; o.kind = GM_ROUTE_NONE; o.bucket = 0xFF; o.match = 0xFF;
+                o.waf = GM_WAF_OFF; o.pend_best = -1; o.slow = 0;
+                route_loc<false, (WPE < GM_ROUTE_WPE_SHIPPED)>(A, reqs + i, t, h, (int32_t)(rsm & 0xFFFFu), o);
+            } else {
+                r = load_rec(reqs + i);
+                route_prefetch(A, arena_len, r, pre);
+                route_one<FASTK, (WPE < GM_ROUTE_WPE_SHIPPED)>(A, arena_len, reqs + i, r, pre, t, h, o, RK ? rkb : nullptr,
+                                 RK && q.list ? RK_DEFER : RK_INLINE, &pend);
+            }
         }
         const bool slow = FASTK && o.slow;
         if (FASTK) {   // to the SLOW pass, one atomic per wave
@@ -1597,7 +1608,10 @@ __global__ __launch_bounds__(ROUTE_BLOCK) __attribute__((amdgpu_waves_per_eu(WPE
                 uint32_t b = 0;
                 if (lane == (uint32_t)leader) b = atomicAdd(q.count, (uint32_t)__popcll(sm));
                 b = __shfl(b, leader);
-                if (slow) q.list[b + (uint32_t)__popcll(sm & ((1ull << lane) - 1))] = make_uint2(i, 0u);
+                // (server, location) | bit 31 when the SLOW pass can resume at route_loc, else 0
+                const uint32_t rsm = o.slow == 2 && o.server < 0x8000u && o.loc < 0x10000u
+                                         ? 0x80000000u | (o.server << 16) | o.loc : 0u;
+                if (slow) q.list[b + (uint32_t)__popcll(sm & ((1ull << lane) - 1))] = make_uint2(i, rsm);
             }
         }
         const uint32_t cloc = slow ? GM_NONE : o.loc;   // (counted by the SLOW pass)
